@@ -1,0 +1,283 @@
+// rt_abi.cpp — C-ABI entry points of librt_hip.so (declared in include/rt_abi.h).
+//
+// Replaces the render-world half of the reference's plugin (src/lib.rs):
+//   ComputeShaderPipeline::from_world (240-324)  -> rt_create (code objects are linked in)
+//   prepare_sphere_buffer (177-207)              -> sphere upload, only when bytes change
+//   prepare_camera_bind_group (151-175)          -> camera passed by value as kernarg
+//   ComputeShaderNode::run (379-421)             -> rt_init_image / rt_update launches
+// Errors are status codes instead of panics/unwraps (lib.rs:216-217, 356-358, 399-411).
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rt_abi.h"
+#include "rt_kernels.h"
+
+struct rt_ctx {
+    int device = 0;
+    float4* d_geom = nullptr;  // count x (cx, cy, cz, r*r)
+    float4* d_sph = nullptr;   // count x 2 float4 (the 32-B GpuSphere records)
+    uint32_t capacity = 0;
+    uint32_t count = 0;
+    bool valid = false;
+    std::vector<rt_sphere> cached;  // bytes currently on the device
+};
+
+namespace {
+
+thread_local std::string g_last_error = "";
+
+rt_status fail(rt_status s, const std::string& msg) {
+    g_last_error = msg;
+    return s;
+}
+
+rt_status hip_fail(hipError_t e, const char* what) {
+    return fail(RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Switches to the context's device for the duration of a call.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+constexpr uint32_t kMaxDim = 1u << 16;         // 65536 x 65536 texels
+constexpr uint32_t kMaxSpheres = 1u << 20;
+
+rt_status check_image(uint32_t w, uint32_t h) {
+    if (w == 0 || h == 0 || w > kMaxDim || h > kMaxDim)
+        return fail(RT_ERR_INVALID_SIZE, "image size out of range (1..65536 per side)");
+    return RT_OK;
+}
+
+rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
+                         hipStream_t stream) {
+    if (count > kMaxSpheres) return fail(RT_ERR_INVALID_SIZE, "sphere_count too large");
+    if (count > 0 && spheres == nullptr)
+        return fail(RT_ERR_INVALID_ARGUMENT, "spheres is NULL with sphere_count > 0");
+    if (ctx->valid && count == ctx->count &&
+        (count == 0 || std::memcmp(ctx->cached.data(), spheres, count * sizeof(rt_sphere)) == 0))
+        return RT_OK;  // unchanged since the last upload
+    if (count > ctx->capacity) {
+        uint32_t cap = ctx->capacity ? ctx->capacity : 64u;
+        while (cap < count) cap *= 2u;
+        float4 *g = nullptr, *s = nullptr;
+        hipError_t e = hipMalloc(&g, (size_t)cap * sizeof(float4));
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(sphere geometry)");
+        e = hipMalloc(&s, (size_t)cap * 2 * sizeof(float4));
+        if (e != hipSuccess) {
+            (void)hipFree(g);
+            return hip_fail(e, "hipMalloc(sphere records)");
+        }
+        // The previous buffers may still be read by queued launches on `stream`.
+        if (ctx->d_geom || ctx->d_sph) {
+            e = hipStreamSynchronize(stream);
+            if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+            (void)hipFree(ctx->d_geom);
+            (void)hipFree(ctx->d_sph);
+        }
+        ctx->d_geom = g;
+        ctx->d_sph = s;
+        ctx->capacity = cap;
+    }
+    if (count > 0) {
+        // Scan record: center + radius^2.  r*r is one IEEE f32 multiply, bit-identical to
+        // the shader's `sphere.radius * sphere.radius` (wgsl:186).
+        std::vector<float4> geom(count);
+        for (uint32_t i = 0; i < count; ++i) {
+            const rt_sphere& s = spheres[i];
+            geom[i] = make_float4(s.position[0], s.position[1], s.position[2],
+                                  s.radius * s.radius);
+        }
+        // Queued launches may still read the old scene: order the copies on the stream,
+        // and wait for them so the host staging vectors can be released.
+        hipError_t e = hipMemcpyAsync(ctx->d_geom, geom.data(), count * sizeof(float4),
+                                      hipMemcpyHostToDevice, stream);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(sphere geometry)");
+        e = hipMemcpyAsync(ctx->d_sph, spheres, count * sizeof(rt_sphere),
+                           hipMemcpyHostToDevice, stream);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(sphere records)");
+        e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    }
+    ctx->cached.assign(spheres, spheres + count);
+    ctx->count = count;
+    ctx->valid = true;
+    return RT_OK;
+}
+
+void fill_camera(rtk::TraceParams& p, const rt_scene_camera& c) {
+    for (int i = 0; i < 3; ++i) {
+        p.center[i] = c.center[i];
+        p.vul[i] = c.viewport_upper_left[i];
+        p.pdu[i] = c.pixel_delta_u[i];
+        p.pdv[i] = c.pixel_delta_v[i];
+        p.ddu[i] = c.defocus_disk_u[i];
+        p.ddv[i] = c.defocus_disk_v[i];
+    }
+    p.defocus_angle = c.defocus_angle;
+    p.max_depth = c.max_depth;
+    p.spp = c.samples_per_pixel;
+}
+
+// Shared body of rt_update / rt_render / rt_render_stripes.
+rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h,
+                uint32_t rank, uint32_t nranks, const rt_scene_camera* cam,
+                const rt_sphere* spheres, uint32_t count, uint32_t frames,
+                const float* seeds, void* stream_v) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!in || !out || !cam) return fail(RT_ERR_INVALID_ARGUMENT, "NULL image or camera");
+    if (rt_status s = check_image(w, h)) return s;
+    if (nranks == 0 || rank >= nranks) return fail(RT_ERR_INVALID_ARGUMENT, "bad rank/nranks");
+    if (frames == 0) return RT_OK;
+    if (!seeds) return fail(RT_ERR_INVALID_ARGUMENT, "random_seeds is NULL");
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    hipStream_t stream = static_cast<hipStream_t>(stream_v);
+    if (rt_status s = upload_spheres(ctx, spheres, count, stream)) return s;
+
+    const uint32_t bands = (h + RT_STRIPE_ROWS - 1) / RT_STRIPE_ROWS;
+    rtk::TraceParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.geom = ctx->d_geom;
+    p.sph = ctx->d_sph;
+    p.width = w;
+    p.height = h;
+    p.count = count;
+    p.band_first = rank;
+    p.band_step = nranks;
+    p.local_bands = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
+    fill_camera(p, *cam);
+    const float4* src = reinterpret_cast<const float4*>(in);
+    float4* dst = reinterpret_cast<float4*>(out);
+    for (uint32_t f0 = 0; f0 < frames; f0 += rtk::kMaxFramesPerLaunch) {
+        const uint32_t nf = std::min<uint32_t>(frames - f0, rtk::kMaxFramesPerLaunch);
+        p.in = src;
+        p.out = dst;
+        p.frames = nf;
+        p.reset_first = (f0 == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
+        std::memcpy(p.seeds, seeds + f0, nf * sizeof(float));
+        hipError_t e = rtk::launch_trace(p, stream);
+        if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
+        src = dst;  // later launches continue the accumulation in place
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char* rt_last_error(void) { return g_last_error.c_str(); }
+
+const char* rt_kernel_name(int which) {
+    (void)which;
+    return rtk::trace_kernel_name();
+}
+
+rt_status rt_create(int device, rt_ctx** out_ctx) {
+    if (!out_ctx) return fail(RT_ERR_INVALID_ARGUMENT, "out_ctx is NULL");
+    *out_ctx = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+    if (device < 0 || device >= n) return fail(RT_ERR_INVALID_DEVICE, "no such HIP device");
+    rt_ctx* ctx = new (std::nothrow) rt_ctx();
+    if (!ctx) return fail(RT_ERR_NO_MEMORY, "out of host memory");
+    ctx->device = device;
+    *out_ctx = ctx;
+    return RT_OK;
+}
+
+rt_status rt_destroy(rt_ctx* ctx) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    {
+        DeviceGuard guard(ctx->device);
+        if (ctx->d_geom || ctx->d_sph) (void)hipDeviceSynchronize();
+        (void)hipFree(ctx->d_geom);
+        (void)hipFree(ctx->d_sph);
+    }
+    delete ctx;
+    return RT_OK;
+}
+
+rt_status rt_set_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count, void* stream) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    return upload_spheres(ctx, spheres, count, static_cast<hipStream_t>(stream));
+}
+
+rt_status rt_init_image(rt_ctx* ctx, float* out, uint32_t w, uint32_t h, void* stream) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!out) return fail(RT_ERR_INVALID_ARGUMENT, "out_rgba is NULL");
+    if (rt_status s = check_image(w, h)) return s;
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    hipError_t e = rtk::launch_init(reinterpret_cast<float4*>(out), (uint64_t)w * h,
+                                    static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? RT_OK : hip_fail(e, "rt_init_kernel launch");
+}
+
+rt_status rt_update(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h,
+                    const rt_scene_camera* cam, const rt_sphere* spheres, uint32_t count,
+                    void* stream) {
+    if (in != nullptr && in == out)
+        return fail(RT_ERR_INVALID_ARGUMENT, "rt_update: in and out must not alias");
+    if (!cam) return fail(RT_ERR_INVALID_ARGUMENT, "camera is NULL");
+    const float seed = cam->random_seed;
+    return trace(ctx, in, out, w, h, 0, 1, cam, spheres, count, 1, &seed, stream);
+}
+
+rt_status rt_render(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h,
+                    const rt_scene_camera* cam, const rt_sphere* spheres, uint32_t count,
+                    uint32_t frames, const float* seeds, void* stream) {
+    return trace(ctx, in, out, w, h, 0, 1, cam, spheres, count, frames, seeds, stream);
+}
+
+uint32_t rt_stripe_local_rows(uint32_t height, uint32_t rank, uint32_t nranks) {
+    if (nranks == 0 || rank >= nranks) return 0;
+    const uint32_t bands = (height + RT_STRIPE_ROWS - 1) / RT_STRIPE_ROWS;
+    const uint32_t local = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
+    return local * RT_STRIPE_ROWS;
+}
+
+rt_status rt_render_stripes(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h,
+                            uint32_t rank, uint32_t nranks, const rt_scene_camera* cam,
+                            const rt_sphere* spheres, uint32_t count, uint32_t frames,
+                            const float* seeds, void* stream) {
+    return trace(ctx, in, out, w, h, rank, nranks, cam, spheres, count, frames, seeds, stream);
+}
+
+rt_status rt_deinterleave_stripes(rt_ctx* ctx, const float* gathered, float* out, uint32_t w,
+                                  uint32_t h, uint32_t nranks, void* stream) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!gathered || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (gathered == out) return fail(RT_ERR_INVALID_ARGUMENT, "gathered and out alias");
+    if (nranks == 0) return fail(RT_ERR_INVALID_ARGUMENT, "nranks is 0");
+    if (rt_status s = check_image(w, h)) return s;
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    hipError_t e = rtk::launch_deinterleave(
+        reinterpret_cast<const float4*>(gathered), reinterpret_cast<float4*>(out), w, h,
+        nranks, rt_stripe_local_rows(h, 0, nranks), static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? RT_OK : hip_fail(e, "rt_deinterleave_kernel launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+// rt_device.h — device-side restatement of the reference shader's per-pixel math
+// (assets/compute_shader.wgsl) for gfx950, under the canonical float semantics of
+// DESIGN.md §3 (explicit fmaf, IEEE sqrt/div, fixed sin/cos polynomial).  Compiled with
+// -ffp-contract=off so that no other fusion happens: the image is bit-identical to the
+// CPU oracle's.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtd {
+
+struct v3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ v3 mk(float x, float y, float z) { return v3{x, y, z}; }
+__device__ __forceinline__ v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ v3 mul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ v3 divs(v3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+// p + s*q (contracted)
+__device__ __forceinline__ v3 fmas(float s, v3 q, v3 p) {
+    return mk(fmaf(s, q.x, p.x), fmaf(s, q.y, p.y), fmaf(s, q.z, p.z));
+}
+__device__ __forceinline__ float dot(v3 a, v3 b) {
+    return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x));
+}
+__device__ __forceinline__ v3 normalize(v3 v) { return divs(v, sqrtf(dot(v, v))); }
+
+// wgsl:50-59.  Three v_mul_lo_u32 (quarter rate) — the RNG's cost per call.
+__device__ __forceinline__ uint32_t hash(uint32_t s) {
+    s ^= 2747636419u;
+    s *= 2654435769u;
+    s ^= s >> 16;
+    s *= 2654435769u;
+    s ^= s >> 16;
+    s *= 2654435769u;
+    return s;
+}
+// wgsl:61-63: f32(hash) / 4294967295.0 where the literal rounds to 2^32 in f32.
+__device__ __forceinline__ float rf(uint32_t v) { return (float)hash(v) * 0x1p-32f; }
+
+// WGSL u32(f32): truncate, saturate, NaN -> 0 (what v_cvt_u32_f32 does).
+__device__ __forceinline__ uint32_t f2u(float f) {
+    if (!(f > 0.0f)) return 0u;
+    if (f >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)f;
+}
+
+// Canonical sin/cos: Cody-Waite by pi/2 in three parts, Cephes minimax.
+__device__ __forceinline__ void sincos_c(float x, float& s, float& c) {
+    const float q = rintf(x * 0x1.45f306p-1f);
+    const int k = (q == q) ? (int)q : 0;
+    float r = fmaf(q, -0x1.921fb6p+0f, x);
+    r = fmaf(q, 0x1.777a5cp-25f, r);
+    r = fmaf(q, 0x1p-49f, r);
+    const float r2 = r * r;
+    const float ps = fmaf(fmaf(-0x1.9943f2p-13f, r2, 0x1.11073cp-7f), r2, -0x1.555546p-3f);
+    const float sr = fmaf(r * r2, ps, r);
+    const float pc = fmaf(fmaf(0x1.99eb9cp-16f, r2, -0x1.6c0c34p-10f), r2, 0x1.55554ap-5f);
+    const float cr = fmaf(r2 * r2, pc, fmaf(-0.5f, r2, 1.0f));
+    const bool swap = (k & 1) != 0;
+    const float s0 = swap ? cr : sr;
+    const float c0 = swap ? sr : cr;
+    s = (k & 2) ? -s0 : s0;
+    c = ((k + 1) & 2) ? -c0 : c0;
+}
+
+// wgsl:234-243
+__device__ __forceinline__ v3 random_unit_vector(uint32_t seed) {
+    const float z = fmaf(2.0f, rf(seed), -1.0f);
+    const float a = rf(seed + 1u) * 0x1.921fb6p+2f;  // 6.283185307 as f32
+    const float r = sqrtf(fmaf(-z, z, 1.0f));
+    float sa, ca;
+    sincos_c(a, sa, ca);
+    return mk(r * ca, r * sa, z);
+}
+
+// WGSL reflect(e1,e2) = e1 - 2*dot(e2,e1)*e2
+__device__ __forceinline__ v3 reflect(v3 e1, v3 e2) {
+    const float k = 2.0f * dot(e2, e1);
+    return fmas(-k, e2, e1);
+}
+
+// WGSL refract(e1,e2,eta)
+__device__ __forceinline__ v3 refract(v3 e1, v3 e2, float eta) {
+    const float d = dot(e2, e1);
+    const float k = fmaf(-(eta * eta), fmaf(-d, d, 1.0f), 1.0f);
+    if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
+    const float m = fmaf(eta, d, sqrtf(k));
+    return mk(fmaf(eta, e1.x, -(m * e2.x)), fmaf(eta, e1.y, -(m * e2.y)),
+              fmaf(eta, e1.z, -(m * e2.z)));
+}
+
+// wgsl:137-141, pow(x, 5.0) = ((x*x)*(x*x))*x
+__device__ __forceinline__ float reflectance(float cos_t, float ri) {
+    float r0 = (1.0f - ri) / (1.0f + ri);
+    r0 = r0 * r0;
+    const float x = 1.0f - cos_t;
+    const float x2 = x * x;
+    return fmaf(1.0f - r0, (x2 * x2) * x, r0);
+}
+
+}  // namespace rtd

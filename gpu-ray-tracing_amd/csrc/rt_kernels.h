@@ -1,0 +1,38 @@
+// rt_kernels.h — launch interface between the C-ABI layer (rt_abi.cpp) and the HIP
+// kernels (rt_kernels.hip).  Internal; not part of the public boundary.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include "rt_abi.h"
+
+namespace rtk {
+
+// Seeds travel in the kernarg segment (no H2D copy, graph-capturable).  rt_render with
+// more frames is split into several launches that continue the accumulation.
+constexpr uint32_t kMaxFramesPerLaunch = 128;
+
+// Everything the `update` kernel needs, passed by value (kernarg -> SGPRs).
+struct TraceParams {
+    const float4* in;    // local image (compact stripes), row pitch = width
+    float4* out;
+    const float4* geom;  // per sphere: (cx, cy, cz, r*r) — the scan's 16-B record
+    const float4* sph;   // per sphere: the 32-B GpuSphere as two float4 (pos+r, color)
+    uint32_t width, height, count;
+    uint32_t band_first, band_step, local_bands;  // stripe map (RT_STRIPE_ROWS rows/band)
+    uint32_t frames;       // accumulation frames in this launch (1 = one `update`)
+    uint32_t reset_first;  // camera_has_moved > 0.5 applies to frame 0 only
+    float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3];
+    float defocus_angle, max_depth, spp;
+    float seeds[kMaxFramesPerLaunch];
+};
+
+hipError_t launch_trace(const TraceParams& p, hipStream_t stream);
+hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream);
+hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t width,
+                               uint32_t height, uint32_t nranks, uint32_t max_local_rows,
+                               hipStream_t stream);
+const char* trace_kernel_name();
+
+}  // namespace rtk

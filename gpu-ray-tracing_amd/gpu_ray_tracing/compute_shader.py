@@ -1,0 +1,184 @@
+"""The compute-shader plugin surface (src/lib.rs), bound to the HIP kernels.
+
+Reference -> here:
+  ComputeShaderPipeline::from_world (lib.rs:240-324)   -> ComputeShaderPipeline(device)
+  ComputeShaderImages {texture_a, texture_b} (138-142)  -> ComputeShaderImages
+  `init` dispatch (lib.rs:398-407, wgsl:65-70)          -> ComputeShaderPipeline.init_image
+  `update` dispatch (lib.rs:408-417, wgsl:333-364)      -> ComputeShaderPipeline.update
+  ComputeShaderNode state machine (lib.rs:326-421)      -> ComputeShaderNode (C++ driver)
+Extensions the reference lacks: fused multi-frame accumulation (``render``), the stripe
+partition for multi-GPU (``render_stripes`` / ``deinterleave``).
+
+Images are torch float32 tensors of shape (H, W, 4) on the pipeline's device (RGBA32F,
+row-major, alpha = sample count).  Every call is enqueued on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .camera import SceneCamera
+from .scene import SphereCollection
+
+RT_STRIPE_ROWS = _lib.RT_STRIPE_ROWS
+
+
+def _ptr(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _check_image(t: torch.Tensor, width: int, height: int, name: str) -> None:
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise ValueError(f"{name} must be a CUDA (HIP) tensor")
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous float32")
+    if t.numel() < width * height * 4:
+        raise ValueError(f"{name} holds {t.numel()} floats, need {width * height * 4}")
+
+
+def stripe_local_rows(height: int, rank: int, nranks: int) -> int:
+    return int(_lib.lib().rt_stripe_local_rows(height, rank, nranks))
+
+
+class ComputeShaderPipeline:
+    """One librt_hip.so context on one HIP device (lib.rs:231-324)."""
+
+    def __init__(self, device: int | torch.device = 0):
+        if isinstance(device, torch.device):
+            device = device.index if device.index is not None else torch.cuda.current_device()
+        self.device = int(device)
+        self.torch_device = torch.device("cuda", self.device)
+        ctx = ctypes.c_void_p()
+        _lib.call("rt_create", self.device, ctypes.byref(ctx))
+        self._ctx = ctx
+        self._sphere_keep = None
+
+    # ---- lifetime ---------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            _lib.call("rt_destroy", self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- helpers ----------------------------------------------------------------------
+    def _stream(self) -> ctypes.c_void_p:
+        return ctypes.c_void_p(torch.cuda.current_stream(self.torch_device).cuda_stream)
+
+    def _spheres(self, spheres: SphereCollection):
+        arr = np.ascontiguousarray(spheres.spheres, np.float32)
+        self._sphere_keep = arr
+        return arr.ctypes.data_as(ctypes.c_void_p), arr.shape[0]
+
+    def new_image(self, width: int, height: int) -> torch.Tensor:
+        return torch.zeros((height, width, 4), dtype=torch.float32, device=self.torch_device)
+
+    # ---- the plugin operations --------------------------------------------------------
+    def set_spheres(self, spheres: SphereCollection) -> None:
+        p, n = self._spheres(spheres)
+        _lib.call("rt_set_spheres", self._ctx, p, n, self._stream())
+
+    def init_image(self, out: torch.Tensor, width: int, height: int) -> None:
+        _check_image(out, width, height, "out")
+        _lib.call("rt_init_image", self._ctx, _ptr(out), width, height, self._stream())
+
+    def update(self, inp: torch.Tensor, out: torch.Tensor, width: int, height: int,
+               camera: SceneCamera, spheres: SphereCollection) -> None:
+        _check_image(inp, width, height, "in")
+        _check_image(out, width, height, "out")
+        cam = camera.to_c()
+        p, n = self._spheres(spheres)
+        _lib.call("rt_update", self._ctx, _ptr(inp), _ptr(out), width, height,
+                  ctypes.byref(cam), p, n, self._stream())
+
+    def render(self, inp: torch.Tensor, out: torch.Tensor, width: int, height: int,
+               camera: SceneCamera, spheres: SphereCollection, seeds) -> None:
+        _check_image(inp, width, height, "in")
+        _check_image(out, width, height, "out")
+        cam = camera.to_c()
+        p, n = self._spheres(spheres)
+        s = np.ascontiguousarray(seeds, np.float32)
+        _lib.call("rt_render", self._ctx, _ptr(inp), _ptr(out), width, height,
+                  ctypes.byref(cam), p, n, s.size, s.ctypes.data_as(ctypes.c_void_p),
+                  self._stream())
+
+    def render_stripes(self, inp: torch.Tensor, out: torch.Tensor, width: int, height: int,
+                       rank: int, nranks: int, camera: SceneCamera,
+                       spheres: SphereCollection, seeds) -> None:
+        rows = stripe_local_rows(height, rank, nranks)
+        _check_image(inp, width, rows, "in")
+        _check_image(out, width, rows, "out")
+        cam = camera.to_c()
+        p, n = self._spheres(spheres)
+        s = np.ascontiguousarray(seeds, np.float32)
+        _lib.call("rt_render_stripes", self._ctx, _ptr(inp), _ptr(out), width, height, rank,
+                  nranks, ctypes.byref(cam), p, n, s.size, s.ctypes.data_as(ctypes.c_void_p),
+                  self._stream())
+
+    def deinterleave(self, gathered: torch.Tensor, out: torch.Tensor, width: int, height: int,
+                     nranks: int) -> None:
+        rows = stripe_local_rows(height, 0, nranks)
+        _check_image(gathered, width, rows * nranks, "gathered")
+        _check_image(out, width, height, "out")
+        _lib.call("rt_deinterleave_stripes", self._ctx, _ptr(gathered), _ptr(out), width,
+                  height, nranks, self._stream())
+
+
+class ComputeShaderImages:
+    """texture_a / texture_b (lib.rs:60-93, 138-142): two zero-filled RGBA32F images."""
+
+    def __init__(self, pipeline: ComputeShaderPipeline, width: int, height: int):
+        self.width, self.height = width, height
+        self.texture_a = pipeline.new_image(width, height)
+        self.texture_b = pipeline.new_image(width, height)
+
+
+class ComputeShaderNode:
+    """Render-graph node (lib.rs:326-421) driving init + ping-pong updates per frame."""
+
+    STATES = {0: "Loading", 1: "Init", 2: "Update(0)", 3: "Update(1)"}
+
+    def __init__(self, pipeline: ComputeShaderPipeline, images: ComputeShaderImages):
+        self.pipeline = pipeline
+        self.images = images
+        drv = ctypes.c_void_p()
+        _lib.call("rt_driver_create", pipeline._ctx, _ptr(images.texture_a),
+                  _ptr(images.texture_b), images.width, images.height, ctypes.byref(drv))
+        self._drv = drv
+
+    @property
+    def state(self) -> str:
+        return self.STATES[_lib.lib().rt_driver_state(self._drv)]
+
+    def frame(self, camera: SceneCamera, spheres: SphereCollection) -> torch.Tensor:
+        """One frame (node.update() + node.run()); returns the image written last."""
+        cam = camera.to_c()
+        p, n = self.pipeline._spheres(spheres)
+        newest = ctypes.c_int(-1)
+        _lib.call("rt_driver_frame", self._drv, ctypes.byref(cam), p, n,
+                  self.pipeline._stream(), ctypes.byref(newest))
+        return self.images.texture_a if newest.value == 0 else self.images.texture_b
+
+    def close(self) -> None:
+        if getattr(self, "_drv", None) and self._drv.value:
+            _lib.call("rt_driver_destroy", self._drv)
+            self._drv = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

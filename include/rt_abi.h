@@ -1,0 +1,224 @@
+/*
+ * rt_abi.h — C-ABI drop-in boundary of the MI355X ray tracer (librt_hip.so).
+ *
+ * Replaces the reference's compute-shader plugin surface for the per-pixel hot path
+ * (Sur091/GPU-Ray-Tracing @ /root/reference):
+ *   - ComputeShaderComputePlugin           src/lib.rs:104-136
+ *   - ComputeShaderPipeline (3 layouts)    src/lib.rs:231-324
+ *   - prepare_* bind-group systems         src/lib.rs:151-229
+ *   - ComputeShaderNode::run dispatch      src/lib.rs:379-421
+ *   - WGSL kernels `init` / `update`       assets/compute_shader.wgsl:65-70, 333-364
+ *
+ * Plain C types only: pointers, sizes, fixed-width integers. No C++ or torch types.
+ * Every function returns an rt_status (0 = ok).
+ *
+ * Data contract (identical to the reference's bind groups):
+ *   group 0  input / output images: RGBA32F, row-major, tightly packed (pitch = width
+ *            texels = width*16 bytes). RGB = running mean, A = sample count
+ *            (wgsl:4-5, 339-341, 362-363).  Device pointers, caller-owned.
+ *   group 1  rt_scene_camera, 176 bytes (wgsl:7-42 == camera.rs:256-291). Host pointer,
+ *            read during the call; passed to the kernel by value (kernarg -> SGPRs).
+ *   group 2  sphere_count + array of rt_sphere, 32-byte stride (wgsl:46-47, 151-155 ==
+ *            sphere.rs:14-26).  Host pointer; uploaded to the device only when its bytes
+ *            change (the reference re-uploads every frame, lib.rs:177-207).
+ *   dispatch one progressive sample per pixel per update (wgsl:352-358).
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__GNUC__)
+#define RT_API __attribute__((visibility("default")))
+#else
+#define RT_API
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------------------ */
+/* Data layouts                                                                          */
+/* ------------------------------------------------------------------------------------ */
+
+/* SceneCamera — camera.rs:256-291 (#[repr(C)], 11 x (Vec3 + f32) = 176 B), wgsl:7-40.
+ * Fields marked "unused" are carried for layout parity only (wgsl "No uses"). */
+typedef struct rt_scene_camera {
+    float center[3];              /*   0  used: ray origin without defocus (wgsl:319) */
+    float viewport_height;        /*  12  unused */
+    float viewport_upper_left[3]; /*  16  used (wgsl:315) */
+    float viewport_width;         /*  28  unused */
+    float pixel_delta_u[3];       /*  32  used (wgsl:316) */
+    float defocus_angle;          /*  44  used: > 0 enables the thin lens (wgsl:319) */
+    float pixel_delta_v[3];       /*  48  used (wgsl:317) */
+    float aspect_ratio;           /*  60  unused */
+    float defocus_disk_u[3];      /*  64  used (wgsl:330) */
+    float _padding0;              /*  76 */
+    float viewport_u[3];          /*  80  unused */
+    float _padding1;              /*  92 */
+    float defocus_disk_v[3];      /*  96  used (wgsl:330) */
+    float max_depth;              /* 108  used: bounce limit, u32(max_depth) (wgsl:264) */
+    float look_from[3];           /* 112  unused */
+    float samples_per_pixel;      /* 124  used: accumulation cap (wgsl:343,352) */
+    float look_at[3];             /* 128  unused */
+    float camera_has_moved;       /* 140  used: > 0.5 resets the accumulator (wgsl:345) */
+    float vup[3];                 /* 144  unused */
+    float random_seed;            /* 156  used: per-frame seed in [0,1) (wgsl:311,353) */
+    float viewport_v[3];          /* 160  unused */
+    float defocus_radius;         /* 172  unused */
+} rt_scene_camera;
+
+/* GpuSphere — sphere.rs:20-26 (position: Vec3, radius: f32, material.color: Vec4), 32 B,
+ * == WGSL Sphere (wgsl:151-155).  Material type is encoded in color[3] (wgsl:272-284):
+ *   color[3] < -1          Lambertian, albedo = color.rgb
+ *   -1 <= color[3] <= 1    metal, albedo = color.rgb, fuzz = color[3]
+ *   color[3] > 1           dielectric, refraction index = color[0]                      */
+typedef struct rt_sphere {
+    float position[3];
+    float radius;
+    float color[4];
+} rt_sphere;
+
+/* CameraSettings — camera.rs:9-28 (main-world settings the camera builder consumes). */
+typedef struct rt_camera_settings {
+    float field_of_view;          /* degrees (camera.rs:37: 20) */
+    uint32_t samples_per_pixel;   /* camera.rs:33: 500 */
+    uint32_t camera_has_moved;    /* bool (camera.rs:35: true) */
+    uint32_t max_depth;           /* camera.rs:34: 30 */
+    float vup[3];                 /* camera.rs:40 */
+    float look_from[3];           /* camera.rs:38 */
+    float look_at[3];             /* camera.rs:39 */
+    float defocus_angle;          /* degrees (camera.rs:42: 0.6) */
+    float focus_distance;         /* camera.rs:43: 10 */
+} rt_camera_settings;
+
+/* Image stripe partition for multi-GPU rendering.  The image is cut into
+ * bands of RT_STRIPE_ROWS rows; band s belongs to rank (s mod nranks).  A rank's local
+ * buffer holds its bands back to back (local row = local_band * RT_STRIPE_ROWS + r).
+ * Pixel coordinates (and therefore every RNG seed) stay global. */
+#define RT_STRIPE_ROWS 8u
+
+/* ------------------------------------------------------------------------------------ */
+/* Status codes (the reference panics / unwraps instead: lib.rs:216-217, 356-358, 399-411) */
+/* ------------------------------------------------------------------------------------ */
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARGUMENT = 1, /* null pointer, zero size, in == out where forbidden */
+    RT_ERR_INVALID_SIZE = 2,     /* width/height/count out of range */
+    RT_ERR_INVALID_DEVICE = 3,   /* device ordinal does not exist */
+    RT_ERR_HIP = 4,              /* a HIP runtime call failed (rt_last_error has text) */
+    RT_ERR_NO_MEMORY = 5,
+    RT_ERR_INVALID_CONTEXT = 6
+} rt_status;
+
+typedef struct rt_ctx rt_ctx; /* one per device; calls on one ctx are externally serialized */
+
+/* Version / introspection ------------------------------------------------------------ */
+RT_API uint32_t rt_abi_version(void); /* RT_ABI_VERSION */
+#define RT_ABI_VERSION 1u
+/* Text of the last error on this thread (never NULL). */
+RT_API const char* rt_last_error(void);
+/* Kernel variant names for profiling/bench labelling; `which` 0 = update, 1 = render. */
+RT_API const char* rt_kernel_name(int which);
+
+/* Context ---------------------------------------------------------------------------- */
+/* Create a context on HIP device `device`.  Replaces ComputeShaderPipeline::from_world
+ * (lib.rs:240-324): there is no shader compile step, code objects are linked in. */
+RT_API rt_status rt_create(int device, rt_ctx** out_ctx);
+RT_API rt_status rt_destroy(rt_ctx* ctx);
+
+/* Scene upload (explicit form of prepare_sphere_buffer, lib.rs:177-207).  The update
+ * calls below also accept host spheres and upload them only when their bytes change. */
+RT_API rt_status rt_set_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
+                         void* stream);
+
+/* `init` (wgsl:65-70; dispatched in the Init state, lib.rs:398-407):
+ * out[x,y] = (0,0,0,0) for every texel of a width x height image. */
+RT_API rt_status rt_init_image(rt_ctx* ctx, float* out_rgba, uint32_t width, uint32_t height,
+                        void* stream);
+
+/* `update` (wgsl:333-364; dispatched every frame, lib.rs:408-417): one progressive sample
+ * per pixel.  in_rgba and out_rgba are device images (must not alias: the reference
+ * ping-pongs two textures, lib.rs:218-227).  spheres/count/camera are host pointers. */
+RT_API rt_status rt_update(rt_ctx* ctx, const float* in_rgba, float* out_rgba, uint32_t width,
+                    uint32_t height, const rt_scene_camera* camera,
+                    const rt_sphere* spheres, uint32_t sphere_count, void* stream);
+
+/* Fused multi-frame accumulate: bit-identical to `frames` chained rt_update calls where
+ * call f uses `camera` with random_seed = random_seeds[f] and camera_has_moved =
+ * (f == 0 ? camera->camera_has_moved : 0).  The accumulator stays in registers across
+ * frames (one HBM read + one write per pixel).  in_rgba may equal out_rgba. */
+RT_API rt_status rt_render(rt_ctx* ctx, const float* in_rgba, float* out_rgba, uint32_t width,
+                    uint32_t height, const rt_scene_camera* camera,
+                    const rt_sphere* spheres, uint32_t sphere_count, uint32_t frames,
+                    const float* random_seeds, void* stream);
+
+/* Multi-GPU tile path: the same as rt_render (frames >= 1) restricted to the stripe
+ * bands of `rank` out of `nranks` (RT_STRIPE_ROWS rows each, band s -> rank s % nranks).
+ * in/out are compact local images of width x rt_stripe_local_rows(height,rank,nranks). */
+RT_API rt_status rt_render_stripes(rt_ctx* ctx, const float* in_local, float* out_local,
+                            uint32_t width, uint32_t height, uint32_t rank,
+                            uint32_t nranks, const rt_scene_camera* camera,
+                            const rt_sphere* spheres, uint32_t sphere_count,
+                            uint32_t frames, const float* random_seeds, void* stream);
+RT_API uint32_t rt_stripe_local_rows(uint32_t height, uint32_t rank, uint32_t nranks);
+
+/* Root side of the gather: `gathered` holds nranks compact buffers back to back, each
+ * padded to max-local-rows (rt_stripe_local_rows(height,0,nranks)) rows; scatter them
+ * into the full width x height image `out_rgba` (device pointers). */
+RT_API rt_status rt_deinterleave_stripes(rt_ctx* ctx, const float* gathered, float* out_rgba,
+                                  uint32_t width, uint32_t height, uint32_t nranks,
+                                  void* stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Host-side mirror of the reference's main-world code (C++ implementation, no device)   */
+/* ------------------------------------------------------------------------------------ */
+
+/* CameraSettings::default() — camera.rs:30-46. */
+RT_API void rt_camera_settings_default(rt_camera_settings* out);
+
+/* SceneCamera::from(&CameraSettings) — camera.rs:293-351, with the image size as a
+ * runtime argument (the reference hard-codes crate::SIZE = 1280x720, camera.rs:296,
+ * 315-316) and the per-frame random_seed supplied by the caller (camera.rs:346 draws
+ * rand::random()).  glam/Rust f32 operation order is reproduced exactly. */
+RT_API rt_status rt_camera_from_settings(const rt_camera_settings* settings, uint32_t width,
+                                  uint32_t height, float random_seed,
+                                  rt_scene_camera* out);
+
+/* Seeded scene generators (create_default_spheres, sphere.rs:45-153).
+ *   kind 0: the three fixed large spheres (sphere.rs:114-136), glass / diffuse / metal.
+ *   kind 1: "default-like": ground + 14x14 jittered grid (a,b in -7..7) + 3 large.
+ *   kind 2: N-sphere: ground + grid a,b in -12..12 truncated to N-4 + 3 large (N>=4).
+ * Uniform variates come from splitmix64(seed), f = (u32 >> 8) * 2^-24 (rand 0.9's f32).
+ * Writes up to `capacity` spheres; *out_count receives the scene's sphere count. */
+RT_API rt_status rt_scene_generate(uint32_t kind, uint32_t n_spheres, uint64_t seed,
+                            rt_sphere* out, uint32_t capacity, uint32_t* out_count);
+
+/* Per-frame seeds: random_seed_f = k_f / 2^24 with k_f the top 24 bits of splitmix64
+ * outputs (seed 0x5EED in the bench).  Stands in for rand::random() (camera.rs:346). */
+RT_API void rt_frame_seeds(uint64_t seed, uint32_t frames, float* out_seeds);
+
+/* ComputeShaderNode state machine (lib.rs:326-421) as a headless frame driver:
+ * Loading -> Init (dispatch init on image B) -> Update(1) <-> Update(0) ping-pong,
+ * update(index) reads images[index] and writes images[1-index] (bind groups lib.rs:218-227:
+ * group 0 = (A -> B), group 1 = (B -> A)).  `rt_driver_frame` advances one frame and
+ * returns which image holds the newest result. */
+typedef struct rt_frame_driver rt_frame_driver;
+RT_API rt_status rt_driver_create(rt_ctx* ctx, float* image_a, float* image_b, uint32_t width,
+                           uint32_t height, rt_frame_driver** out);
+RT_API rt_status rt_driver_destroy(rt_frame_driver* drv);
+/* Runs one render-graph frame: node.update() then node.run() (lib.rs:345-421).
+ * *out_newest = 0 if image A holds the latest output, 1 for image B. */
+RT_API rt_status rt_driver_frame(rt_frame_driver* drv, const rt_scene_camera* camera,
+                          const rt_sphere* spheres, uint32_t sphere_count, void* stream,
+                          int* out_newest);
+/* 0 = Loading, 1 = Init, 2 = Update(0), 3 = Update(1). */
+RT_API int rt_driver_state(const rt_frame_driver* drv);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_ABI_H */
