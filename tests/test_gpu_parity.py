@@ -1,0 +1,299 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle and the
+committed golden fixtures, bit for bit (NaN == NaN).  Run on a real MI355X with -m gpu."""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import bits_equal, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pipe(rt):
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    p = rt.ComputeShaderPipeline(0)
+    yield p
+    p.close()
+
+
+def to_dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def assert_same(got, want):
+    ok, bad = bits_equal(got, want)
+    assert ok, f"{bad} channels differ"
+
+
+def camera(rt, w, h, depth=1, spp=500, seed=0.5, moved=True, defocus=0.6, fov=20.0):
+    s = rt.CameraSettings(max_depth=depth, samples_per_pixel=spp, camera_has_moved=moved,
+                          defocus_angle=defocus, field_of_view=fov)
+    return rt.SceneCamera.from_settings(s, w, h, seed)
+
+
+SCENES = {
+    "three": lambda rt: rt.three_spheres(),
+    "default": lambda rt: rt.create_default_spheres(1),
+    "n500": lambda rt: rt.synthetic_scene(500),
+}
+
+
+@pytest.mark.parametrize("scene", ["three", "default", "n500"])
+@pytest.mark.parametrize("w,h,depth,defocus", [(64, 48, 1, 0.6), (67, 45, 3, 0.6),
+                                               (40, 24, 8, 0.0), (16, 8, 0, 0.6),
+                                               (1, 1, 2, 0.6), (129, 7, 5, 1.5)])
+def test_update_matches_oracle(rt, oracle, pipe, scene, w, h, depth, defocus):
+    sc = SCENES[scene](rt)
+    cam = camera(rt, w, h, depth=depth, defocus=defocus, seed=0.3125)
+    inp = np.zeros((h, w, 4), np.float32)
+    a, b = to_dev(inp), pipe.new_image(w, h)
+    pipe.update(a, b, w, h, cam, sc)
+    want, _ = oracle.update(inp, cam.blob, sc.spheres)
+    assert_same(host(b), want)
+
+
+def test_update_accumulates_from_state(rt, oracle, pipe):
+    """Non-zero input accumulator, no reset; samples capped at spp; reset on move."""
+    w, h = 48, 40
+    sc = rt.create_default_spheres(2)
+    rng = np.random.default_rng(0)
+    state = np.concatenate([rng.random((h, w, 3), np.float32),
+                            rng.integers(0, 8, (h, w, 1)).astype(np.float32)], axis=2)
+    for moved, spp in [(False, 500), (False, 4), (True, 500), (False, 0)]:
+        cam = camera(rt, w, h, depth=4, spp=spp, moved=moved, seed=0.71875)
+        a, b = to_dev(state), pipe.new_image(w, h)
+        pipe.update(a, b, w, h, cam, sc)
+        want, _ = oracle.update(state, cam.blob, sc.spheres)
+        assert_same(host(b), want)
+
+
+def test_golden_k1_and_accumulator(rt, pipe):
+    g = load_golden("k1.npz")
+    cam = rt.SceneCamera(g["camera"])
+    sc = rt.SphereCollection(g["spheres"])
+    a, b = pipe.new_image(256, 256), pipe.new_image(256, 256)
+    pipe.update(a, b, 256, 256, cam, sc)
+    assert_same(host(b), g["image"])
+
+    g = load_golden("accum_default.npz")
+    h, w = g["state0"].shape[:2]
+    sc = rt.SphereCollection(g["spheres"])
+    cur = to_dev(g["state0"])
+    for f in range(3):
+        nxt = pipe.new_image(w, h)
+        pipe.update(cur, nxt, w, h, rt.SceneCamera(g["cameras"][f]), sc)
+        assert_same(host(nxt), g["frames"][f])
+        cur = nxt
+
+
+@pytest.mark.parametrize("name", ["k2.npz", "k3.npz"])
+def test_golden_full_hd_single_frame(rt, pipe, name):
+    """BASELINE configs[1], [2] at full size: the whole image hashes to the oracle's."""
+    g = load_golden(name)
+    w, h = int(g["width"]), int(g["height"])
+    a, b = pipe.new_image(w, h), pipe.new_image(w, h)
+    pipe.update(a, b, w, h, rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"]))
+    img = host(b)
+    assert_same(img[g["py"], g["px"]], g["pixels"])
+    assert hashlib.sha256(img.tobytes()).hexdigest() == str(g["sha256"])
+    assert np.array_equal(img.astype(np.float64).sum((0, 1)), g["channel_sums"])
+
+
+def test_golden_k4_fused_64spp(rt, pipe):
+    """configs[3]: 1920x1080, 500 spheres, 64 spp fused accumulate — full-image hash."""
+    g = load_golden("k4.npz")
+    w, h = int(g["width"]), int(g["height"])
+    a = pipe.new_image(w, h)
+    pipe.render(a, a, w, h, rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"]),
+                g["seeds"])
+    img = host(a)
+    assert_same(img[g["py"], g["px"]], g["pixels"])
+    assert hashlib.sha256(img.tobytes()).hexdigest() == str(g["sha256"])
+
+
+def test_golden_k5_sampled(rt, pipe):
+    """configs[4] shape on one GPU: 3840x2160, 500 spheres, 64 spp, depth 8 (sampled)."""
+    g = load_golden("k5.npz")
+    w, h = int(g["width"]), int(g["height"])
+    a = pipe.new_image(w, h)
+    pipe.render(a, a, w, h, rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"]),
+                g["seeds"])
+    img = host(a)
+    assert_same(img[g["py"], g["px"]], g["pixels"])
+    assert np.all(img[..., 3] == 64)
+
+
+@pytest.mark.parametrize("frames", [1, 3, 130])
+def test_render_equals_chained_updates(rt, oracle, pipe, frames):
+    """rt_render == `frames` chained rt_update calls (and the oracle), incl. >128 frames
+    (several launches) and the f32 sample-count round trip."""
+    w, h = 40, 32
+    sc = rt.create_default_spheres(3)
+    seeds = rt.frame_seeds(11, frames)
+    cam = camera(rt, w, h, depth=3, spp=100)  # cap hit inside the 130-frame run
+    a = pipe.new_image(w, h)
+    pipe.render(a, a, w, h, cam, sc, seeds)
+    fused = host(a)
+    cur, nxt = pipe.new_image(w, h), pipe.new_image(w, h)
+    for f in range(frames):
+        c = cam.with_fields(random_seed=float(seeds[f]), camera_has_moved=cam.camera_has_moved if f == 0 else 0.0)
+        pipe.update(cur, nxt, w, h, c, sc)
+        cur, nxt = nxt, cur
+    assert_same(fused, host(cur))
+    if frames <= 3:
+        want, _ = oracle.render(np.zeros((h, w, 4), np.float32), cam.blob, sc.spheres, seeds)
+        assert_same(fused, want)
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("w,h", [(64, 72), (50, 37)])
+def test_stripes_partition_invariance(rt, pipe, nranks, w, h):
+    """Rendering each rank's stripes separately and de-interleaving gives the full image."""
+    sc = rt.synthetic_scene(100)
+    seeds = rt.frame_seeds(5, 2)
+    cam = camera(rt, w, h, depth=2)
+    full = pipe.new_image(w, h)
+    pipe.render(full, full, w, h, cam, sc, seeds)
+    rows0 = rt.stripe_local_rows(h, 0, nranks)
+    gathered = torch.zeros((nranks * rows0, w, 4), dtype=torch.float32, device="cuda")
+    for r in range(nranks):
+        rows = rt.stripe_local_rows(h, r, nranks)
+        loc = pipe.new_image(w, max(rows, 1))
+        if rows:
+            pipe.render_stripes(loc, loc, w, h, r, nranks, cam, sc, seeds)
+            gathered[r * rows0:r * rows0 + rows] = loc[:rows]
+    out = pipe.new_image(w, h)
+    pipe.deinterleave(gathered, out, w, h, nranks)
+    assert_same(host(out), host(full))
+    # numpy restatement of the de-interleave
+    g = host(gathered).reshape(nranks, rows0, w, 4)
+    ref = np.empty((h, w, 4), np.float32)
+    for y in range(h):
+        band = y // 8
+        ref[y] = g[band % nranks, (band // nranks) * 8 + y % 8]
+    assert_same(host(out), ref)
+
+
+def test_init_and_frame_driver(rt, pipe):
+    """ComputeShaderNode (lib.rs:326-421): Loading->Init zeroes B, then B->A, A->B, ..."""
+    w, h = 32, 24
+    sc = rt.three_spheres()
+    imgs = rt.ComputeShaderImages(pipe, w, h)
+    imgs.texture_b.fill_(7.0)
+    node = rt.ComputeShaderNode(pipe, imgs)
+    assert node.state == "Loading"
+    seeds = rt.frame_seeds(9, 5)
+    newest = node.frame(camera(rt, w, h, seed=float(seeds[0])), sc)
+    assert node.state == "Init" and newest.data_ptr() == imgs.texture_b.data_ptr()
+    assert torch.count_nonzero(imgs.texture_b).item() == 0
+    ref_a, ref_b = pipe.new_image(w, h), pipe.new_image(w, h)
+    states = []
+    for f in range(4):
+        cam = camera(rt, w, h, seed=float(seeds[f + 1]), moved=(f == 0))
+        newest = node.frame(cam, sc)
+        states.append(node.state)
+        src, dst = (ref_b, ref_a) if f % 2 == 0 else (ref_a, ref_b)
+        pipe.update(src, dst, w, h, cam, sc)
+        assert_same(host(newest), host(dst))
+    assert states == ["Update(1)", "Update(0)", "Update(1)", "Update(0)"]
+    node.close()
+
+
+def test_errors_on_device(rt, pipe):
+    sc = rt.three_spheres()
+    cam = camera(rt, 8, 8)
+    a = pipe.new_image(8, 8)
+    with pytest.raises(rt.RtError) as e:
+        pipe.update(a, a, 8, 8, cam, sc)   # in == out is forbidden for update
+    assert e.value.status == 1
+    L = rt._lib.lib()
+    import ctypes
+    c = ctypes.c_void_p()
+    assert L.rt_create(999, ctypes.byref(c)) == 3
+    assert L.rt_init_image(pipe._ctx, ctypes.c_void_p(a.data_ptr()), 0, 8, None) == 2
+    assert L.rt_init_image(pipe._ctx, ctypes.c_void_p(a.data_ptr()), 70000, 8, None) == 2
+
+
+def test_nan_camera_propagates_like_oracle(rt, oracle, pipe):
+    """A degenerate camera (zero pixel deltas + zero disk => zero direction => NaN) gives
+    NaN where the oracle does; every sphere then counts as hit (!(NaN < 0))."""
+    w, h = 16, 8
+    cam = camera(rt, w, h, depth=3, defocus=0.0).with_fields(
+        pixel_delta_u=(0.0, 0.0, 0.0), pixel_delta_v=(0.0, 0.0, 0.0))
+    cam = cam.with_fields(viewport_upper_left=tuple(cam.center))
+    sc = rt.create_default_spheres(1)
+    a, b = pipe.new_image(w, h), pipe.new_image(w, h)
+    pipe.update(a, b, w, h, cam, sc)
+    want, _ = oracle.update(np.zeros((h, w, 4), np.float32), cam.blob, sc.spheres)
+    got = host(b)
+    assert np.isnan(want).any()
+    assert_same(got, want)
+
+
+def test_first_sphere_wins_ties(rt, oracle, pipe):
+    """Two coincident spheres: the first in the list is the hit (strict tmax <= root)."""
+    w, h = 32, 32
+    s = rt.three_spheres().spheres.copy()
+    dup = s[1].copy()
+    dup[4:8] = [0.9, 0.1, 0.1, -2.0]          # same geometry, different albedo
+    sc = rt.SphereCollection(np.vstack([s, dup]))
+    cam = camera(rt, w, h, depth=1)
+    a, b = pipe.new_image(w, h), pipe.new_image(w, h)
+    pipe.update(a, b, w, h, cam, sc)
+    want, _ = oracle.update(np.zeros((h, w, 4), np.float32), cam.blob, sc.spheres)
+    assert_same(host(b), want)
+    sc2 = rt.SphereCollection(s)
+    c = pipe.new_image(w, h)
+    pipe.update(a, c, w, h, cam, sc2)
+    assert_same(host(b), host(c))
+
+
+def test_scene_reupload_on_change(rt, oracle, pipe):
+    """Changing sphere bytes between calls re-uploads (prepare_sphere_buffer semantics)."""
+    w, h = 24, 16
+    cam = camera(rt, w, h, depth=2)
+    sc1, sc2 = rt.synthetic_scene(50, seed=1), rt.synthetic_scene(300, seed=2)
+    for sc in (sc1, sc2, sc1):
+        a, b = pipe.new_image(w, h), pipe.new_image(w, h)
+        pipe.update(a, b, w, h, cam, sc)
+        want, _ = oracle.update(np.zeros((h, w, 4), np.float32), cam.blob, sc.spheres)
+        assert_same(host(b), want)
+
+
+def test_full_size_properties(rt, pipe):
+    """3840x2160 (configs[4] frame size), depth 8: fused == chained, stripes == full,
+    deterministic across runs."""
+    w, h = 3840, 2160
+    sc = rt.synthetic_scene(500)
+    seeds = rt.frame_seeds(0x5EED, 2)
+    cam = camera(rt, w, h, depth=8, spp=64)
+    full = pipe.new_image(w, h)
+    pipe.render(full, full, w, h, cam, sc, seeds)
+    again = pipe.new_image(w, h)
+    pipe.render(again, again, w, h, cam, sc, seeds)
+    assert torch.equal(full, again)
+    cur, nxt = pipe.new_image(w, h), pipe.new_image(w, h)
+    for f in range(2):
+        pipe.update(cur, nxt, w, h, cam.with_fields(random_seed=float(seeds[f]),
+                                                   camera_has_moved=1.0 if f == 0 else 0.0), sc)
+        cur, nxt = nxt, cur
+    assert torch.equal(full, cur)
+    n = 8
+    rows0 = rt.stripe_local_rows(h, 0, n)
+    gathered = torch.zeros((n * rows0, w, 4), dtype=torch.float32, device="cuda")
+    for r in range(n):
+        rows = rt.stripe_local_rows(h, r, n)
+        loc = pipe.new_image(w, rows)
+        pipe.render_stripes(loc, loc, w, h, r, n, cam, sc, seeds)
+        gathered[r * rows0:r * rows0 + rows] = loc
+    out = pipe.new_image(w, h)
+    pipe.deinterleave(gathered, out, w, h, n)
+    assert torch.equal(out, full)

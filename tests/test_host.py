@@ -1,0 +1,143 @@
+"""CPU tests of the C-ABI library's host side: it loads, exports every symbol the header
+declares, has the reference's struct layouts, and its C++ host mirror (camera builder,
+scene generator, seeds, frame driver argument checks) matches the oracle restatements."""
+import ctypes
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PKG_DIR, ROOT
+
+HEADER = ROOT / "include" / "rt_abi.h"
+LIB = PKG_DIR / "build" / "librt_hip.so"
+
+
+def header_functions():
+    text = HEADER.read_text()
+    return re.findall(r"^RT_API [^(]*?\b(rt_\w+)\(", text, flags=re.M)
+
+
+def test_library_exports_every_declared_symbol(rt):
+    declared = header_functions()
+    assert len(declared) == 20
+    nm = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True,
+                        text=True, check=True).stdout
+    exported = set(re.findall(r" T (rt_\w+)$", nm, flags=re.M))
+    assert set(declared) <= exported, set(declared) - exported
+    # the ctypes binding covers exactly the header
+    assert set(rt._lib.exported_symbols()) == set(declared)
+    assert rt._lib.lib().rt_abi_version() == 1
+
+
+def test_scene_camera_layout_matches_reference(rt):
+    """camera.rs:256-291 / wgsl:7-40 byte offsets."""
+    C = rt._lib.SceneCameraC
+    want = dict(center=0, viewport_height=12, viewport_upper_left=16, viewport_width=28,
+                pixel_delta_u=32, defocus_angle=44, pixel_delta_v=48, aspect_ratio=60,
+                defocus_disk_u=64, _padding0=76, viewport_u=80, _padding1=92,
+                defocus_disk_v=96, max_depth=108, look_from=112, samples_per_pixel=124,
+                look_at=128, camera_has_moved=140, vup=144, random_seed=156, viewport_v=160,
+                defocus_radius=172)
+    for name, off in want.items():
+        assert getattr(C, name).offset == off, name
+    assert ctypes.sizeof(C) == 176
+    S = rt._lib.SphereC
+    assert (S.position.offset, S.radius.offset, S.color.offset, ctypes.sizeof(S)) == (0, 12, 16, 32)
+
+
+def test_camera_defaults(rt):
+    d = rt.CameraSettings.default_from_library()
+    ref = rt.CameraSettings()  # camera.rs:30-46
+    assert bytes(d.to_c()) == bytes(ref.to_c())
+
+
+@pytest.mark.parametrize("w,h,fov,defocus,seed", [
+    (1280, 720, 20.0, 0.6, 0.0), (1920, 1080, 20.0, 0.6, 0.5), (256, 256, 45.0, 0.0, 0.25),
+    (3840, 2160, 20.0, 0.6, 0.75), (333, 77, 90.0, 2.5, 0.125)])
+def test_camera_builder_matches_restatement(rt, w, h, fov, defocus, seed):
+    from oracle import host_ref as H
+    got = rt.SceneCamera.from_settings(
+        rt.CameraSettings(field_of_view=fov, defocus_angle=defocus), w, h, seed).blob
+    want = H.scene_camera_from(fov=fov, defocus_angle=defocus, width=w, height=h,
+                               random_seed=seed)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_camera_builder_hand_values(rt):
+    """Spot values by hand (camera.rs:293-351) at 1280x720 (the reference's SIZE)."""
+    cam = rt.SceneCamera.from_settings(rt.CameraSettings(), 1280, 720, 0.0)
+    assert cam.aspect_ratio == pytest.approx(16 / 9, rel=1e-7)
+    vh = 2 * np.tan(np.radians(10.0)) * 10
+    assert cam.viewport_height == pytest.approx(vh, rel=1e-6)
+    assert cam.viewport_width == pytest.approx(vh * 16 / 9, rel=1e-6)
+    assert cam.defocus_radius == pytest.approx(10 * np.tan(np.radians(0.3)), rel=1e-6)
+    w = np.array([13, 2, 3.0]) / np.linalg.norm([13, 2, 3])
+    ul = np.array(cam.viewport_upper_left)
+    center = np.array(cam.center) - 10 * w
+    assert np.linalg.norm(ul - center) == pytest.approx(
+        0.5 * np.hypot(cam.viewport_width, cam.viewport_height), rel=1e-5)
+    assert cam.max_depth == 30 and cam.samples_per_pixel == 500 and cam.camera_has_moved == 1
+
+
+@pytest.mark.parametrize("kind,n,seed", [(0, 0, 1), (1, 0, 1), (1, 0, 99), (2, 500, 1),
+                                         (2, 4, 1), (2, 64, 3), (2, 1500, 2)])
+def test_scene_generator_matches_restatement(rt, kind, n, seed):
+    from oracle import host_ref as H
+    got = rt.SphereCollection.generate(kind, n, seed).spheres
+    want = H.generate_scene(kind, n, seed)
+    assert got.shape == want.shape
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_scene_contents(rt):
+    """sphere.rs:49-136: ground first, three large last, materials encoded in color.w."""
+    s = rt.synthetic_scene(500).spheres
+    assert s.shape == (500, 8)
+    assert list(s[0]) == [0, -1000, 0, 1000, 0.5, 0.5, 0.5, -2]
+    assert [list(r) for r in s[-3:]] == [[0, 1, 0, 1, 1.5, 0, 0, 2],
+                                         [-4, 1, 0, 1, 0.4, 0.2, 0.1, -2],
+                                         [4, 1, 0, 1, 0.7, 0.6, 0.5, 0]]
+    small = s[1:-3]
+    assert np.all(small[:, 1] == np.float32(0.2)) and np.all(small[:, 3] == np.float32(0.2))
+    assert np.all(np.linalg.norm(small[:, :3] - np.array([4, 0.2, 0], np.float32), axis=1) > 0.9)
+    kinds = np.where(small[:, 7] < -1, 0, np.where(small[:, 7] <= 1, 1, 2))
+    frac = np.bincount(kinds, minlength=3) / len(kinds)
+    assert 0.7 < frac[0] < 0.9 and 0.08 < frac[1] < 0.22 and frac[2] < 0.1
+    d = rt.create_default_spheres(1)
+    assert 190 <= d.count <= 200  # 196 - skipped + 4
+
+
+def test_frame_seeds(rt):
+    from oracle import host_ref as H
+    s = rt.frame_seeds(0x5EED, 1000)
+    assert np.array_equal(s, H.frame_seeds(0x5EED, 1000))
+    assert np.all((s >= 0) & (s < 1)) and np.all(s * 2 ** 24 == np.round(s * 2 ** 24))
+
+
+def test_stripe_local_rows(rt):
+    for h in (1, 7, 8, 9, 64, 1080, 2160, 2161):
+        for n in (1, 2, 3, 4, 8):
+            rows = [rt.stripe_local_rows(h, r, n) for r in range(n)]
+            bands = (h + 7) // 8
+            assert sum(rows) // 8 == bands
+            assert max(rows) == rows[0]
+            assert max(rows) - min(rows) <= 8
+
+
+def test_argument_errors_without_device(rt):
+    """Argument checks that fail before touching a device."""
+    L = rt._lib.lib()
+    assert L.rt_create(0, None) == 1                         # NULL out pointer
+    assert L.rt_update(None, None, None, 8, 8, None, None, 0, None) == 1
+    assert L.rt_destroy(None) == 6
+    cnt = rt._lib.U32(0)
+    assert L.rt_scene_generate(2, 3, 1, None, 0, ctypes.byref(cnt)) == 2  # N < 4
+    assert L.rt_scene_generate(9, 0, 1, None, 0, ctypes.byref(cnt)) == 1
+    s = rt._lib.CameraSettingsC()
+    out = rt._lib.SceneCameraC()
+    assert L.rt_camera_from_settings(ctypes.byref(s), 0, 10, ctypes.c_float(0), ctypes.byref(out)) == 2
+    assert L.rt_driver_create(None, None, None, 8, 8, None) == 1
+    assert L.rt_driver_state(None) == -1
+    assert L.rt_stripe_local_rows(100, 3, 2) == 0
