@@ -57,6 +57,7 @@ struct DeviceGuard {
 
 constexpr uint32_t kMaxDim = 1u << 16;         // 65536 x 65536 texels
 constexpr uint32_t kMaxSpheres = 1u << 20;
+constexpr uint32_t kScanPad = 16;  // >= one scan chunk (rt_kernels.hip)
 
 rt_status check_image(uint32_t w, uint32_t h) {
     if (w == 0 || h == 0 || w > kMaxDim || h > kMaxDim)
@@ -72,12 +73,19 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
     if (ctx->valid && count == ctx->count &&
         (count == 0 || std::memcmp(ctx->cached.data(), spheres, count * sizeof(rt_sphere)) == 0))
         return RT_OK;  // unchanged since the last upload
-    if (count > ctx->capacity) {
+    if (count > ctx->capacity || ctx->d_geom == nullptr) {
         uint32_t cap = ctx->capacity ? ctx->capacity : 64u;
         while (cap < count) cap *= 2u;
         float4 *g = nullptr, *s = nullptr;
-        hipError_t e = hipMalloc(&g, (size_t)cap * sizeof(float4));
+        // kScanPad zero records after the list: the scan prefetches one chunk ahead.
+        const size_t geom_bytes = ((size_t)cap + kScanPad) * sizeof(float4);
+        hipError_t e = hipMalloc(&g, geom_bytes);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(sphere geometry)");
+        e = hipMemsetAsync(g, 0, geom_bytes, stream);
+        if (e != hipSuccess) {
+            (void)hipFree(g);
+            return hip_fail(e, "hipMemsetAsync(sphere geometry)");
+        }
         e = hipMalloc(&s, (size_t)cap * 2 * sizeof(float4));
         if (e != hipSuccess) {
             (void)hipFree(g);
@@ -98,14 +106,27 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
         // Scan record: center + radius^2.  r*r is one IEEE f32 multiply, bit-identical to
         // the shader's `sphere.radius * sphere.radius` (wgsl:186).
         std::vector<float4> geom(count);
-        for (uint32_t i = 0; i < count; ++i) {
-            const rt_sphere& s = spheres[i];
-            geom[i] = make_float4(s.position[0], s.position[1], s.position[2],
-                                  s.radius * s.radius);
+        if (rtk::scan_layout() == 0) {
+            for (uint32_t i = 0; i < count; ++i) {
+                const rt_sphere& s = spheres[i];
+                geom[i] = make_float4(s.position[0], s.position[1], s.position[2],
+                                      s.radius * s.radius);
+            }
+        } else {  // SoA blocks of 4: {cx0..3, cy0..3, cz0..3, rr0..3}; tail zero-filled
+            geom.assign(((size_t)count + 3u) / 4u * 4u, make_float4(0.f, 0.f, 0.f, 0.f));
+            float* f = reinterpret_cast<float*>(geom.data());
+            for (uint32_t i = 0; i < count; ++i) {
+                const rt_sphere& s = spheres[i];
+                float* b = f + (size_t)(i / 4u) * 16u + (i % 4u);
+                b[0] = s.position[0];
+                b[4] = s.position[1];
+                b[8] = s.position[2];
+                b[12] = s.radius * s.radius;
+            }
         }
         // Queued launches may still read the old scene: order the copies on the stream,
         // and wait for them so the host staging vectors can be released.
-        hipError_t e = hipMemcpyAsync(ctx->d_geom, geom.data(), count * sizeof(float4),
+        hipError_t e = hipMemcpyAsync(ctx->d_geom, geom.data(), geom.size() * sizeof(float4),
                                       hipMemcpyHostToDevice, stream);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(sphere geometry)");
         e = hipMemcpyAsync(ctx->d_sph, spheres, count * sizeof(rt_sphere),

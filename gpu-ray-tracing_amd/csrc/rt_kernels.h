@@ -34,5 +34,8 @@ hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t wid
                                uint32_t height, uint32_t nranks, uint32_t max_local_rows,
                                hipStream_t stream);
 const char* trace_kernel_name();
+// Layout of TraceParams::geom the kernels expect: 0 = one float4 (cx,cy,cz,r*r) per
+// sphere; 1 = SoA blocks of 4 spheres {cx0..3, cy0..3, cz0..3, rr0..3}.
+int scan_layout();
 
 }  // namespace rtk

@@ -29,33 +29,187 @@ struct Hit {
 // sphere_list_hit (wgsl:164-180) + sphere_hit (wgsl:182-201) without the hit record:
 // only the closest root and its index are tracked; the record (p, normal, face,
 // material) is rebuilt once for the winner, bit-identical to the WGSL's last assignment.
+//
+// The scan walks the list in chunks of 4 spheres.  The 16-byte scan records of the next
+// chunk are fetched with scalar loads while the current chunk is computed (the index is
+// wave-uniform, so the records live in SGPRs and feed the VALU directly).  Per sphere the
+// common (miss) path is 12 VALU ops for the discriminant; the chunk's four "!(D < 0)"
+// tests collapse into one integer max + compare on the float bit patterns (exact: D is
+// never -0, see below), so the root-finding path is entered once per chunk at most.
+
+// Discriminant of wgsl:183-187 for one sphere record g = (center, r*r).
+__device__ __forceinline__ float discriminant(const float4 g, v3 o, v3 d, float a, float& h) {
+    const float ocx = g.x - o.x;                                        // wgsl:183
+    const float ocy = g.y - o.y;
+    const float ocz = g.z - o.z;
+    h = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));                      // wgsl:185
+    const float c = fmaf(ocz, ocz, fmaf(ocy, ocy, ocx * ocx)) - g.w;    // wgsl:186
+    return fmaf(h, h, -(a * c));                                        // wgsl:187
+}
+
+// Root selection of wgsl:189-201 for sphere i, given its discriminant.
+__device__ __forceinline__ void consider(float disc, float h, float a, uint32_t i, float& tmax,
+                                         int& idx) {
+    if (!(disc < 0.0f)) {                                               // wgsl:189
+        const float q = sqrtf(disc);
+        float root = (h - q) / a;
+        if (root <= 0x1.0624dep-10f || tmax <= root) {                  // wgsl:196
+            root = (h + q) / a;
+            if (root <= 0x1.0624dep-10f || tmax <= root) return;        // wgsl:198
+        }
+        tmax = root;
+        idx = (int)i;
+    }
+}
+
+// "!(D < 0)" for any of K discriminants, on the bit patterns: a float is < 0 exactly
+// when its int32 view is <= 0xFF800000 (-inf) and it is not -0.  D = fma(h, h, -(a*c))
+// with h*h >= +0 and a >= +0 cannot round to -0, so the test is one max-tree and one
+// compare per chunk (max_bits below).
+
+// Scan variant selection (compile-time, for A/B builds only; the product uses the
+// default).  0: one sphere per iteration; 1: chunks of 4 + prefetch + one test per chunk;
+// 2: as 1, but the records are staged in LDS once per workgroup (ds_read broadcast).
+#ifndef RT_SCAN_VARIANT
+#define RT_SCAN_VARIANT 1
+#endif
+
+#if RT_SCAN_VARIANT == 0
 __device__ __forceinline__ Hit scan_spheres(const float4* __restrict__ geom, uint32_t count,
+                                            v3 o, v3 d) {
+    const float a = dot(d, d);
+    float tmax = 0x1.05ed2ep+118f;
+    int idx = -1;
+    for (uint32_t i = 0; i < count; ++i) {
+        float h;
+        const float disc = discriminant(geom[i], o, d, a, h);
+        consider(disc, h, a, i, tmax, idx);
+    }
+    return Hit{idx, tmax};
+}
+#elif RT_SCAN_VARIANT == 3
+// Scan records in SoA blocks of 4 spheres (64 B = one s_load_dwordx16):
+//   {cx0..cx3, cy0..cy3, cz0..cz3, rr0..rr3}.
+// On gfx950 a VALU op with an SGPR operand issues at half rate (~4.2 vs ~2.3 cycles per
+// wave64 instruction, tools/valu_microbench.hip), while a packed op reading an SGPR pair
+// costs the same 4.2 cycles for two elements.  So the four SGPR-consuming ops per sphere
+// (oc = C - O and c = dot(oc,oc) - r*r) are issued as v_pk_add_f32 on sphere pairs, and
+// everything else runs as full-rate single-precision VGPR ops.
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void disc_pair(f2v cx, f2v cy, f2v cz, f2v rr, v3 o, v3 d, float a,
+                                          float& h0, float& h1, float& d0, float& d1) {
+    const f2v ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const f2v ocx = cx - ox, ocy = cy - oy, ocz = cz - oz;                   // wgsl:183
+    h0 = fmaf(ocz.x, d.z, fmaf(ocy.x, d.y, ocx.x * d.x));                    // wgsl:185
+    h1 = fmaf(ocz.y, d.z, fmaf(ocy.y, d.y, ocx.y * d.x));
+    f2v cc;
+    cc.x = fmaf(ocz.x, ocz.x, fmaf(ocy.x, ocy.x, ocx.x * ocx.x));
+    cc.y = fmaf(ocz.y, ocz.y, fmaf(ocy.y, ocy.y, ocx.y * ocx.y));
+    const f2v c = cc - rr;                                                   // wgsl:186
+    d0 = fmaf(h0, h0, -(a * c.x));                                           // wgsl:187
+    d1 = fmaf(h1, h1, -(a * c.y));
+}
+
+__device__ __forceinline__ Hit scan_spheres(const float4* __restrict__ geom4, uint32_t count,
                                             v3 o, v3 d) {
     const float a = dot(d, d);                 // wgsl:184 (ray-invariant)
     float tmax = 0x1.05ed2ep+118f;             // 3.4e35 (wgsl:266)
     int idx = -1;
-#pragma unroll 4
-    for (uint32_t i = 0; i < count; ++i) {
-        const float4 g = geom[i];              // wave-uniform -> s_load into SGPRs
-        const float ocx = g.x - o.x;           // wgsl:183
-        const float ocy = g.y - o.y;
-        const float ocz = g.z - o.z;
-        const float h = fmaf(ocz, d.z, fmaf(ocy, d.y, ocx * d.x));          // wgsl:185
-        const float c = fmaf(ocz, ocz, fmaf(ocy, ocy, ocx * ocx)) - g.w;    // wgsl:186
-        const float disc = fmaf(h, h, -(a * c));                            // wgsl:187
-        if (!(disc < 0.0f)) {                                               // wgsl:189
-            const float q = sqrtf(disc);
-            float root = (h - q) / a;
-            if (root <= 0x1.0624dep-10f || tmax <= root) {                  // wgsl:196
-                root = (h + q) / a;
-                if (root <= 0x1.0624dep-10f || tmax <= root) continue;      // wgsl:198
-            }
-            tmax = root;
-            idx = (int)i;
+    const uint32_t nchunks = (count + 3u) >> 2;
+    // one zero block of padding after the last chunk keeps the prefetch in bounds
+    float4 c0 = geom4[0], c1 = geom4[1], c2 = geom4[2], c3 = geom4[3];
+    for (uint32_t k = 0; k < nchunks; ++k) {
+        const float4* nb = geom4 + 4u * (k + 1u);
+        const float4 n0 = nb[0], n1 = nb[1], n2 = nb[2], n3 = nb[3];
+        float h[4], dd[4];
+        disc_pair(f2v{c0.x, c0.y}, f2v{c1.x, c1.y}, f2v{c2.x, c2.y}, f2v{c3.x, c3.y}, o, d, a,
+                  h[0], h[1], dd[0], dd[1]);
+        disc_pair(f2v{c0.z, c0.w}, f2v{c1.z, c1.w}, f2v{c2.z, c2.w}, f2v{c3.z, c3.w}, o, d, a,
+                  h[2], h[3], dd[2], dd[3]);
+        const int m = max(max(__float_as_int(dd[0]), __float_as_int(dd[1])),
+                          max(__float_as_int(dd[2]), __float_as_int(dd[3])));
+        if (__builtin_expect(m > (int)0xFF800000, 0)) {
+            const uint32_t i0 = 4u * k;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (i0 + j < count) consider(dd[j], h[j], a, i0 + j, tmax, idx);
         }
+        c0 = n0;
+        c1 = n1;
+        c2 = n2;
+        c3 = n3;
     }
     return Hit{idx, tmax};
 }
+#else
+#ifndef RT_SCAN_CHUNK
+#define RT_SCAN_CHUNK 4
+#endif
+#ifndef RT_SCAN_PIN_LOADS
+#define RT_SCAN_PIN_LOADS 0
+#endif
+#ifndef RT_SCAN_ABLATE_RARE
+#define RT_SCAN_ABLATE_RARE 0
+#endif
+// max over the int32 views of K discriminants
+template <int K>
+__device__ __forceinline__ int max_bits(const float (&dd)[K]) {
+    int m = __float_as_int(dd[0]);
+#pragma unroll
+    for (int k = 1; k < K; ++k) m = max(m, __float_as_int(dd[k]));
+    return m;
+}
+
+__device__ __forceinline__ Hit scan_spheres(const float4* __restrict__ geom, uint32_t count,
+                                            v3 o, v3 d) {
+    constexpr int K = RT_SCAN_CHUNK;
+    const float a = dot(d, d);                 // wgsl:184 (ray-invariant)
+    float tmax = 0x1.05ed2ep+118f;             // 3.4e35 (wgsl:266)
+    int idx = -1;
+    const uint32_t nk = count - count % K;
+    // geom is padded with zero records, so the prefetch of the chunk after the last one
+    // stays inside the allocation.
+    float4 cur[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) cur[k] = geom[k];
+    uint32_t i = 0;
+#if RT_SCAN_ABLATE_RARE
+    float sink = 0.0f;
+#endif
+    for (; i < nk; i += K) {
+        float4 nxt[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) nxt[k] = geom[i + K + k];
+#if RT_SCAN_PIN_LOADS
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+        float hh[K], dd[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) dd[k] = discriminant(cur[k], o, d, a, hh[k]);
+#if RT_SCAN_ABLATE_RARE
+#pragma unroll
+        for (int k = 0; k < K; ++k) sink += dd[k] + hh[k];
+#else
+        if (__builtin_expect(max_bits<K>(dd) > (int)0xFF800000, 0)) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) consider(dd[k], hh[k], a, i + k, tmax, idx);
+        }
+#endif
+#pragma unroll
+        for (int k = 0; k < K; ++k) cur[k] = nxt[k];
+    }
+#if RT_SCAN_ABLATE_RARE
+    if (sink == 12345.0f) idx = 0;
+#endif
+    for (; i < count; ++i) {
+        float h;
+        const float disc = discriminant(geom[i], o, d, a, h);
+        consider(disc, h, a, i, tmax, idx);
+    }
+    return Hit{idx, tmax};
+}
+#endif
 
 struct Cam {
     v3 center, vul, pdu, pdv, ddu, ddv;
@@ -135,7 +289,18 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, const float4* __re
 }
 
 // One wave = one 8x8 tile of the (local) image; lanes are row-major inside the tile.
-__global__ __launch_bounds__(256) void rt_trace_kernel(const TraceParams p) {
+#ifndef RT_TRACE_MIN_WAVES
+#define RT_TRACE_MIN_WAVES 8
+#endif
+__global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const TraceParams p) {
+#if RT_SCAN_VARIANT == 2
+    extern __shared__ float4 lds_geom[];
+    for (uint32_t j = threadIdx.x; j < p.count + 8u; j += blockDim.x) lds_geom[j] = p.geom[j];
+    __syncthreads();
+    const float4* scan_geom = lds_geom;
+#else
+    const float4* scan_geom = p.geom;
+#endif
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t tiles_x = (p.width + 7u) >> 3;
@@ -175,7 +340,7 @@ __global__ __launch_bounds__(256) void rt_trace_kernel(const TraceParams p) {
             const uint32_t seed = 1u + n + B;
             v3 o, d;
             get_ray(cam, x, y, hxy, seed, B, o, d);
-            const v3 col = ray_color(p, p.geom, p.sph, depth, o, d, seed + 1u);
+            const v3 col = ray_color(p, scan_geom, p.sph, depth, o, d, seed + 1u);
             const float k = (float)(n + 1u);                      // wgsl:356
             c = mk(c.x + (col.x - c.x) / k, c.y + (col.y - c.y) / k, c.z + (col.z - c.z) / k);
             n += 1u;
@@ -216,7 +381,13 @@ hipError_t launch_trace(const TraceParams& p, hipStream_t stream) {
     const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
     const uint32_t blocks = (uint32_t)((tiles + 3u) / 4u);
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(rt_trace_kernel, dim3(blocks), dim3(256), 0, stream, p);
+#if RT_SCAN_VARIANT == 2
+    const size_t lds = ((size_t)p.count + 8u) * sizeof(float4);
+    if (lds > 65536) return hipErrorInvalidValue;
+#else
+    const size_t lds = 0;
+#endif
+    hipLaunchKernelGGL(rt_trace_kernel, dim3(blocks), dim3(256), lds, stream, p);
     return hipGetLastError();
 }
 
@@ -242,5 +413,7 @@ hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t wid
 }
 
 const char* trace_kernel_name() { return "rt_trace_kernel"; }
+
+int scan_layout() { return RT_SCAN_VARIANT == 3 ? 1 : 0; }
 
 }  // namespace rtk

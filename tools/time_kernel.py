@@ -1,0 +1,28 @@
+"""Time the trace kernel for one library build (RT_HIP_LIB) on a config; check the K3/K2
+golden hash.  Used by tools/ab_variants.py for interleaved A/B runs."""
+import hashlib, json, sys
+from pathlib import Path
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT / "gpu-ray-tracing_amd"), str(ROOT)]
+import numpy as np, torch
+import gpu_ray_tracing as rt
+
+def main(cfg="k3", iters=40):
+    g = dict(np.load(ROOT / "tests" / "golden" / f"{cfg}.npz"))
+    w, h = int(g["width"]), int(g["height"])
+    cam = rt.SceneCamera(g["camera"]); sc = rt.SphereCollection(g["spheres"])
+    pipe = rt.ComputeShaderPipeline(0)
+    a, b = pipe.new_image(w, h), pipe.new_image(w, h)
+    pipe.update(a, b, w, h, cam, sc); torch.cuda.synchronize()
+    ok = hashlib.sha256(b.cpu().numpy().tobytes()).hexdigest() == str(g["sha256"]) if "sha256" in g else None
+    c2 = cam.with_fields(camera_has_moved=0.0, samples_per_pixel=1e6)
+    st = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for k in range(iters):
+        evs[k][0].record(st); pipe.update(a, b, w, h, c2, sc); evs[k][1].record(st); a, b = b, a
+    torch.cuda.synchronize()
+    t = sorted(x.elapsed_time(y) * 1e3 for x, y in evs)
+    print(json.dumps({"cfg": cfg, "median_us": t[len(t) // 2], "min_us": t[0], "hash_ok": ok}))
+
+if __name__ == "__main__":
+    main(*(sys.argv[1:2] or ["k3"]))
