@@ -11,9 +11,11 @@ round-robin, and after the K timed steps the finished tiles are gathered to rank
 ONE RCCL gather + the de-interleave kernel — both inside the timed region.
 
 value = W*H*K camera rays / max-over-ranks wall time (Mrays/s, whole job).
-roofline: the trace kernel's algorithmic FP32 work (23 FLOP per ray-sphere test,
-SURVEY §8d) per launch / its average launch time from HIP events, against the FP32 vector
-peak (157.3 TFLOP/s); the HBM side (32 B/pixel/step) is reported beside it.
+roofline (trace kernel, average launch time from HIP events): for the default culled scan
+the algorithmic HBM bytes (32 B/pixel/step) against 8 TB/s; for --scan exhaustive the
+algorithmic FP32 work (23 FLOP per ray-sphere test) against the 157.3 TFLOP/s
+FP32 vector peak.  The exhaustive kernel is also timed on the same frames
+(fp32_exhaustive_scan) so both rooflines appear in one line.
 cpu_baseline: the scalar C oracle on one host core over a bounded sample (rank 0, N=1).
 """
 from __future__ import annotations
@@ -56,6 +58,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="K3", choices=sorted(CONFIGS))
+    ap.add_argument("--scan", default="culled", choices=["culled", "exhaustive"],
+                    help="sphere-list scan: exact wave-level culling (default) or the "
+                         "reference's exhaustive linear walk; images are bit-identical")
+    ap.add_argument("--exhaustive-steps", type=int, default=10,
+                    help="also time the exhaustive-scan kernel for its FP32 roofline")
     ap.add_argument("--cpu-frames", type=float, default=2.0,
                     help="CPU baseline sample size in frames of the workload (0 = skip)")
     return ap.parse_args()
@@ -111,6 +118,7 @@ def main():
                              camera_has_moved=1.0 if f == 0 else 0.0) for f in range(frames)]
 
     pipe = rt.ComputeShaderPipeline(local_rank)
+    pipe.set_scan_mode(args.scan)
     pipe.set_spheres(spheres)
     r = StripeRenderer(pipe, w, h, rank, world)
     stream = torch.cuda.current_stream()
@@ -145,11 +153,46 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     launch_s = float(np.mean(kern_ms)) / 1e3
     local_px = w * min(r.rows, h)
-    flops = local_px * 1 * nsph * FLOP_PER_TEST  # depth-1: one segment per sample
-    if depth != 1:
-        flops = None  # segments per sample vary; reported from the oracle count elsewhere
+    # SURVEY §8d algorithmic units: the reference's exhaustive scan does N tests of 23 FLOP
+    # per segment; at max_depth 1 every sample is exactly one segment.
+    flops = local_px * nsph * FLOP_PER_TEST if depth == 1 else None
     hbm_bytes = local_px * BYTES_PER_PIXEL_STEP
     value = w * h * args.steps / dt / 1e6
+
+    # The exhaustive (reference-algorithm) kernel on the same frames, for its FP32 roofline.
+    exh = None
+    if args.scan == "culled" and flops and args.exhaustive_steps > 0:
+        pipe.set_scan_mode("exhaustive")
+        e2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.exhaustive_steps)]
+        for k in range(args.exhaustive_steps):
+            f = args.warmup + k % args.steps
+            e2[k][0].record(stream)
+            r.frame(cams[f], spheres, seeds[f:f + 1])
+            e2[k][1].record(stream)
+        torch.cuda.synchronize()
+        pipe.set_scan_mode(args.scan)
+        t_exh = float(np.mean([a.elapsed_time(b) for a, b in e2])) / 1e3
+        exh = {"kernel_avg_us": round(t_exh * 1e6, 2),
+               "achieved": round(flops / t_exh / 1e12, 3), "peak": PEAK_FP32_TFLOPS,
+               "unit": "TFLOP/s", "frac": round(flops / t_exh / 1e12 / PEAK_FP32_TFLOPS, 4),
+               "flop_per_launch": flops,
+               "speedup_of_culled": round(t_exh / launch_s, 2)}
+
+    if args.scan == "exhaustive" and flops:
+        roof = {"bound": "valu", "achieved": round(flops / launch_s / 1e12, 3),
+                "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(flops / launch_s / 1e12 / PEAK_FP32_TFLOPS, 4),
+                "traffic": load_pmc(f"{args.config}_exhaustive"),
+                "kernel_avg_us": round(launch_s * 1e6, 2), "flop_per_launch": flops}
+    else:
+        # Culled scan: the redundant ray-sphere tests are gone (exactly), so
+        # the algorithm-independent unit left is the accumulator's 32 B/pixel of HBM.
+        roof = {"bound": "hbm", "achieved": round(hbm_bytes / launch_s / 1e9, 1),
+                "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(hbm_bytes / launch_s / 1e9 / PEAK_HBM_GBS, 4),
+                "traffic": load_pmc(f"{args.config}_culled"),
+                "kernel_avg_us": round(launch_s * 1e6, 2), "bytes_per_launch": hbm_bytes}
 
     if rank == 0:
         sample_ok = image is not None and bool(torch.all(image[..., 3] == frames).item())
@@ -169,21 +212,10 @@ def main():
             "config": {"workload": f"{args.config} {desc}, max_depth {depth}",
                        "width": w, "height": h, "spheres": nsph, "spp_per_step": 1,
                        "max_depth": depth, "parallelism": f"stripes{world}",
+                       "scan": args.scan,
                        "kernel": rt._lib.lib().rt_kernel_name(0).decode()},
-            "roofline": {
-                "bound": "valu" if flops is not None and flops / (PEAK_FP32_TFLOPS * 1e12)
-                > hbm_bytes / (PEAK_HBM_GBS * 1e9) else "hbm",
-                "achieved": round(flops / launch_s / 1e12, 3) if flops else None,
-                "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(flops / launch_s / 1e12 / PEAK_FP32_TFLOPS, 4) if flops else None,
-                "traffic": load_pmc(args.config),
-                "kernel_avg_us": round(launch_s * 1e6, 2),
-                "flop_per_launch": flops,
-            },
-            "hbm": {"achieved_gbs": round(hbm_bytes / launch_s / 1e9, 1),
-                    "peak_gbs": PEAK_HBM_GBS,
-                    "frac": round(hbm_bytes / launch_s / 1e9 / PEAK_HBM_GBS, 4),
-                    "bytes_per_launch": hbm_bytes},
+            "roofline": roof,
+            "fp32_exhaustive_scan": exh,
             "accumulated_spp_ok": sample_ok,
         }
         if world == 1 and args.cpu_frames > 0:

@@ -20,6 +20,7 @@
 
 struct rt_ctx {
     int device = 0;
+    int scan_mode = RT_SCAN_CULLED;
     float4* d_geom = nullptr;  // count x (cx, cy, cz, r*r)
     float4* d_sph = nullptr;   // count x 2 float4 (the 32-B GpuSphere records)
     uint32_t capacity = 0;
@@ -57,7 +58,7 @@ struct DeviceGuard {
 
 constexpr uint32_t kMaxDim = 1u << 16;         // 65536 x 65536 texels
 constexpr uint32_t kMaxSpheres = 1u << 20;
-constexpr uint32_t kScanPad = 16;  // >= one scan chunk (rt_kernels.hip)
+constexpr uint32_t kScanPad = 68;  // >= chunk round-up + one chunk + a 64-lane block
 
 rt_status check_image(uint32_t w, uint32_t h) {
     if (w == 0 || h == 0 || w > kMaxDim || h > kMaxDim)
@@ -106,23 +107,10 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
         // Scan record: center + radius^2.  r*r is one IEEE f32 multiply, bit-identical to
         // the shader's `sphere.radius * sphere.radius` (wgsl:186).
         std::vector<float4> geom(count);
-        if (rtk::scan_layout() == 0) {
-            for (uint32_t i = 0; i < count; ++i) {
-                const rt_sphere& s = spheres[i];
-                geom[i] = make_float4(s.position[0], s.position[1], s.position[2],
-                                      s.radius * s.radius);
-            }
-        } else {  // SoA blocks of 4: {cx0..3, cy0..3, cz0..3, rr0..3}; tail zero-filled
-            geom.assign(((size_t)count + 3u) / 4u * 4u, make_float4(0.f, 0.f, 0.f, 0.f));
-            float* f = reinterpret_cast<float*>(geom.data());
-            for (uint32_t i = 0; i < count; ++i) {
-                const rt_sphere& s = spheres[i];
-                float* b = f + (size_t)(i / 4u) * 16u + (i % 4u);
-                b[0] = s.position[0];
-                b[4] = s.position[1];
-                b[8] = s.position[2];
-                b[12] = s.radius * s.radius;
-            }
+        for (uint32_t i = 0; i < count; ++i) {
+            const rt_sphere& s = spheres[i];
+            geom[i] = make_float4(s.position[0], s.position[1], s.position[2],
+                                  s.radius * s.radius);
         }
         // Queued launches may still read the old scene: order the copies on the stream,
         // and wait for them so the host staging vectors can be released.
@@ -183,6 +171,10 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
     p.band_step = nranks;
     p.local_bands = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
     fill_camera(p, *cam);
+    if (ctx->scan_mode == RT_SCAN_CULLED) {
+        const uint32_t padded = (count + 63u) & ~63u;   // <= count + 63 < count + kScanPad
+        p.lds_records = padded <= rtk::kLdsMaxRecords ? padded : 0u;
+    }
     const float4* src = reinterpret_cast<const float4*>(in);
     float4* dst = reinterpret_cast<float4*>(out);
     for (uint32_t f0 = 0; f0 < frames; f0 += rtk::kMaxFramesPerLaunch) {
@@ -192,7 +184,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         p.frames = nf;
         p.reset_first = (f0 == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
         std::memcpy(p.seeds, seeds + f0, nf * sizeof(float));
-        hipError_t e = rtk::launch_trace(p, stream);
+        hipError_t e = rtk::launch_trace(p, ctx->scan_mode, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         src = dst;  // later launches continue the accumulation in place
     }
@@ -235,6 +227,14 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->d_sph);
     }
     delete ctx;
+    return RT_OK;
+}
+
+rt_status rt_set_scan_mode(rt_ctx* ctx, int mode) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (mode != RT_SCAN_EXHAUSTIVE && mode != RT_SCAN_CULLED)
+        return fail(RT_ERR_INVALID_ARGUMENT, "unknown scan mode");
+    ctx->scan_mode = mode;
     return RT_OK;
 }
 

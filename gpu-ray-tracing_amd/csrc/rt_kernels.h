@@ -12,6 +12,8 @@ namespace rtk {
 // Seeds travel in the kernarg segment (no H2D copy, graph-capturable).  rt_render with
 // more frames is split into several launches that continue the accumulation.
 constexpr uint32_t kMaxFramesPerLaunch = 128;
+// Culled scan: lists up to this many spheres are staged in LDS (64 KiB per workgroup).
+constexpr uint32_t kLdsMaxRecords = 4096;
 
 // Everything the `update` kernel needs, passed by value (kernarg -> SGPRs).
 struct TraceParams {
@@ -23,19 +25,17 @@ struct TraceParams {
     uint32_t band_first, band_step, local_bands;  // stripe map (RT_STRIPE_ROWS rows/band)
     uint32_t frames;       // accumulation frames in this launch (1 = one `update`)
     uint32_t reset_first;  // camera_has_moved > 0.5 applies to frame 0 only
+    uint32_t lds_records;  // culled scan: records staged in LDS (0 = read from HBM/L2)
     float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3];
     float defocus_angle, max_depth, spp;
     float seeds[kMaxFramesPerLaunch];
 };
 
-hipError_t launch_trace(const TraceParams& p, hipStream_t stream);
+hipError_t launch_trace(const TraceParams& p, int scan_mode, hipStream_t stream);
 hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream);
 hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t width,
                                uint32_t height, uint32_t nranks, uint32_t max_local_rows,
                                hipStream_t stream);
 const char* trace_kernel_name();
-// Layout of TraceParams::geom the kernels expect: 0 = one float4 (cx,cy,cz,r*r) per
-// sphere; 1 = SoA blocks of 4 spheres {cx0..3, cy0..3, cz0..3, rr0..3}.
-int scan_layout();
 
 }  // namespace rtk

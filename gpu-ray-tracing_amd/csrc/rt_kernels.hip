@@ -21,6 +21,36 @@ namespace rtk {
 
 using namespace rtd;
 
+// ---- diagnostic phase stamps (RT_STAMPS=1 builds only; never in the product) ---------
+#ifndef RT_STAMPS
+#define RT_STAMPS 0
+#endif
+#if RT_STAMPS
+constexpr int kStampWaves = 65536;
+__device__ unsigned long long g_stamp[kStampWaves][8];
+__shared__ unsigned long long s_last[4], s_acc[4][8];
+__device__ __forceinline__ void stamp(int k) {
+    const unsigned w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        if (k == -2)
+            for (int i = 0; i < 8; ++i) s_acc[w][i] = i == 7 ? t : 0;  // [7] = entry time
+        if (k == 0 && s_acc[w][6] == 0) s_acc[w][6] = t - s_acc[w][7];  // entry -> 1st ray
+        if (k > 0) s_acc[w][k] += t - s_last[w];
+        if (k == 5) s_acc[w][7] = t - s_acc[w][7];                      // lifetime
+        s_last[w] = t;
+        if (k == 5) {
+            const unsigned gw = blockIdx.x * 4u + w;
+            if (gw < kStampWaves)
+                for (int i = 0; i < 8; ++i) g_stamp[gw][i] = s_acc[w][i];
+        }
+    }
+}
+#define STAMP(k) stamp(k)
+#else
+#define STAMP(k) ((void)0)
+#endif
+
 struct Hit {
     int idx;     // winning sphere, -1 = miss
     float t;     // its root
@@ -47,7 +77,8 @@ __device__ __forceinline__ float discriminant(const float4 g, v3 o, v3 d, float 
     return fmaf(h, h, -(a * c));                                        // wgsl:187
 }
 
-// Root selection of wgsl:189-201 for sphere i, given its discriminant.
+// Root selection of wgsl:189-201 for sphere i, given its discriminant.  (Callers only
+// pass indices < count.)
 __device__ __forceinline__ void consider(float disc, float h, float a, uint32_t i, float& tmax,
                                          int& idx) {
     if (!(disc < 0.0f)) {                                               // wgsl:189
@@ -67,91 +98,11 @@ __device__ __forceinline__ void consider(float disc, float h, float a, uint32_t 
 // with h*h >= +0 and a >= +0 cannot round to -0, so the test is one max-tree and one
 // compare per chunk (max_bits below).
 
-// Scan variant selection (compile-time, for A/B builds only; the product uses the
-// default).  0: one sphere per iteration; 1: chunks of 4 + prefetch + one test per chunk;
-// 2: as 1, but the records are staged in LDS once per workgroup (ds_read broadcast).
-#ifndef RT_SCAN_VARIANT
-#define RT_SCAN_VARIANT 1
-#endif
-
-#if RT_SCAN_VARIANT == 0
-__device__ __forceinline__ Hit scan_spheres(const float4* __restrict__ geom, uint32_t count,
-                                            v3 o, v3 d) {
-    const float a = dot(d, d);
-    float tmax = 0x1.05ed2ep+118f;
-    int idx = -1;
-    for (uint32_t i = 0; i < count; ++i) {
-        float h;
-        const float disc = discriminant(geom[i], o, d, a, h);
-        consider(disc, h, a, i, tmax, idx);
-    }
-    return Hit{idx, tmax};
-}
-#elif RT_SCAN_VARIANT == 3
-// Scan records in SoA blocks of 4 spheres (64 B = one s_load_dwordx16):
-//   {cx0..cx3, cy0..cy3, cz0..cz3, rr0..rr3}.
-// On gfx950 a VALU op with an SGPR operand issues at half rate (~4.2 vs ~2.3 cycles per
-// wave64 instruction, tools/valu_microbench.hip), while a packed op reading an SGPR pair
-// costs the same 4.2 cycles for two elements.  So the four SGPR-consuming ops per sphere
-// (oc = C - O and c = dot(oc,oc) - r*r) are issued as v_pk_add_f32 on sphere pairs, and
-// everything else runs as full-rate single-precision VGPR ops.
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ void disc_pair(f2v cx, f2v cy, f2v cz, f2v rr, v3 o, v3 d, float a,
-                                          float& h0, float& h1, float& d0, float& d1) {
-    const f2v ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
-    const f2v ocx = cx - ox, ocy = cy - oy, ocz = cz - oz;                   // wgsl:183
-    h0 = fmaf(ocz.x, d.z, fmaf(ocy.x, d.y, ocx.x * d.x));                    // wgsl:185
-    h1 = fmaf(ocz.y, d.z, fmaf(ocy.y, d.y, ocx.y * d.x));
-    f2v cc;
-    cc.x = fmaf(ocz.x, ocz.x, fmaf(ocy.x, ocy.x, ocx.x * ocx.x));
-    cc.y = fmaf(ocz.y, ocz.y, fmaf(ocy.y, ocy.y, ocx.y * ocx.y));
-    const f2v c = cc - rr;                                                   // wgsl:186
-    d0 = fmaf(h0, h0, -(a * c.x));                                           // wgsl:187
-    d1 = fmaf(h1, h1, -(a * c.y));
-}
-
-__device__ __forceinline__ Hit scan_spheres(const float4* __restrict__ geom4, uint32_t count,
-                                            v3 o, v3 d) {
-    const float a = dot(d, d);                 // wgsl:184 (ray-invariant)
-    float tmax = 0x1.05ed2ep+118f;             // 3.4e35 (wgsl:266)
-    int idx = -1;
-    const uint32_t nchunks = (count + 3u) >> 2;
-    // one zero block of padding after the last chunk keeps the prefetch in bounds
-    float4 c0 = geom4[0], c1 = geom4[1], c2 = geom4[2], c3 = geom4[3];
-    for (uint32_t k = 0; k < nchunks; ++k) {
-        const float4* nb = geom4 + 4u * (k + 1u);
-        const float4 n0 = nb[0], n1 = nb[1], n2 = nb[2], n3 = nb[3];
-        float h[4], dd[4];
-        disc_pair(f2v{c0.x, c0.y}, f2v{c1.x, c1.y}, f2v{c2.x, c2.y}, f2v{c3.x, c3.y}, o, d, a,
-                  h[0], h[1], dd[0], dd[1]);
-        disc_pair(f2v{c0.z, c0.w}, f2v{c1.z, c1.w}, f2v{c2.z, c2.w}, f2v{c3.z, c3.w}, o, d, a,
-                  h[2], h[3], dd[2], dd[3]);
-        const int m = max(max(__float_as_int(dd[0]), __float_as_int(dd[1])),
-                          max(__float_as_int(dd[2]), __float_as_int(dd[3])));
-        if (__builtin_expect(m > (int)0xFF800000, 0)) {
-            const uint32_t i0 = 4u * k;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (i0 + j < count) consider(dd[j], h[j], a, i0 + j, tmax, idx);
-        }
-        c0 = n0;
-        c1 = n1;
-        c2 = n2;
-        c3 = n3;
-    }
-    return Hit{idx, tmax};
-}
-#else
+// Exhaustive scan: the reference's linear walk over every sphere (wgsl:169-177).
 #ifndef RT_SCAN_CHUNK
 #define RT_SCAN_CHUNK 4
 #endif
-#ifndef RT_SCAN_PIN_LOADS
-#define RT_SCAN_PIN_LOADS 0
-#endif
-#ifndef RT_SCAN_ABLATE_RARE
-#define RT_SCAN_ABLATE_RARE 0
-#endif
+
 // max over the int32 views of K discriminants
 template <int K>
 __device__ __forceinline__ int max_bits(const float (&dd)[K]) {
@@ -161,55 +112,174 @@ __device__ __forceinline__ int max_bits(const float (&dd)[K]) {
     return m;
 }
 
-__device__ __forceinline__ Hit scan_spheres(const float4* __restrict__ geom, uint32_t count,
-                                            v3 o, v3 d) {
+__device__ __forceinline__ Hit scan_exhaustive(const float4* __restrict__ geom, uint32_t count,
+                                               v3 o, v3 d) {
     constexpr int K = RT_SCAN_CHUNK;
     const float a = dot(d, d);                 // wgsl:184 (ray-invariant)
     float tmax = 0x1.05ed2ep+118f;             // 3.4e35 (wgsl:266)
     int idx = -1;
-    const uint32_t nk = count - count % K;
-    // geom is padded with zero records, so the prefetch of the chunk after the last one
-    // stays inside the allocation.
+    // The record list is zero-padded to whole chunks plus one chunk more (rt_abi.cpp), so
+    // every chunk (and the one-ahead prefetch) is a full s_load_dwordx16; padding records
+    // are never accepted (consider() bounds the index).
     float4 cur[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) cur[k] = geom[k];
-    uint32_t i = 0;
-#if RT_SCAN_ABLATE_RARE
-    float sink = 0.0f;
-#endif
-    for (; i < nk; i += K) {
+    for (uint32_t i = 0; i < count; i += K) {
         float4 nxt[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) nxt[k] = geom[i + K + k];
-#if RT_SCAN_PIN_LOADS
-        __builtin_amdgcn_sched_barrier(0);
-#endif
         float hh[K], dd[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) dd[k] = discriminant(cur[k], o, d, a, hh[k]);
-#if RT_SCAN_ABLATE_RARE
-#pragma unroll
-        for (int k = 0; k < K; ++k) sink += dd[k] + hh[k];
-#else
         if (__builtin_expect(max_bits<K>(dd) > (int)0xFF800000, 0)) {
 #pragma unroll
-            for (int k = 0; k < K; ++k) consider(dd[k], hh[k], a, i + k, tmax, idx);
+            for (int k = 0; k < K; ++k)
+                if (i + k < count) consider(dd[k], hh[k], a, i + k, tmax, idx);
         }
-#endif
 #pragma unroll
         for (int k = 0; k < K; ++k) cur[k] = nxt[k];
     }
-#if RT_SCAN_ABLATE_RARE
-    if (sink == 12345.0f) idx = 0;
-#endif
-    for (; i < count; ++i) {
-        float h;
-        const float disc = discriminant(geom[i], o, d, a, h);
-        consider(disc, h, a, i, tmax, idx);
-    }
     return Hit{idx, tmax};
 }
+
+// ---- Exact wave-level culling --------------------------------------------------------
+//
+// The 64 rays of a wave (one 8x8 tile, plus lens offsets) are nearly coherent.  Bound all
+// of the wave's live rays by one double cone: apex = centroid of the origins, every
+// origin within r_O of it, every unit direction within angle theta of the axis A (either
+// sign).  For sphere (C, R) with v = C - apex, t = v.A, p = |v - tA|, every ray line is at
+// distance >= p cos(theta) - |t| sin(theta) - r_O from C.  In exact arithmetic
+// D = |d|^2 (R^2 - dist^2), and the f32 evaluation of wgsl:183-187 errs by less than
+// ~32 eps |d|^2 (|oc|^2 + R^2) (eps = 2^-24), so the computed D is certainly negative when
+// dist > R + m with m = 2.5e-3 (|oc| + |R|) >= 2.5x sqrt(16 eps)|oc| + sqrt(6 eps)|R|, and
+// |oc| <= |t| + p + r_O + d_max (DESIGN.md §5 has the derivation).
+// Such a sphere can never be the hit of any lane and is skipped; every other sphere goes
+// through the exact per-lane test in list order, so the closest-hit result (including
+// the first-index-wins tie rule) is bit-identical to the exhaustive scan.  One sphere
+// per lane is tested against the cone (64 spheres per VALU instruction); survivors are
+// picked from the ballot mask in increasing index order.  Non-finite or degenerate rays,
+// wide cones (theta >~ 60 deg, e.g. diffuse bounces) and short lists use the exhaustive
+// scan instead.
+constexpr uint32_t kCullMinSpheres = 32;
+
+// Wave-wide reductions on the VALU: row_ror DPP inside each 16-lane row, then the four
+// row results are read into SGPRs (v_readlane) and combined, so every lane receives the
+// same (uniform) value.  Rounding order does not matter here: the cone only needs to be
+// conservative, and the margins of cone_misses() dwarf these errors.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int kRowRor8 = 0x128, kRowRor4 = 0x124, kRowRor2 = 0x122, kRowRor1 = 0x121;
+__device__ __forceinline__ float lane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+    v += dpp<kRowRor8>(v);
+    v += dpp<kRowRor4>(v);
+    v += dpp<kRowRor2>(v);
+    v += dpp<kRowRor1>(v);
+    return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
+}
+__device__ __forceinline__ float wave_max(float v) {
+    v = fmaxf(v, dpp<kRowRor8>(v));
+    v = fmaxf(v, dpp<kRowRor4>(v));
+    v = fmaxf(v, dpp<kRowRor2>(v));
+    v = fmaxf(v, dpp<kRowRor1>(v));
+    return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
+}
+__device__ __forceinline__ bool finite3(v3 v) {
+    return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z);
+}
+
+struct Cone {
+    v3 apex, axis;
+    float cos_t, sin_t, r_o, d_max;
+};
+
+// Builds the cone of the live lanes' rays; false when culling cannot be used.  Must be
+// called with the whole wave active (it reduces across lanes).  The apex is the centroid
+// of the points q = o + d: for camera rays these are the sample points on the focus
+// plane, where the beam of a tile is narrowest; r_o bounds |q - apex| and d_max bounds
+// |d| (so |o - apex| <= r_o + d_max for the rounding margin).
+__device__ __forceinline__ bool wave_cone(v3 o, v3 d, bool live, Cone& k) {
+    const float dd = dot(d, d);
+    const v3 q = add(o, d);
+    const bool bad = live && !(finite3(o) && finite3(q) && dd > 0.0f && __builtin_isfinite(dd));
+    const unsigned long long lm = __ballot(live);
+    if (lm == 0ull || __ballot(bad)) return false;
+    // Axis and apex come from the first live lane (v_readlane: no cross-lane reduction);
+    // the half-angle, the apex radius and max |d| are then exact max-reductions.
+    const int L = (int)__builtin_ctzll(lm);
+    const float inv = rsqrtf(dd);
+    const v3 u = mk(d.x * inv, d.y * inv, d.z * inv);
+    k.axis = mk(lane_f(u.x, L), lane_f(u.y, L), lane_f(u.z, L));
+    k.apex = mk(lane_f(q.x, L), lane_f(q.y, L), lane_f(q.z, L));
+    const v3 du = sub(u, k.axis), dq = sub(q, k.apex);
+    const float s = wave_max(live ? __builtin_amdgcn_sqrtf(dot(du, du)) : 0.0f);  // chord
+    const float r = wave_max(live ? __builtin_amdgcn_sqrtf(dot(dq, dq)) : 0.0f);
+    const float dm = wave_max(live ? __builtin_amdgcn_sqrtf(dd) : 0.0f);
+    const float su = s * 1.001f + 1e-6f;
+    if (!(su < 1.0f)) return false;                                  // theta >~ 60 degrees
+    k.cos_t = 1.0f - 0.5f * su * su;
+    k.sin_t = su * __builtin_amdgcn_sqrtf(1.0f - 0.25f * su * su) * 1.001f;
+    k.r_o = r * 1.001f + 1e-6f * (fabsf(k.apex.x) + fabsf(k.apex.y) + fabsf(k.apex.z));
+    k.d_max = dm * 1.001f;
+    return true;
+}
+
+// True when sphere record g = (center, r*r) provably misses every ray of the cone.
+__device__ __forceinline__ bool cone_misses(const Cone& k, float4 g) {
+    const v3 v = mk(g.x - k.apex.x, g.y - k.apex.y, g.z - k.apex.z);
+    const float t = dot(v, k.axis);
+    const float p = __builtin_amdgcn_sqrtf(fmaxf(fmaf(-t, t, dot(v, v)), 0.0f));
+    const float at = fabsf(t), R = __builtin_amdgcn_sqrtf(g.w) * 1.0001f;
+    const float lhs = fmaf(p, k.cos_t, -at * k.sin_t) - k.r_o;
+    const float m = 2.5e-3f * (at + p + k.r_o + k.d_max + R);
+    return lhs > R + m;                                   // NaN anywhere -> keep
+}
+
+// Scan records staged in LDS by the workgroup (culled scan, lists up to kLdsMaxRecords).
+extern __shared__ float4 lds_recs[];
+
+// kLds: read the cull records from the workgroup's LDS copy (else from the global array);
+// both hold count records zero-padded to a multiple of 64.
+template <bool kLds>
+__device__ __forceinline__ Hit scan_culled(const float4* __restrict__ geom, uint32_t count,
+                                           v3 o, v3 d, bool live) {
+    const float4* recs = kLds ? lds_recs : geom;
+    Cone k;
+    if (count < kCullMinSpheres || !wave_cone(o, d, live, k))
+        return scan_exhaustive(geom, count, o, d);
+    STAMP(2);
+    const uint32_t lane = threadIdx.x & 63u;
+    const float a = dot(d, d);
+    float tmax = 0x1.05ed2ep+118f;
+    int idx = -1;
+#ifndef RT_CULL_READLANE
+#define RT_CULL_READLANE 0
 #endif
+    for (uint32_t base = 0; base < count; base += 64u) {
+        const float4 g = recs[base + lane];
+        const bool keep = (base + lane < count) && !cone_misses(k, g);
+        unsigned long long mask = __ballot(keep);
+        while (mask) {                                    // survivors, in index order
+            const int j = __builtin_ctzll(mask);
+            mask &= mask - 1ull;
+#if RT_CULL_READLANE
+            const float4 gs = make_float4(lane_f(g.x, j), lane_f(g.y, j), lane_f(g.z, j),
+                                          lane_f(g.w, j));
+#else
+            const float4 gs = recs[base + (uint32_t)j];   // broadcast read
+#endif
+            float h;
+            const float disc = discriminant(gs, o, d, a, h);
+            consider(disc, h, a, base + (uint32_t)j, tmax, idx);
+        }
+    }
+    STAMP(3);
+    return Hit{idx, tmax};
+}
 
 struct Cam {
     v3 center, vul, pdu, pdv, ddu, ddv;
@@ -238,17 +308,28 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
     d = sub(pc, o);
 }
 
-// ray_color (wgsl:261-297).
-__device__ __forceinline__ v3 ray_color(const TraceParams& p, const float4* __restrict__ geom,
-                                        const float4* __restrict__ sph, uint32_t depth, v3 o,
-                                        v3 d, uint32_t seed) {
+// ray_color (wgsl:261-297), executed by the whole wave: `live` marks the lanes whose path
+// is still being traced; the bounce loop runs while any lane is live, and a lane's
+// values are only updated while it is live, so each lane computes exactly its own
+// per-pixel result.
+template <bool kCull>
+__device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t depth, v3 o, v3 d,
+                                        uint32_t seed, bool live) {
     v3 cf = mk(1.0f, 1.0f, 1.0f);
+    bool black = false;
     for (uint32_t i = 0; i < depth; ++i) {
-        const Hit hit = scan_spheres(geom, p.count, o, d);
-        if (hit.idx < 0) break;                                   // wgsl:288-290
+        if (__ballot(live) == 0ull) break;
+        const Hit hit = !kCull          ? scan_exhaustive(p.geom, p.count, o, d)
+                        : p.lds_records ? scan_culled<true>(p.geom, p.count, o, d, live)
+                                        : scan_culled<false>(p.geom, p.count, o, d, live);
+        if (!live) continue;
+        if (hit.idx < 0) {                                        // wgsl:288-290
+            live = false;
+            continue;
+        }
         // Hit record of the winner (wgsl:205-218).
-        const float4 pr = sph[2 * hit.idx];       // position, radius
-        const float4 mat = sph[2 * hit.idx + 1];  // material color
+        const float4 pr = p.sph[2 * hit.idx];       // position, radius
+        const float4 mat = p.sph[2 * hit.idx + 1];  // material color
         const v3 C = mk(pr.x, pr.y, pr.z);
         const v3 hp = fmas(hit.t, d, o);
         const v3 outward = divs(sub(hp, C), pr.w);
@@ -263,7 +344,11 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, const float4* __re
             att = mk(mat.x, mat.y, mat.z);
         } else if (mat.w <= 1.0f) {                               // metal wgsl:95-100
             const v3 refl = fmas(mat.w, random_unit_vector(sb), normalize(reflect(d, n)));
-            if (!(dot(refl, n) > 0.0f)) return mk(0.0f, 0.0f, 0.0f);
+            if (!(dot(refl, n) > 0.0f)) {                         // wgsl:277-279
+                black = true;
+                live = false;
+                continue;
+            }
             nd = normalize(refl);
             att = mk(mat.x, mat.y, mat.z);
         } else {                                                  // dielectric wgsl:102-135
@@ -277,10 +362,11 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, const float4* __re
             const v3 dir = refl ? reflect(u, n) : refract(u, n, ratio);
             nd = normalize(dir);
         }
-        cf = mul(cf, att);
+        cf = mul(cf, att);                                        // wgsl:285-286
         o = hp;
         d = nd;
     }
+    if (black) return mk(0.0f, 0.0f, 0.0f);
     // Sky (wgsl:293-296): only normalize(d).y is used.
     const float uy = d.y / sqrtf(dot(d, d));
     const float a = 0.5f * (uy + 1.0f);
@@ -289,29 +375,84 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, const float4* __re
 }
 
 // One wave = one 8x8 tile of the (local) image; lanes are row-major inside the tile.
+// Control flow is wave-uniform down to the shading (the culled scan reduces across
+// lanes); per-lane conditions of the reference (n < spp, the image bounds) become the
+// `live` flag instead of branches.
+struct TileCoord {
+    uint32_t x, y;
+    size_t idx;
+    bool valid;
+};
+
+__device__ __forceinline__ TileCoord tile_coord(const TraceParams& p, uint32_t tile,
+                                                uint32_t tiles_x, uint32_t lane) {
+    const uint32_t lband = tile / tiles_x;
+    TileCoord t;
+    t.x = (tile - lband * tiles_x) * 8u + (lane & 7u);
+    const uint32_t gband = p.band_first + lband * p.band_step;
+    t.y = gband * RT_STRIPE_ROWS + (lane >> 3);
+    const uint32_t ly = lband * RT_STRIPE_ROWS + (lane >> 3);
+    t.valid = (t.x < p.width) && (t.y < p.height);
+    t.idx = (size_t)ly * p.width + t.x;
+    return t;
+}
+
+template <bool kCull>
+__device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& cam,
+                                              const TileCoord& tc, float4 acc) {
+    v3 c = mk(acc.x, acc.y, acc.z);                               // wgsl:339-341
+    uint32_t n = f2u(acc.w);
+    const uint32_t spp = f2u(p.spp);                              // wgsl:343
+    const uint32_t depth = f2u(p.max_depth);
+    const uint32_t hxy = hash(tc.x * 73u) ^ hash(tc.y * 51u);     // wgsl:309-310
+    for (uint32_t f = 0; f < p.frames; ++f) {
+        const uint32_t B = f2u(p.seeds[f] * 4294967296.0f);      // wgsl:311,353
+        if (f == 0 && p.reset_first) {                            // wgsl:345-350
+            c = mk(0.0f, 0.0f, 0.0f);
+            n = 0u;
+        }
+        const bool live = tc.valid && n < spp;                    // wgsl:352
+        if (__ballot(live) != 0ull) {
+            const uint32_t seed = 1u + n + B;
+            v3 o, d;
+            STAMP(0);
+            get_ray(cam, tc.x, tc.y, hxy, seed, B, o, d);
+            STAMP(1);
+            const v3 col = ray_color<kCull>(p, depth, o, d, seed + 1u, live);
+            STAMP(4);
+            if (live) {
+                const float k = (float)(n + 1u);                  // wgsl:356
+                c = mk(c.x + (col.x - c.x) / k, c.y + (col.y - c.y) / k,
+                       c.z + (col.z - c.z) / k);
+                n += 1u;
+            }
+        }
+        // The chained form stores f32(n) and reloads u32(.) each frame (wgsl:341,362).
+        n = f2u((float)n);
+    }
+    return make_float4(c.x, c.y, c.z, (float)n);                  // wgsl:362
+}
+
+// One workgroup = 4 waves = 4 consecutive tiles.  (A persistent grid that walks tiles
+// with the next tile's accumulator prefetched — into VGPRs, or into LDS with
+// global_load_lds — measured 15-50 % slower: the loop pushes the kernel past 64 VGPRs /
+// into scratch, and the hardware dispatcher already overlaps the waves' HBM phases.)
 #ifndef RT_TRACE_MIN_WAVES
 #define RT_TRACE_MIN_WAVES 8
 #endif
+template <bool kCull>
 __global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const TraceParams p) {
-#if RT_SCAN_VARIANT == 2
-    extern __shared__ float4 lds_geom[];
-    for (uint32_t j = threadIdx.x; j < p.count + 8u; j += blockDim.x) lds_geom[j] = p.geom[j];
-    __syncthreads();
-    const float4* scan_geom = lds_geom;
-#else
-    const float4* scan_geom = p.geom;
-#endif
+    // Culled scan: the workgroup stages the scan records (count padded to 64) in LDS once;
+    // the per-block cone test then reads them at LDS latency instead of L2 latency.
+    STAMP(-2);
+    if (kCull && p.lds_records) {
+        for (uint32_t j = threadIdx.x; j < p.lds_records; j += 256u) lds_recs[j] = p.geom[j];
+        __syncthreads();
+    }
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t tiles_x = (p.width + 7u) >> 3;
-    const uint32_t lband = tile / tiles_x;
-    if (lband >= p.local_bands) return;                // whole wave exits together
-    const uint32_t x = (tile - lband * tiles_x) * 8u + (lane & 7u);
-    const uint32_t gband = p.band_first + lband * p.band_step;
-    const uint32_t y = gband * RT_STRIPE_ROWS + (lane >> 3);
-    const uint32_t ly = lband * RT_STRIPE_ROWS + (lane >> 3);
-    const bool valid = (x < p.width) && (y < p.height);
-    const size_t idx = (size_t)ly * p.width + x;
+    const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (tile >= tiles_x * p.local_bands) return;                  // whole wave exits
 
     Cam cam;
     cam.center = mk(p.center[0], p.center[1], p.center[2]);
@@ -322,33 +463,12 @@ __global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const
     cam.ddv = mk(p.ddv[0], p.ddv[1], p.ddv[2]);
     cam.defocus_angle = p.defocus_angle;
 
+    const TileCoord tc = tile_coord(p, tile, tiles_x, lane);
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (valid) acc = p.in[idx];                                   // wgsl:339
-    v3 c = mk(acc.x, acc.y, acc.z);
-    uint32_t n = f2u(acc.w);
-    const uint32_t spp = f2u(p.spp);                              // wgsl:343
-    const uint32_t depth = f2u(p.max_depth);
-    const uint32_t hxy = hash(x * 73u) ^ hash(y * 51u);           // wgsl:309-310
-
-    for (uint32_t f = 0; f < p.frames; ++f) {
-        const uint32_t B = f2u(p.seeds[f] * 4294967296.0f);      // wgsl:311,353
-        if (f == 0 && p.reset_first) {                            // wgsl:345-350
-            c = mk(0.0f, 0.0f, 0.0f);
-            n = 0u;
-        }
-        if (n < spp) {                                            // wgsl:352
-            const uint32_t seed = 1u + n + B;
-            v3 o, d;
-            get_ray(cam, x, y, hxy, seed, B, o, d);
-            const v3 col = ray_color(p, scan_geom, p.sph, depth, o, d, seed + 1u);
-            const float k = (float)(n + 1u);                      // wgsl:356
-            c = mk(c.x + (col.x - c.x) / k, c.y + (col.y - c.y) / k, c.z + (col.z - c.z) / k);
-            n += 1u;
-        }
-        // The chained form stores f32(n) and reloads u32(.) each frame (wgsl:341,362).
-        n = f2u((float)n);
-    }
-    if (valid) p.out[idx] = make_float4(c.x, c.y, c.z, (float)n); // wgsl:362-363
+    if (tc.valid) acc = p.in[tc.idx];                             // wgsl:339
+    const float4 res = trace_pixel<kCull>(p, cam, tc, acc);
+    if (tc.valid) p.out[tc.idx] = res;                            // wgsl:363
+    STAMP(5);
 }
 
 __global__ __launch_bounds__(256) void rt_init_kernel(float4* __restrict__ out, uint64_t n) {
@@ -377,17 +497,15 @@ __global__ __launch_bounds__(256) void rt_deinterleave_kernel(const float4* __re
     }
 }
 
-hipError_t launch_trace(const TraceParams& p, hipStream_t stream) {
+hipError_t launch_trace(const TraceParams& p, int scan_mode, hipStream_t stream) {
     const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
-    const uint32_t blocks = (uint32_t)((tiles + 3u) / 4u);
+    const uint64_t blocks = (tiles + 3u) / 4u;
     if (blocks == 0) return hipSuccess;
-#if RT_SCAN_VARIANT == 2
-    const size_t lds = ((size_t)p.count + 8u) * sizeof(float4);
-    if (lds > 65536) return hipErrorInvalidValue;
-#else
-    const size_t lds = 0;
-#endif
-    hipLaunchKernelGGL(rt_trace_kernel, dim3(blocks), dim3(256), lds, stream, p);
+    if (scan_mode == RT_SCAN_CULLED)
+        hipLaunchKernelGGL(rt_trace_kernel<true>, dim3((uint32_t)blocks), dim3(256),
+                           (size_t)p.lds_records * sizeof(float4), stream, p);
+    else
+        hipLaunchKernelGGL(rt_trace_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, stream, p);
     return hipGetLastError();
 }
 
@@ -414,6 +532,25 @@ hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t wid
 
 const char* trace_kernel_name() { return "rt_trace_kernel"; }
 
-int scan_layout() { return RT_SCAN_VARIANT == 3 ? 1 : 0; }
+}  // namespace rtk
+
+#if RT_STAMPS
+// Diagnostic builds: summed cycles per phase (1 get_ray, 2 cone, 3 cull loop, 4 rest of
+// ray_color, 5 accumulate + store) over all waves since the last call; resets them.
+extern "C" __attribute__((visibility("default"))) int rt_diag_stamps(unsigned long long* out,
+                                                                     unsigned waves) {
+    // out[1..5]: summed phase cycles (get_ray, cone, cull loop, rest of ray_color,
+    // accumulate + store); out[6]: entry -> first ray; out[7]: wave lifetime.
+    static unsigned long long host[rtk::kStampWaves][8];
+    if (waves > (unsigned)rtk::kStampWaves) waves = rtk::kStampWaves;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(rtk::g_stamp), sizeof(host)) != hipSuccess) return 1;
+    for (int i = 0; i < 8; ++i) out[i] = 0;
+    for (unsigned wv = 0; wv < waves; ++wv)
+        for (int i = 1; i < 8; ++i) out[i] += host[wv][i];
+    return 0;
+}
+#endif
+
+namespace rtk {
 
 }  // namespace rtk

@@ -42,6 +42,8 @@ STATUS_NAMES = {
     6: "RT_ERR_INVALID_CONTEXT",
 }
 RT_STRIPE_ROWS = 8
+RT_SCAN_EXHAUSTIVE = 0
+RT_SCAN_CULLED = 1
 
 
 class SceneCameraC(ctypes.Structure):
@@ -88,6 +90,7 @@ _SIGS = {
     "rt_kernel_name": (ctypes.c_char_p, [ctypes.c_int]),
     "rt_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(P)]),
     "rt_destroy": (ctypes.c_int, [P]),
+    "rt_set_scan_mode": (ctypes.c_int, [P, ctypes.c_int]),
     "rt_set_spheres": (ctypes.c_int, [P, P, U32, P]),
     "rt_init_image": (ctypes.c_int, [P, P, U32, U32, P]),
     "rt_update": (ctypes.c_int, [P, P, P, U32, U32, P, P, U32, P]),

@@ -55,6 +55,7 @@ class ComputeShaderPipeline:
         _lib.call("rt_create", self.device, ctypes.byref(ctx))
         self._ctx = ctx
         self._sphere_keep = None
+        self.scan_mode = "culled"
 
     # ---- lifetime ---------------------------------------------------------------------
     def close(self) -> None:
@@ -87,6 +88,12 @@ class ComputeShaderPipeline:
         return torch.zeros((height, width, 4), dtype=torch.float32, device=self.torch_device)
 
     # ---- the plugin operations --------------------------------------------------------
+    def set_scan_mode(self, mode: str) -> None:
+        """"culled" (default, exact wave-level culling) or "exhaustive" (linear walk)."""
+        code = {"exhaustive": _lib.RT_SCAN_EXHAUSTIVE, "culled": _lib.RT_SCAN_CULLED}[mode]
+        _lib.call("rt_set_scan_mode", self._ctx, code)
+        self.scan_mode = mode
+
     def set_spheres(self, spheres: SphereCollection) -> None:
         p, n = self._spheres(spheres)
         _lib.call("rt_set_spheres", self._ctx, p, n, self._stream())

@@ -129,6 +129,16 @@ RT_API const char* rt_kernel_name(int which);
 RT_API rt_status rt_create(int device, rt_ctx** out_ctx);
 RT_API rt_status rt_destroy(rt_ctx* ctx);
 
+/* Sphere-list scan strategy of the trace kernel.  Both give bit-identical images.
+ *   RT_SCAN_EXHAUSTIVE  the reference's linear walk: every ray tests every sphere
+ *                       (wgsl:169-177).
+ *   RT_SCAN_CULLED      (default) exact wave-level culling: spheres that provably miss
+ *                       every ray of a 64-ray wave are skipped, the rest are tested
+ *                       exactly in list order. */
+#define RT_SCAN_EXHAUSTIVE 0
+#define RT_SCAN_CULLED 1
+RT_API rt_status rt_set_scan_mode(rt_ctx* ctx, int mode);
+
 /* Scene upload (explicit form of prepare_sphere_buffer, lib.rs:177-207).  The update
  * calls below also accept host spheres and upload them only when their bytes change. */
 RT_API rt_status rt_set_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,

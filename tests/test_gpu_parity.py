@@ -11,10 +11,12 @@ from conftest import bits_equal, load_golden
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def pipe(rt):
+@pytest.fixture(scope="module", params=["culled", "exhaustive"])
+def pipe(rt, request):
+    """Every parity test runs against both sphere-scan strategies."""
     assert torch.cuda.is_available(), "GPU tests need a HIP device"
     p = rt.ComputeShaderPipeline(0)
+    p.set_scan_mode(request.param)
     yield p
     p.close()
 
@@ -300,3 +302,45 @@ def test_full_size_properties(rt, pipe):
     out = pipe.new_image(w, h)
     pipe.deinterleave(gathered, out, w, h, n)
     assert torch.equal(out, full)
+
+
+def _random_scene(rng, n):
+    """Spheres of mixed sizes (incl. huge, tiny, zero and negative radii) and materials."""
+    s = np.zeros((n, 8), np.float32)
+    s[:, 0:3] = rng.uniform(-15, 15, (n, 3))
+    s[:, 1] = rng.uniform(-1, 4, n)
+    s[:, 3] = rng.choice([0.2, 0.5, 1.0, 3.0, 0.01, 0.0, -0.4], n)
+    kind = rng.integers(0, 3, n)
+    s[:, 4:7] = rng.uniform(0, 1, (n, 3))
+    s[:, 7] = np.where(kind == 0, -2.0, np.where(kind == 1, rng.uniform(0, 0.5, n), 2.0))
+    s[kind == 2, 4] = 1.5
+    s[0] = [0, -1000, 0, 1000, 0.5, 0.5, 0.5, -2]
+    return s
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_culled_scan_equals_exhaustive(rt, seed):
+    """Exactness of the wave-level culling: random cameras (position, fov, lens), random
+    scenes of 40-700 spheres, depth 1-6, several frames — bitwise equal to the exhaustive
+    linear scan on the full image."""
+    rng = np.random.default_rng(seed)
+    w, h = int(rng.integers(64, 400)), int(rng.integers(48, 300))
+    n = int(rng.integers(40, 700))
+    sc = rt.SphereCollection(_random_scene(rng, n))
+    s = rt.CameraSettings(field_of_view=float(rng.uniform(5, 120)),
+                          max_depth=int(rng.integers(1, 7)),
+                          defocus_angle=float(rng.choice([0.0, 0.6, 3.0])),
+                          focus_distance=float(rng.uniform(2, 20)),
+                          look_from=tuple(rng.uniform(-20, 20, 3)),
+                          look_at=tuple(rng.uniform(-3, 3, 3)))
+    cam = rt.SceneCamera.from_settings(s, w, h, float(rng.uniform()))
+    seeds = rt.frame_seeds(seed, 3)
+    out = {}
+    for mode in ("culled", "exhaustive"):
+        p = rt.ComputeShaderPipeline(0)
+        p.set_scan_mode(mode)
+        img = p.new_image(w, h)
+        p.render(img, img, w, h, cam, sc, seeds)
+        out[mode] = host(img)
+        p.close()
+    assert_same(out["culled"], out["exhaustive"])

@@ -1,0 +1,4 @@
+cd $GRAFT_REPO_ROOT
+for c in k3 k2; do for m in culled exhaustive; do
+RT_SCAN_MODE=$m RT_HIP_LIB=$GRAFT_REPO_ROOT/gpu-ray-tracing_amd/build/variants/librt_hip_st4.so timeout -k 10 120 python tools/time_kernel.py $c
+done; done

@@ -12,6 +12,8 @@ def main(cfg="k3", iters=40):
     w, h = int(g["width"]), int(g["height"])
     cam = rt.SceneCamera(g["camera"]); sc = rt.SphereCollection(g["spheres"])
     pipe = rt.ComputeShaderPipeline(0)
+    import os
+    pipe.set_scan_mode(os.environ.get('RT_SCAN_MODE', 'culled'))
     a, b = pipe.new_image(w, h), pipe.new_image(w, h)
     pipe.update(a, b, w, h, cam, sc); torch.cuda.synchronize()
     ok = hashlib.sha256(b.cpu().numpy().tobytes()).hexdigest() == str(g["sha256"]) if "sha256" in g else None
@@ -22,7 +24,16 @@ def main(cfg="k3", iters=40):
         evs[k][0].record(st); pipe.update(a, b, w, h, c2, sc); evs[k][1].record(st); a, b = b, a
     torch.cuda.synchronize()
     t = sorted(x.elapsed_time(y) * 1e3 for x, y in evs)
-    print(json.dumps({"cfg": cfg, "median_us": t[len(t) // 2], "min_us": t[0], "hash_ok": ok}))
+    L = rt._lib.lib()
+    stamps = None
+    if hasattr(L, "rt_diag_stamps"):
+        import ctypes
+        buf = (ctypes.c_ulonglong * 8)()
+        waves = ((w + 7) // 8) * ((h + 7) // 8)
+        L.rt_diag_stamps(buf, ctypes.c_uint(waves))
+        stamps = [round(buf[k] / waves, 1) for k in range(1, 8)]
+    print(json.dumps({"cfg": cfg, "median_us": t[len(t) // 2], "min_us": t[0], "hash_ok": ok,
+                      "stamps_cycles_per_wave": stamps}))
 
 if __name__ == "__main__":
     main(*(sys.argv[1:2] or ["k3"]))
