@@ -27,6 +27,13 @@ struct rt_ctx {
     uint32_t count = 0;
     bool valid = false;
     std::vector<rt_sphere> cached;  // bytes currently on the device
+    uint64_t scene_gen = 0;         // bumped on every sphere upload
+    // Per-tile candidate lists of camera rays (culled scan), valid for cand_key.
+    uint32_t* cand_cnt = nullptr;
+    uint32_t* cand_idx = nullptr;
+    float4* cand_rec = nullptr;
+    uint64_t cand_tiles = 0;        // allocated tiles
+    std::vector<unsigned char> cand_key;
 };
 
 namespace {
@@ -126,6 +133,73 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
     ctx->cached.assign(spheres, spheres + count);
     ctx->count = count;
     ctx->valid = true;
+    ctx->scene_gen++;
+    return RT_OK;
+}
+
+void free_candidates(rt_ctx* ctx) {
+    (void)hipFree(ctx->cand_cnt);
+    (void)hipFree(ctx->cand_idx);
+    (void)hipFree(ctx->cand_rec);
+    ctx->cand_cnt = nullptr;
+    ctx->cand_idx = nullptr;
+    ctx->cand_rec = nullptr;
+    ctx->cand_tiles = 0;
+    ctx->cand_key.clear();
+}
+
+// Makes the per-tile candidate lists current for p's camera geometry, image, stripes and
+// scene; rebuilds them (one small kernel) only when one of those changed.  The per-frame
+// fields (random_seed, camera_has_moved, samples_per_pixel, max_depth) are not part of
+// the key: the lists hold for every frame of a camera.
+rt_status ensure_candidates(rt_ctx* ctx, rtk::TraceParams& p, hipStream_t stream) {
+    struct Key {
+        float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3], defocus;
+        uint32_t w, h, first, step, bands;
+        uint64_t scene;
+    } key;
+    std::memset(&key, 0, sizeof(key));
+    std::memcpy(key.center, p.center, sizeof(key.center));
+    std::memcpy(key.vul, p.vul, sizeof(key.vul));
+    std::memcpy(key.pdu, p.pdu, sizeof(key.pdu));
+    std::memcpy(key.pdv, p.pdv, sizeof(key.pdv));
+    std::memcpy(key.ddu, p.ddu, sizeof(key.ddu));
+    std::memcpy(key.ddv, p.ddv, sizeof(key.ddv));
+    key.defocus = p.defocus_angle;
+    key.w = p.width;
+    key.h = p.height;
+    key.first = p.band_first;
+    key.step = p.band_step;
+    key.bands = p.local_bands;
+    key.scene = ctx->scene_gen;
+    const unsigned char* kb = reinterpret_cast<const unsigned char*>(&key);
+    const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
+    p.cand_k = rtk::kCandMax;
+    if (ctx->cand_key.size() != sizeof(key) ||
+        std::memcmp(ctx->cand_key.data(), kb, sizeof(key)) != 0) {
+        if (tiles > ctx->cand_tiles) {
+            if (ctx->cand_tiles) {
+                hipError_t e = hipStreamSynchronize(stream);  // old lists may be in use
+                if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+            }
+            free_candidates(ctx);
+            hipError_t e = hipMalloc(&ctx->cand_cnt, tiles * sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMalloc(&ctx->cand_idx, tiles * rtk::kCandMax * sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMalloc(&ctx->cand_rec, tiles * rtk::kCandMax * sizeof(float4));
+            if (e != hipSuccess) {
+                free_candidates(ctx);
+                return hip_fail(e, "hipMalloc(candidate lists)");
+            }
+            ctx->cand_tiles = tiles;
+        }
+        hipError_t e = rtk::launch_candidates(p, ctx->cand_cnt, ctx->cand_idx, ctx->cand_rec,
+                                              stream);
+        if (e != hipSuccess) return hip_fail(e, "rt_candidates_kernel launch");
+        ctx->cand_key.assign(kb, kb + sizeof(key));
+    }
+    p.cand_cnt = ctx->cand_cnt;
+    p.cand_idx = ctx->cand_idx;
+    p.cand_rec = ctx->cand_rec;
     return RT_OK;
 }
 
@@ -174,6 +248,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
     if (ctx->scan_mode == RT_SCAN_CULLED) {
         const uint32_t padded = (count + 63u) & ~63u;   // <= count + 63 < count + kScanPad
         p.lds_records = padded <= rtk::kLdsMaxRecords ? padded : 0u;
+        if (rt_status s = ensure_candidates(ctx, p, stream)) return s;
     }
     const float4* src = reinterpret_cast<const float4*>(in);
     float4* dst = reinterpret_cast<float4*>(out);
@@ -222,9 +297,10 @@ rt_status rt_destroy(rt_ctx* ctx) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     {
         DeviceGuard guard(ctx->device);
-        if (ctx->d_geom || ctx->d_sph) (void)hipDeviceSynchronize();
+        if (ctx->d_geom || ctx->d_sph || ctx->cand_cnt) (void)hipDeviceSynchronize();
         (void)hipFree(ctx->d_geom);
         (void)hipFree(ctx->d_sph);
+        free_candidates(ctx);
     }
     delete ctx;
     return RT_OK;

@@ -43,10 +43,10 @@ __device__ __forceinline__ uint32_t hash(uint32_t s) {
 __device__ __forceinline__ float rf(uint32_t v) { return (float)hash(v) * 0x1p-32f; }
 
 // WGSL u32(f32): truncate, saturate, NaN -> 0 (what v_cvt_u32_f32 does).
+// Branch-free (selects only): NaN and negatives go through fmaxf to 0.
 __device__ __forceinline__ uint32_t f2u(float f) {
-    if (!(f > 0.0f)) return 0u;
-    if (f >= 4294967296.0f) return 0xFFFFFFFFu;
-    return (uint32_t)f;
+    const uint32_t t = (uint32_t)fminf(fmaxf(f, 0.0f), 4294967040.0f);  // largest f32 < 2^32
+    return f >= 4294967296.0f ? 0xFFFFFFFFu : t;
 }
 
 // Canonical sin/cos: Cody-Waite by pi/2 in three parts, Cephes minimax.

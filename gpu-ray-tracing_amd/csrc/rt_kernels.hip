@@ -40,7 +40,7 @@ __device__ __forceinline__ void stamp(int k) {
         if (k == 5) s_acc[w][7] = t - s_acc[w][7];                      // lifetime
         s_last[w] = t;
         if (k == 5) {
-            const unsigned gw = blockIdx.x * 4u + w;
+            const unsigned gw = (blockIdx.y * gridDim.x + blockIdx.x) * 4u + w;
             if (gw < kStampWaves)
                 for (int i = 0; i < 8; ++i) g_stamp[gw][i] = s_acc[w][i];
         }
@@ -281,6 +281,75 @@ __device__ __forceinline__ Hit scan_culled(const float4* __restrict__ geom, uint
     return Hit{idx, tmax};
 }
 
+// ---- Per-tile candidate lists for camera rays -----------------------------------------
+//
+// Every camera ray of a tile passes through the tile's footprint on the focus plane
+// (pc = vul + pdu*sx + pdv*sy with sx in [x0, x0+8], sy in [y0, y0+8] for any jitter, since
+// rounding is monotonic) and through the lens disk (|o - center| <= |(px,py)| *
+// sqrt(|ddu|^2 + |ddv|^2)), whatever the frame seed.  That gives a cone valid for ALL
+// frames of a camera: apex = footprint centre Pc, r_O = footprint radius, axis =
+// Pc - center, sin(theta) <= (r_O + r_lens) / (|Pc - center| - r_O - r_lens).  Spheres
+// that cone_misses() rejects can never be hit by a camera ray of the tile; the others are
+// listed (records + indices, in index order) once per camera/scene by
+// rt_candidates_kernel, and each frame's camera rays test only that list.
+__device__ __forceinline__ float len3(v3 v) { return __builtin_amdgcn_sqrtf(dot(v, v)); }
+
+__device__ __forceinline__ bool tile_cone(const TraceParams& p, uint32_t tx, uint32_t lband,
+                                          Cone& k) {
+    const float x0 = (float)(tx * 8u);
+    const float y0 = (float)((p.band_first + lband * p.band_step) * RT_STRIPE_ROWS);
+    const v3 vul = mk(p.vul[0], p.vul[1], p.vul[2]), pdu = mk(p.pdu[0], p.pdu[1], p.pdu[2]),
+             pdv = mk(p.pdv[0], p.pdv[1], p.pdv[2]);
+    const v3 ctr = mk(p.center[0], p.center[1], p.center[2]);
+    const v3 pc = fmas(y0 + 4.0f, pdv, fmas(x0 + 4.0f, pdu, vul));
+    float rq = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const v3 q = fmas(y0 + (c & 2 ? 8.0f : 0.0f), pdv, fmas(x0 + (c & 1 ? 8.0f : 0.0f), pdu, vul));
+        rq = fmaxf(rq, len3(sub(q, pc)));
+    }
+    float rl = 0.0f;
+    if (p.defocus_angle > 0.0f) {
+        const v3 du = mk(p.ddu[0], p.ddu[1], p.ddu[2]), dv = mk(p.ddv[0], p.ddv[1], p.ddv[2]);
+        rl = __builtin_amdgcn_sqrtf(dot(du, du) + dot(dv, dv));
+    }
+    const float mag = fabsf(pc.x) + fabsf(pc.y) + fabsf(pc.z) + fabsf(ctr.x) + fabsf(ctr.y) +
+                      fabsf(ctr.z);
+    rq = rq * 1.001f + 1e-5f * mag;                 // f32 evaluation of pc and o = pc - d + d
+    rl = rl * 1.001f + 1e-5f * mag;
+    const v3 w = sub(pc, ctr);
+    const float L = len3(w), delta = rq + rl;
+    if (!(L > 4.0f * delta) || !__builtin_isfinite(L + mag)) return false;
+    k.axis = mk(w.x / L, w.y / L, w.z / L);
+    k.apex = pc;
+    k.sin_t = delta / (L - delta) * 1.01f;
+    k.cos_t = __builtin_amdgcn_sqrtf(1.0f - k.sin_t * k.sin_t) * 0.999f;
+    k.r_o = rq;
+    k.d_max = (L + delta) * 1.001f;
+    return true;
+}
+
+// Closest hit among a tile's listed spheres (records in index order, zero-padded to a
+// multiple of 4): the exhaustive chunk loop restricted to the list.
+__device__ __forceinline__ Hit scan_list(const float4* __restrict__ rec,
+                                         const uint32_t* __restrict__ ids, uint32_t n, v3 o,
+                                         v3 d) {
+    const float a = dot(d, d);
+    float tmax = 0x1.05ed2ep+118f;
+    int slot = -1;
+    for (uint32_t c = 0; c < n; c += 4) {
+        float hh[4], dd[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dd[k] = discriminant(rec[c + k], o, d, a, hh[k]);
+        if (max_bits<4>(dd) > (int)0xFF800000) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (c + k < n) consider(dd[k], hh[k], a, c + k, tmax, slot);
+        }
+    }
+    return Hit{slot < 0 ? -1 : (int)ids[slot], tmax};
+}
+
 struct Cam {
     v3 center, vul, pdu, pdv, ddu, ddv;
     float defocus_angle;
@@ -313,15 +382,21 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
 // values are only updated while it is live, so each lane computes exactly its own
 // per-pixel result.
 template <bool kCull>
-__device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t depth, v3 o, v3 d,
-                                        uint32_t seed, bool live) {
+__device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uint32_t depth,
+                                        v3 o, v3 d, uint32_t seed, bool live) {
+    // candidates of this tile's camera rays (kCandNone: no list, use the scans below)
+    const uint32_t ncand = (kCull && p.cand_k) ? p.cand_cnt[tile] : kCandNone;
     v3 cf = mk(1.0f, 1.0f, 1.0f);
     bool black = false;
     for (uint32_t i = 0; i < depth; ++i) {
         if (__ballot(live) == 0ull) break;
-        const Hit hit = !kCull          ? scan_exhaustive(p.geom, p.count, o, d)
-                        : p.lds_records ? scan_culled<true>(p.geom, p.count, o, d, live)
-                                        : scan_culled<false>(p.geom, p.count, o, d, live);
+        const Hit hit =
+            !kCull ? scan_exhaustive(p.geom, p.count, o, d)
+            : (i == 0 && ncand != kCandNone)
+                ? scan_list(p.cand_rec + (size_t)tile * p.cand_k,
+                            p.cand_idx + (size_t)tile * p.cand_k, ncand, o, d)
+            : p.lds_records ? scan_culled<true>(p.geom, p.count, o, d, live)
+                            : scan_culled<false>(p.geom, p.count, o, d, live);
         if (!live) continue;
         if (hit.idx < 0) {                                        // wgsl:288-290
             live = false;
@@ -384,11 +459,11 @@ struct TileCoord {
     bool valid;
 };
 
-__device__ __forceinline__ TileCoord tile_coord(const TraceParams& p, uint32_t tile,
-                                                uint32_t tiles_x, uint32_t lane) {
-    const uint32_t lband = tile / tiles_x;
+// Launch grid: blockIdx.y = local stripe band, blockIdx.x * 4 + wave = tile column.
+__device__ __forceinline__ TileCoord tile_coord(const TraceParams& p, uint32_t tx,
+                                                uint32_t lband, uint32_t lane) {
     TileCoord t;
-    t.x = (tile - lband * tiles_x) * 8u + (lane & 7u);
+    t.x = tx * 8u + (lane & 7u);
     const uint32_t gband = p.band_first + lband * p.band_step;
     t.y = gband * RT_STRIPE_ROWS + (lane >> 3);
     const uint32_t ly = lband * RT_STRIPE_ROWS + (lane >> 3);
@@ -399,7 +474,7 @@ __device__ __forceinline__ TileCoord tile_coord(const TraceParams& p, uint32_t t
 
 template <bool kCull>
 __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& cam,
-                                              const TileCoord& tc, float4 acc) {
+                                              uint32_t tile, const TileCoord& tc, float4 acc) {
     v3 c = mk(acc.x, acc.y, acc.z);                               // wgsl:339-341
     uint32_t n = f2u(acc.w);
     const uint32_t spp = f2u(p.spp);                              // wgsl:343
@@ -418,7 +493,7 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
             STAMP(0);
             get_ray(cam, tc.x, tc.y, hxy, seed, B, o, d);
             STAMP(1);
-            const v3 col = ray_color<kCull>(p, depth, o, d, seed + 1u, live);
+            const v3 col = ray_color<kCull>(p, tile, depth, o, d, seed + 1u, live);
             STAMP(4);
             if (live) {
                 const float k = (float)(n + 1u);                  // wgsl:356
@@ -442,17 +517,27 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 #endif
 template <bool kCull>
 __global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const TraceParams p) {
-    // Culled scan: the workgroup stages the scan records (count padded to 64) in LDS once;
-    // the per-block cone test then reads them at LDS latency instead of L2 latency.
     STAMP(-2);
-    if (kCull && p.lds_records) {
-        for (uint32_t j = threadIdx.x; j < p.lds_records; j += 256u) lds_recs[j] = p.geom[j];
-        __syncthreads();
-    }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tiles_x = (p.width + 7u) >> 3;
-    const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (tile >= tiles_x * p.local_bands) return;                  // whole wave exits
+    const uint32_t tx = blockIdx.x * 4u + (threadIdx.x >> 6), lband = blockIdx.y;
+    const bool wave_in = tx < tiles_x;
+    // Issue the accumulator load first: its HBM latency overlaps the rest of the setup.
+    const TileCoord tc = tile_coord(p, tx, lband, lane);
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (wave_in && tc.valid) acc = p.in[tc.idx];                  // wgsl:339
+    // Culled scan: the workgroup stages the scan records (count padded to 64) in LDS once;
+    // the per-block cone test then reads them at LDS latency instead of L2 latency.
+    if (kCull && p.lds_records) {
+        for (uint32_t j = threadIdx.x; j < p.lds_records; j += 512u) {
+            const float4 g0 = p.geom[j];
+            const float4 g1 = p.geom[j + 256u < p.lds_records ? j + 256u : j];
+            lds_recs[j] = g0;
+            if (j + 256u < p.lds_records) lds_recs[j + 256u] = g1;
+        }
+        __syncthreads();
+    }
+    if (!wave_in) return;                                         // whole wave exits
 
     Cam cam;
     cam.center = mk(p.center[0], p.center[1], p.center[2]);
@@ -463,12 +548,48 @@ __global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const
     cam.ddv = mk(p.ddv[0], p.ddv[1], p.ddv[2]);
     cam.defocus_angle = p.defocus_angle;
 
-    const TileCoord tc = tile_coord(p, tile, tiles_x, lane);
-    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (tc.valid) acc = p.in[tc.idx];                             // wgsl:339
-    const float4 res = trace_pixel<kCull>(p, cam, tc, acc);
+    const float4 res = trace_pixel<kCull>(p, cam, lband * tiles_x + tx, tc, acc);
     if (tc.valid) p.out[tc.idx] = res;                            // wgsl:363
     STAMP(5);
+}
+
+// One wave per tile: list the spheres the tile's camera rays can hit (see tile_cone).
+__global__ __launch_bounds__(256) void rt_candidates_kernel(const TraceParams p,
+                                                            uint32_t* __restrict__ cnt,
+                                                            uint32_t* __restrict__ ids,
+                                                            float4* __restrict__ rec) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t tiles_x = (p.width + 7u) >> 3;
+    const uint32_t tx = blockIdx.x * 4u + (threadIdx.x >> 6), lband = blockIdx.y;
+    if (tx >= tiles_x) return;
+    const uint32_t tile = lband * tiles_x + tx;
+    const uint32_t K = p.cand_k;
+    Cone k;
+    if (!tile_cone(p, tx, lband, k)) {
+        if (lane == 0) cnt[tile] = kCandNone;
+        return;
+    }
+    uint32_t n = 0;
+    for (uint32_t base = 0; base < p.count; base += 64u) {
+        const uint32_t i = base + lane;
+        const float4 g = p.geom[i < p.count ? i : 0u];
+        const bool keep = i < p.count && !cone_misses(k, g);
+        const unsigned long long mask = __ballot(keep);
+        if (keep) {
+            const uint32_t pos = n + __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+            if (pos < K) {
+                ids[(size_t)tile * K + pos] = i;
+                rec[(size_t)tile * K + pos] = g;
+            }
+        }
+        n += (uint32_t)__builtin_popcountll(mask);
+    }
+    // zero the chunk padding after the last record
+    const uint32_t pad = ((n + 3u) & ~3u) - n;
+    if (n <= K && lane < pad && n + lane < K)
+        rec[(size_t)tile * K + n + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (lane == 0) cnt[tile] = n <= K ? n : kCandNone;
 }
 
 __global__ __launch_bounds__(256) void rt_init_kernel(float4* __restrict__ out, uint64_t n) {
@@ -497,15 +618,28 @@ __global__ __launch_bounds__(256) void rt_deinterleave_kernel(const float4* __re
     }
 }
 
+// 256-thread workgroups: 4 waves = 4 tiles along a stripe band; grid (columns/4, bands).
+static dim3 tile_grid(const TraceParams& p) {
+    const uint32_t tiles_x = (p.width + 7u) >> 3;
+    return dim3((tiles_x + 3u) / 4u, p.local_bands);
+}
+
 hipError_t launch_trace(const TraceParams& p, int scan_mode, hipStream_t stream) {
-    const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
-    const uint64_t blocks = (tiles + 3u) / 4u;
-    if (blocks == 0) return hipSuccess;
+    const dim3 grid = tile_grid(p);
+    if (grid.x == 0 || grid.y == 0) return hipSuccess;
     if (scan_mode == RT_SCAN_CULLED)
-        hipLaunchKernelGGL(rt_trace_kernel<true>, dim3((uint32_t)blocks), dim3(256),
+        hipLaunchKernelGGL(rt_trace_kernel<true>, grid, dim3(256),
                            (size_t)p.lds_records * sizeof(float4), stream, p);
     else
-        hipLaunchKernelGGL(rt_trace_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL(rt_trace_kernel<false>, grid, dim3(256), 0, stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_candidates(const TraceParams& p, uint32_t* cnt, uint32_t* ids, float4* rec,
+                             hipStream_t stream) {
+    const dim3 grid = tile_grid(p);
+    if (grid.x == 0 || grid.y == 0) return hipSuccess;
+    hipLaunchKernelGGL(rt_candidates_kernel, grid, dim3(256), 0, stream, p, cnt, ids, rec);
     return hipGetLastError();
 }
 

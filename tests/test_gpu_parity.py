@@ -344,3 +344,48 @@ def test_culled_scan_equals_exhaustive(rt, seed):
         out[mode] = host(img)
         p.close()
     assert_same(out["culled"], out["exhaustive"])
+
+
+def test_candidate_lists_follow_camera_and_scene(rt, oracle):
+    """The per-tile camera-ray candidate lists are rebuilt when the camera geometry, the
+    scene or the stripe partition change, and reused across frames (seed, reset, spp)."""
+    w, h = 96, 64
+    p = rt.ComputeShaderPipeline(0)
+    p.set_scan_mode("culled")
+    sc = rt.synthetic_scene(300, seed=3)
+    cams = [camera(rt, w, h, depth=2, seed=0.125),
+            rt.SceneCamera.from_settings(rt.CameraSettings(look_from=(-9.0, 3.0, 7.0),
+                                                           max_depth=2), w, h, 0.625)]
+    for cam in cams + cams[:1]:
+        for seed in (0.25, 0.75):
+            c = cam.with_fields(random_seed=seed)
+            a, b = p.new_image(w, h), p.new_image(w, h)
+            p.update(a, b, w, h, c, sc)
+            want, _ = oracle.update(np.zeros((h, w, 4), np.float32), c.blob, sc.spheres)
+            assert_same(host(b), want)
+    p.close()
+
+
+def test_candidate_list_overflow_falls_back(rt):
+    """A tile whose camera rays can reach more spheres than a list holds (a dense cluster
+    straight ahead) uses the per-wave culled scan instead — still bit-exact."""
+    rng = np.random.default_rng(7)
+    n = 400
+    s = np.zeros((n, 8), np.float32)
+    s[:, 0:3] = rng.normal(0, 0.05, (n, 3)) + np.array([0, 1, 0], np.float32)
+    s[:, 3] = 0.01
+    s[:, 4:7] = 0.5
+    s[:, 7] = -2.0
+    s[0] = [0, -1000, 0, 1000, 0.5, 0.5, 0.5, -2]
+    sc = rt.SphereCollection(s)
+    w, h = 64, 64
+    cam = rt.SceneCamera.from_settings(rt.CameraSettings(field_of_view=3.0, max_depth=3), w, h, 0.5)
+    out = {}
+    for mode in ("culled", "exhaustive"):
+        p = rt.ComputeShaderPipeline(0)
+        p.set_scan_mode(mode)
+        img = p.new_image(w, h)
+        p.render(img, img, w, h, cam, sc, rt.frame_seeds(3, 2))
+        out[mode] = host(img)
+        p.close()
+    assert_same(out["culled"], out["exhaustive"])
