@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--scan", default="culled", choices=["culled", "exhaustive"],
                     help="sphere-list scan: exact wave-level culling (default) or the "
                          "reference's exhaustive linear walk; images are bit-identical")
-    ap.add_argument("--exhaustive-steps", type=int, default=10,
+    ap.add_argument("--exhaustive-steps", type=int, default=20,
                     help="also time the exhaustive-scan kernel for its FP32 roofline")
     ap.add_argument("--cpu-frames", type=float, default=2.0,
                     help="CPU baseline sample size in frames of the workload (0 = skip)")
@@ -111,11 +111,12 @@ def main():
     w, h, kind, nsph, depth, desc = CONFIGS[args.config]
     spheres = rt.SphereCollection.generate(kind, nsph, 1)
     frames = args.warmup + args.steps
-    seeds = rt.frame_seeds(FRAME_SEED, frames)
-    settings = rt.CameraSettings(max_depth=depth, samples_per_pixel=max(500, frames))
+    seeds = rt.frame_seeds(FRAME_SEED, frames + args.exhaustive_steps)
+    # spp cap above every frame this run traces (so no frame is a no-op)
+    settings = rt.CameraSettings(max_depth=depth,
+                                 samples_per_pixel=max(500, frames + args.exhaustive_steps))
     cam0 = rt.SceneCamera.from_settings(settings, w, h, float(seeds[0]))
-    cams = [cam0.with_fields(random_seed=float(seeds[f]),
-                             camera_has_moved=1.0 if f == 0 else 0.0) for f in range(frames)]
+    cams = [cam0.with_fields(camera_has_moved=1.0 if f == 0 else 0.0) for f in range(2)]
 
     pipe = rt.ComputeShaderPipeline(local_rank)
     pipe.set_scan_mode(args.scan)
@@ -124,21 +125,21 @@ def main():
     stream = torch.cuda.current_stream()
 
     # warmup (untimed) — frame 0 resets the accumulator (camera_has_moved = 1)
-    for f in range(args.warmup):
-        r.frame(cams[f], spheres, seeds[f:f + 1])
+    if args.warmup:
+        r.frames(cams[0], spheres, seeds[:args.warmup])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    # timed: `steps` progressive frames = `steps` update dispatches issued by one C call
+    # (rt_update_frames), then the single gather of the finished tiles.
+    cam_t = cams[min(1, frames - 1)]          # camera_has_moved = 0 from here on
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        f = args.warmup + k
-        ev[k][0].record(stream)
-        r.frame(cams[f], spheres, seeds[f:f + 1])
-        ev[k][1].record(stream)
+    ev0.record(stream)
+    r.frames(cam_t, spheres, seeds[args.warmup:])
+    ev1.record(stream)
     image = r.finish()
     torch.cuda.synchronize()
     if world > 1:
@@ -152,8 +153,8 @@ def main():
 
     # every pixel of the gathered image must hold exactly warmup + steps samples
     sample_ok = image is not None and bool(torch.all(image[..., 3] == frames).item())
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    launch_s = float(np.mean(kern_ms)) / 1e3
+    # HIP events around the timed dispatches: average per launch, inter-kernel gaps included
+    launch_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
     local_px = w * min(r.rows, h)
     # SURVEY §8d algorithmic units: the reference's exhaustive scan does N tests of 23 FLOP
     # per segment; at max_depth 1 every sample is exactly one segment.
@@ -165,16 +166,13 @@ def main():
     exh = None
     if args.scan == "culled" and flops and args.exhaustive_steps > 0:
         pipe.set_scan_mode("exhaustive")
-        e2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.exhaustive_steps)]
-        for k in range(args.exhaustive_steps):
-            f = args.warmup + k % args.steps
-            e2[k][0].record(stream)
-            r.frame(cams[f], spheres, seeds[f:f + 1])
-            e2[k][1].record(stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        r.frames(cam_t, spheres, seeds[frames:frames + args.exhaustive_steps])
+        e1.record(stream)
         torch.cuda.synchronize()
         pipe.set_scan_mode(args.scan)
-        t_exh = float(np.mean([a.elapsed_time(b) for a, b in e2])) / 1e3
+        t_exh = e0.elapsed_time(e1) / 1e3 / args.exhaustive_steps
         exh = {"kernel_avg_us": round(t_exh * 1e6, 2),
                "achieved": round(flops / t_exh / 1e12, 3), "peak": PEAK_FP32_TFLOPS,
                "unit": "TFLOP/s", "frac": round(flops / t_exh / 1e12 / PEAK_FP32_TFLOPS, 4),

@@ -217,24 +217,20 @@ void fill_camera(rtk::TraceParams& p, const rt_scene_camera& c) {
     p.spp = c.samples_per_pixel;
 }
 
-// Shared body of rt_update / rt_render / rt_render_stripes.
-rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h,
-                uint32_t rank, uint32_t nranks, const rt_scene_camera* cam,
-                const rt_sphere* spheres, uint32_t count, uint32_t frames,
-                const float* seeds, void* stream_v) {
+// Common setup of every trace launch: argument checks, scene upload, kernel parameters
+// (camera, stripe map, scan-mode data such as the candidate lists).
+rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint32_t h,
+                  uint32_t rank, uint32_t nranks, const rt_scene_camera* cam,
+                  const rt_sphere* spheres, uint32_t count, const float* seeds,
+                  hipStream_t stream, rtk::TraceParams& p) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     if (!in || !out || !cam) return fail(RT_ERR_INVALID_ARGUMENT, "NULL image or camera");
     if (rt_status s = check_image(w, h)) return s;
     if (nranks == 0 || rank >= nranks) return fail(RT_ERR_INVALID_ARGUMENT, "bad rank/nranks");
-    if (frames == 0) return RT_OK;
     if (!seeds) return fail(RT_ERR_INVALID_ARGUMENT, "random_seeds is NULL");
-    DeviceGuard guard(ctx->device);
-    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
-    hipStream_t stream = static_cast<hipStream_t>(stream_v);
     if (rt_status s = upload_spheres(ctx, spheres, count, stream)) return s;
 
     const uint32_t bands = (h + RT_STRIPE_ROWS - 1) / RT_STRIPE_ROWS;
-    rtk::TraceParams p;
     std::memset(&p, 0, sizeof(p));
     p.geom = ctx->d_geom;
     p.sph = ctx->d_sph;
@@ -246,10 +242,32 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
     p.local_bands = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
     fill_camera(p, *cam);
     if (ctx->scan_mode == RT_SCAN_CULLED) {
+        // Camera rays use the per-tile candidate lists; the LDS copy of the records only
+        // serves the per-wave cone culling of bounce rays, so it is skipped at depth <= 1
+        // (tiles without a list then read the records from L2).
         const uint32_t padded = (count + 63u) & ~63u;   // <= count + 63 < count + kScanPad
-        p.lds_records = padded <= rtk::kLdsMaxRecords ? padded : 0u;
+        const bool bounces = cam->max_depth >= 2.0f;
+        p.lds_records = (bounces && padded <= rtk::kLdsMaxRecords) ? padded : 0u;
         if (rt_status s = ensure_candidates(ctx, p, stream)) return s;
     }
+    return RT_OK;
+}
+
+// Shared body of rt_update / rt_render / rt_render_stripes: `frames` accumulated in
+// launches of up to kMaxFramesPerLaunch frames each.
+rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h,
+                uint32_t rank, uint32_t nranks, const rt_scene_camera* cam,
+                const rt_sphere* spheres, uint32_t count, uint32_t frames,
+                const float* seeds, void* stream_v) {
+    if (frames == 0) return ctx ? RT_OK : fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    hipStream_t stream = static_cast<hipStream_t>(stream_v);
+    rtk::TraceParams p;
+    if (rt_status s = prepare(ctx, in, out, w, h, rank, nranks, cam, spheres, count, seeds,
+                              stream, p))
+        return s;
     const float4* src = reinterpret_cast<const float4*>(in);
     float4* dst = reinterpret_cast<float4*>(out);
     for (uint32_t f0 = 0; f0 < frames; f0 += rtk::kMaxFramesPerLaunch) {
@@ -346,6 +364,35 @@ rt_status rt_render(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32
                     const rt_scene_camera* cam, const rt_sphere* spheres, uint32_t count,
                     uint32_t frames, const float* seeds, void* stream) {
     return trace(ctx, in, out, w, h, 0, 1, cam, spheres, count, frames, seeds, stream);
+}
+
+rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t w, uint32_t h,
+                           uint32_t rank, uint32_t nranks, const rt_scene_camera* cam,
+                           const rt_sphere* spheres, uint32_t count, uint32_t frames,
+                           const float* seeds, void* stream_v, int* out_newest) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (image_a == image_b) return fail(RT_ERR_INVALID_ARGUMENT, "image_a and image_b alias");
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    hipStream_t stream = static_cast<hipStream_t>(stream_v);
+    rtk::TraceParams p;
+    if (rt_status s = prepare(ctx, image_a, image_b, w, h, rank, nranks, cam, spheres, count,
+                              seeds, stream, p))
+        return s;
+    float4* img[2] = {reinterpret_cast<float4*>(image_a), reinterpret_cast<float4*>(image_b)};
+    int cur = 0;
+    p.frames = 1;
+    for (uint32_t f = 0; f < frames; ++f) {   // one `update` dispatch per frame
+        p.in = img[cur];
+        p.out = img[1 - cur];
+        p.reset_first = (f == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
+        p.seeds[0] = seeds[f];
+        hipError_t e = rtk::launch_trace(p, ctx->scan_mode, stream);
+        if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
+        cur = 1 - cur;
+    }
+    if (out_newest) *out_newest = cur;
+    return RT_OK;
 }
 
 uint32_t rt_stripe_local_rows(uint32_t height, uint32_t rank, uint32_t nranks) {

@@ -96,6 +96,8 @@ _SIGS = {
     "rt_update": (ctypes.c_int, [P, P, P, U32, U32, P, P, U32, P]),
     "rt_render": (ctypes.c_int, [P, P, P, U32, U32, P, P, U32, U32, P, P]),
     "rt_render_stripes": (ctypes.c_int, [P, P, P, U32, U32, U32, U32, P, P, U32, U32, P, P]),
+    "rt_update_frames": (ctypes.c_int, [P, P, P, U32, U32, U32, U32, P, P, U32, U32, P, P,
+                                        ctypes.POINTER(ctypes.c_int)]),
     "rt_stripe_local_rows": (U32, [U32, U32, U32]),
     "rt_deinterleave_stripes": (ctypes.c_int, [P, P, P, U32, U32, U32, P]),
     "rt_camera_settings_default": (None, [P]),

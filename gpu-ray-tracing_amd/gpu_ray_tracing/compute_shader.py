@@ -135,6 +135,24 @@ class ComputeShaderPipeline:
                   nranks, ctypes.byref(cam), p, n, s.size, s.ctypes.data_as(ctypes.c_void_p),
                   self._stream())
 
+    def update_frames(self, image_a: torch.Tensor, image_b: torch.Tensor, width: int,
+                      height: int, camera: SceneCamera, spheres: SphereCollection, seeds,
+                      rank: int = 0, nranks: int = 1) -> int:
+        """len(seeds) progressive `update` dispatches ping-ponging a -> b -> a ... (the
+        reference's per-frame loop, lib.rs:366-417); returns 0 if image_a holds the
+        result, 1 for image_b.  Frame 0 honours camera.camera_has_moved."""
+        rows = stripe_local_rows(height, rank, nranks) if nranks > 1 else height
+        _check_image(image_a, width, rows, "image_a")
+        _check_image(image_b, width, rows, "image_b")
+        cam = camera.to_c()
+        p, n = self._spheres(spheres)
+        s = np.ascontiguousarray(seeds, np.float32)
+        newest = ctypes.c_int(-1)
+        _lib.call("rt_update_frames", self._ctx, _ptr(image_a), _ptr(image_b), width, height,
+                  rank, nranks, ctypes.byref(cam), p, n, s.size,
+                  s.ctypes.data_as(ctypes.c_void_p), self._stream(), ctypes.byref(newest))
+        return newest.value
+
     def deinterleave(self, gathered: torch.Tensor, out: torch.Tensor, width: int, height: int,
                      nranks: int) -> None:
         rows = stripe_local_rows(height, 0, nranks)

@@ -56,6 +56,17 @@ class StripeRenderer:
                                      camera, spheres, seeds)
         self.cur = 1 - self.cur
 
+    def frames(self, camera, spheres, seeds) -> None:
+        """len(seeds) progressive frames, one `update` dispatch each, from a single call."""
+        if self.rows:
+            a, b = self.buf[self.cur], self.buf[1 - self.cur]
+            newest = self.pipe.update_frames(a, b, self.width, self.height, camera, spheres,
+                                             seeds, self.rank, self.world)
+            if newest == 1:
+                self.cur = 1 - self.cur
+        elif len(seeds) % 2:
+            self.cur = 1 - self.cur
+
     @property
     def local(self) -> torch.Tensor:
         return self.buf[self.cur]

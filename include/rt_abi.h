@@ -165,6 +165,20 @@ RT_API rt_status rt_render(rt_ctx* ctx, const float* in_rgba, float* out_rgba, u
                     const rt_sphere* spheres, uint32_t sphere_count, uint32_t frames,
                     const float* random_seeds, void* stream);
 
+/* The reference's per-frame loop (ComputeShaderNode ping-pong, lib.rs:366-374, 408-417)
+ * driven from C: `frames` separate progressive `update` dispatches alternating between
+ * image_a and image_b (frame f reads the image frame f-1 wrote; frame 0 reads image_a).
+ * Frame f uses random_seeds[f] and camera_has_moved = (f == 0 ? camera->camera_has_moved
+ * : 0).  Restricted to the stripe bands of rank/nranks (nranks = 1: whole image; images
+ * are then compact local buffers as for rt_render_stripes).  *out_newest receives 0 if
+ * image_a holds the result, 1 for image_b.  One call = `frames` kernel launches with no
+ * per-frame host round trip. */
+RT_API rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t width,
+                                  uint32_t height, uint32_t rank, uint32_t nranks,
+                                  const rt_scene_camera* camera, const rt_sphere* spheres,
+                                  uint32_t sphere_count, uint32_t frames,
+                                  const float* random_seeds, void* stream, int* out_newest);
+
 /* Multi-GPU tile path: the same as rt_render (frames >= 1) restricted to the stripe
  * bands of `rank` out of `nranks` (RT_STRIPE_ROWS rows each, band s -> rank s % nranks).
  * in/out are compact local images of width x rt_stripe_local_rows(height,rank,nranks). */

@@ -389,3 +389,33 @@ def test_candidate_list_overflow_falls_back(rt):
         out[mode] = host(img)
         p.close()
     assert_same(out["culled"], out["exhaustive"])
+
+
+@pytest.mark.parametrize("nranks", [1, 3])
+def test_update_frames_equals_chained_updates(rt, pipe, nranks):
+    """rt_update_frames (the per-frame dispatch loop in C) == chained rt_update calls, for
+    the whole image and for stripe ranks (compact local buffers)."""
+    w, h = 56, 40
+    sc = rt.synthetic_scene(120)
+    seeds = rt.frame_seeds(21, 5)
+    cam = camera(rt, w, h, depth=2)
+    full_a, full_b = pipe.new_image(w, h), pipe.new_image(w, h)
+    cur, nxt = full_a, full_b
+    for f in range(5):
+        pipe.update(cur, nxt, w, h, cam.with_fields(random_seed=float(seeds[f]),
+                                                   camera_has_moved=1.0 if f == 0 else 0.0), sc)
+        cur, nxt = nxt, cur
+    want = host(cur)
+    rows0 = rt.stripe_local_rows(h, 0, nranks)
+    got = np.zeros((h, w, 4), np.float32)
+    for r in range(nranks):
+        a, b = pipe.new_image(w, rows0), pipe.new_image(w, rows0)
+        newest = pipe.update_frames(a, b, w, h, cam, sc, seeds, r, nranks)
+        img = host(a if newest == 0 else b)
+        rows = rt.stripe_local_rows(h, r, nranks)
+        for lr in range(rows):
+            band = r + (lr // 8) * nranks
+            y = band * 8 + lr % 8
+            if y < h:
+                got[y] = img[lr]
+    assert_same(got, want)
