@@ -63,28 +63,62 @@ def parse():
                          "reference's exhaustive linear walk; images are bit-identical")
     ap.add_argument("--exhaustive-steps", type=int, default=20,
                     help="also time the exhaustive-scan kernel for its FP32 roofline")
-    ap.add_argument("--cpu-frames", type=float, default=2.0,
-                    help="CPU baseline sample size in frames of the workload (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="CPU baseline budget in seconds (0 = skip)")
     return ap.parse_args()
 
 
-def cpu_baseline(cam, spheres, w, h, frames):
-    """Scalar C oracle, one thread, on `frames` x (a row subset of) the same workload."""
+def host_threads():
+    """Host cores for the threaded baseline: this process's CPU set, at most 16 (the GPU
+    box's per-GPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_model():
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cam, spheres, w, h, seconds):
+    """The scalar C oracle on the same frame: (i) one thread on a row band
+    sized to ~seconds/3, (ii) host_threads() threads over 8-row bands of whole frames
+    for ~2*seconds/3.  The threaded run is the reported value."""
     from oracle import oracle as O
-    rows = max(1, int(round(h * min(frames, 1.0))))
-    reps = max(1, int(round(frames))) if frames >= 1 else 1
     img = np.zeros((h, w, 4), np.float32)
     O.lib()
+    # single thread: calibrate on 8 rows through the middle of the image, then size the band
+    mid = (h // 2) & ~7
     t0 = time.perf_counter()
-    segs = 0
-    for _ in range(reps):
-        _, s = O.update(img, cam.blob, spheres.spheres, rows=(0, rows))
-        segs += s
+    O.update(img, cam.blob, spheres.spheres, rows=(mid, mid + 8))
+    per_row = (time.perf_counter() - t0) / 8
+    rows1 = int(min(h, max(8, seconds / 3 / max(per_row, 1e-9)))) & ~7 or 8
+    y0 = max(0, (h - rows1) // 2) & ~7
+    t0 = time.perf_counter()
+    O.update(img, cam.blob, spheres.spheres, rows=(y0, y0 + rows1))
+    single = rows1 * w / (time.perf_counter() - t0) / 1e6
+    # threaded: whole frames
+    T = host_threads()
+    frames = max(1, int(round(2 * seconds / 3 / (w * h / (single * 1e6 * T)))))
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        O.update_parallel(img, cam.blob, spheres.spheres, T)
     dt = time.perf_counter() - t0
-    rays = rows * w * reps
-    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} x {w}x{rows} progressive update(s) of the same scene/camera, "
-                      f"scalar C oracle (oracle/rt_oracle.c, gcc -O3), 1 thread, {dt:.1f} s"}
+    return {"value": round(w * h * frames / dt / 1e6, 3), "unit": "Mrays/s", "cores": T,
+            "kind": "port",
+            "sample": f"{frames} full {w}x{h} update(s) on {T} threads (8-row bands from a "
+                      f"queue), {dt:.1f} s; scalar C oracle (oracle/rt_oracle.c, gcc -O3)",
+            "single_thread": {"value": round(single, 3), "cores": 1,
+                              "sample": f"{w}x{rows1} rows of one update"},
+            "cpu_model": cpu_model()}
 
 
 def load_pmc(config):
@@ -138,7 +172,7 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    r.frames(cam_t, spheres, seeds[args.warmup:])
+    r.frames(cam_t, spheres, seeds[args.warmup:frames])
     ev1.record(stream)
     image = r.finish()
     torch.cuda.synchronize()
@@ -179,6 +213,24 @@ def main():
                "flop_per_launch": flops,
                "speedup_of_culled": round(t_exh / launch_s, 2)}
 
+    # Presentation kernel on the gathered image: 16 B read + 4 B written per
+    # pixel, HBM-bound.
+    present = None
+    if image is not None:
+        out8 = torch.empty((h, w, 4), dtype=torch.uint8, device=image.device)
+        pipe.present(image, w, h, "srgb", out8)
+        p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        p0.record(stream)
+        for _ in range(20):
+            pipe.present(image, w, h, "srgb", out8)
+        p1.record(stream)
+        torch.cuda.synchronize()
+        t_p = p0.elapsed_time(p1) / 1e3 / 20
+        present = {"kernel": "rt_present_kernel<srgb>", "avg_us": round(t_p * 1e6, 2),
+                   "achieved": round(w * h * 20 / t_p / 1e9, 1), "peak": PEAK_HBM_GBS,
+                   "unit": "GB/s", "frac": round(w * h * 20 / t_p / 1e9 / PEAK_HBM_GBS, 4),
+                   "bytes_per_launch": w * h * 20}
+
     if args.scan == "exhaustive" and flops:
         roof = {"bound": "valu", "achieved": round(flops / launch_s / 1e12, 3),
                 "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
@@ -215,10 +267,11 @@ def main():
                        "kernel": rt._lib.lib().rt_kernel_name(0).decode()},
             "roofline": roof,
             "fp32_exhaustive_scan": exh,
+            "present_rgba8": present,
             "accumulated_spp_ok": sample_ok,
         }
-        if world == 1 and args.cpu_frames > 0:
-            line["cpu_baseline"] = cpu_baseline(cams[0], spheres, w, h, args.cpu_frames)
+        if world == 1 and args.cpu_seconds > 0:
+            line["cpu_baseline"] = cpu_baseline(cams[0], spheres, w, h, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

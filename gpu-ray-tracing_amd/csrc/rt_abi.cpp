@@ -9,6 +9,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -34,6 +35,16 @@ struct rt_ctx {
     float4* cand_rec = nullptr;
     uint64_t cand_tiles = 0;        // allocated tiles
     std::vector<unsigned char> cand_key;
+    // Sample count each recently written image holds (if uniform), by device pointer: the
+    // trace kernel's speculation hint (TraceParams::n_hint).  Only a hint — a stale entry
+    // costs a second pass over the mismatching lanes, never a different image.
+    struct Hint {
+        const void* buf = nullptr;
+        uint32_t n = 0;
+    };
+    Hint hints[8];
+    uint32_t hint_next = 0;
+    float* d_srgb = nullptr;  // rt_srgb_thresholds table on the device (256 floats)
 };
 
 namespace {
@@ -66,6 +77,48 @@ struct DeviceGuard {
 constexpr uint32_t kMaxDim = 1u << 16;         // 65536 x 65536 texels
 constexpr uint32_t kMaxSpheres = 1u << 20;
 constexpr uint32_t kScanPad = 68;  // >= chunk round-up + one chunk + a 64-lane block
+
+// WGSL u32(f32) on the host (truncate, saturate, NaN -> 0), as rtd::f2u.
+uint32_t host_f2u(float f) {
+    if (!(f > 0.0f)) return 0u;
+    if (f >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)f;
+}
+
+uint32_t hint_for(const rt_ctx* ctx, const void* buf) {
+    for (const auto& e : ctx->hints)
+        if (e.buf == buf && buf != nullptr) return e.n;
+    return rtk::kNoHint;
+}
+
+void set_hint(rt_ctx* ctx, const void* buf, uint32_t n) {
+    for (auto& e : ctx->hints)
+        if (e.buf == buf) {
+            e.n = n;
+            if (n == rtk::kNoHint) e.buf = nullptr;
+            return;
+        }
+    if (n == rtk::kNoHint) return;
+    auto& e = ctx->hints[ctx->hint_next++ % (sizeof(ctx->hints) / sizeof(ctx->hints[0]))];
+    e.buf = buf;
+    e.n = n;
+}
+
+// Count after `frames` updates of a pixel that held n (wgsl:352-362): +1 per frame below spp.
+uint32_t advance_count(uint32_t n, uint32_t frames, uint32_t spp) {
+    if (n == rtk::kNoHint || n >= spp) return n;
+    const uint64_t m = (uint64_t)n + frames;
+    const uint32_t r = m < spp ? (uint32_t)m : spp;
+    return r < (1u << 24) ? r : rtk::kNoHint;  // beyond 2^24 the f32 round trip differs
+}
+
+// Sets p.n_hint for a launch of nf frames reading `in` and records the count `out` will
+// hold.
+void apply_hint(rt_ctx* ctx, rtk::TraceParams& p, const void* in, const void* out, uint32_t nf) {
+    const uint32_t n_in = p.reset_first ? 0u : hint_for(ctx, in);
+    p.n_hint = p.reset_first ? rtk::kNoHint : n_in;
+    set_hint(ctx, out, advance_count(n_in, nf, host_f2u(p.spp)));
+}
 
 rt_status check_image(uint32_t w, uint32_t h) {
     if (w == 0 || h == 0 || w > kMaxDim || h > kMaxDim)
@@ -277,6 +330,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         p.frames = nf;
         p.reset_first = (f0 == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
         std::memcpy(p.seeds, seeds + f0, nf * sizeof(float));
+        apply_hint(ctx, p, src, dst, nf);
         hipError_t e = rtk::launch_trace(p, ctx->scan_mode, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         src = dst;  // later launches continue the accumulation in place
@@ -318,6 +372,7 @@ rt_status rt_destroy(rt_ctx* ctx) {
         if (ctx->d_geom || ctx->d_sph || ctx->cand_cnt) (void)hipDeviceSynchronize();
         (void)hipFree(ctx->d_geom);
         (void)hipFree(ctx->d_sph);
+        (void)hipFree(ctx->d_srgb);
         free_candidates(ctx);
     }
     delete ctx;
@@ -347,7 +402,9 @@ rt_status rt_init_image(rt_ctx* ctx, float* out, uint32_t w, uint32_t h, void* s
     if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
     hipError_t e = rtk::launch_init(reinterpret_cast<float4*>(out), (uint64_t)w * h,
                                     static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? RT_OK : hip_fail(e, "rt_init_kernel launch");
+    if (e != hipSuccess) return hip_fail(e, "rt_init_kernel launch");
+    set_hint(ctx, out, 0u);
+    return RT_OK;
 }
 
 rt_status rt_update(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h,
@@ -387,6 +444,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         p.out = img[1 - cur];
         p.reset_first = (f == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
         p.seeds[0] = seeds[f];
+        apply_hint(ctx, p, p.in, p.out, 1);
         hipError_t e = rtk::launch_trace(p, ctx->scan_mode, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         cur = 1 - cur;
@@ -421,7 +479,49 @@ rt_status rt_deinterleave_stripes(rt_ctx* ctx, const float* gathered, float* out
     hipError_t e = rtk::launch_deinterleave(
         reinterpret_cast<const float4*>(gathered), reinterpret_cast<float4*>(out), w, h,
         nranks, rt_stripe_local_rows(h, 0, nranks), static_cast<hipStream_t>(stream));
+    set_hint(ctx, out, rtk::kNoHint);
     return e == hipSuccess ? RT_OK : hip_fail(e, "rt_deinterleave_kernel launch");
+}
+
+void rt_srgb_thresholds(float out[256]) {
+    out[0] = 0.0f;
+    for (int j = 1; j < 256; ++j) {
+        const double v = (j - 0.5) / 255.0;  // encoded boundary between j-1 and j
+        const double lin = v <= 0.04045 ? v / 12.92 : std::pow((v + 0.055) / 1.055, 2.4);
+        float f = (float)lin;
+        if ((double)f < lin) f = std::nextafter(f, 2.0f);
+        out[j] = f;
+    }
+}
+
+rt_status rt_present_rgba8(rt_ctx* ctx, const float* in, uint8_t* out, uint32_t w, uint32_t h,
+                           int encoding, void* stream_v) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!in || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL image");
+    if (encoding != RT_ENCODE_LINEAR && encoding != RT_ENCODE_SRGB)
+        return fail(RT_ERR_INVALID_ARGUMENT, "unknown encoding");
+    if (rt_status s = check_image(w, h)) return s;
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    hipStream_t stream = static_cast<hipStream_t>(stream_v);
+    if (encoding == RT_ENCODE_SRGB && !ctx->d_srgb) {
+        float t[256];
+        rt_srgb_thresholds(t);
+        float* d = nullptr;
+        hipError_t e = hipMalloc(&d, sizeof(t));
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(sRGB table)");
+        e = hipMemcpy(d, t, sizeof(t), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(d);
+            return hip_fail(e, "hipMemcpy(sRGB table)");
+        }
+        ctx->d_srgb = d;
+    }
+    hipError_t e = rtk::launch_present(reinterpret_cast<const float4*>(in),
+                                       reinterpret_cast<uchar4*>(out), (uint64_t)w * h,
+                                       encoding == RT_ENCODE_SRGB ? ctx->d_srgb : nullptr,
+                                       stream);
+    return e == hipSuccess ? RT_OK : hip_fail(e, "rt_present_kernel launch");
 }
 
 }  // extern "C"

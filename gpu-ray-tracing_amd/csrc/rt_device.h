@@ -68,9 +68,9 @@ __device__ __forceinline__ void sincos_c(float x, float& s, float& c) {
     c = ((k + 1) & 2) ? -c0 : c0;
 }
 
-// wgsl:234-243
-__device__ __forceinline__ v3 random_unit_vector(uint32_t seed) {
-    const float z = fmaf(2.0f, rf(seed), -1.0f);
+// wgsl:234-243; rf_seed = rf(seed)
+__device__ __forceinline__ v3 random_unit_vector(float rf_seed, uint32_t seed) {
+    const float z = fmaf(2.0f, rf_seed, -1.0f);
     const float a = rf(seed + 1u) * 0x1.921fb6p+2f;  // 6.283185307 as f32
     const float r = sqrtf(fmaf(-z, z, 1.0f));
     float sa, ca;

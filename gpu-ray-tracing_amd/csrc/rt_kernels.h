@@ -16,6 +16,7 @@ constexpr uint32_t kMaxFramesPerLaunch = 128;
 constexpr uint32_t kLdsMaxRecords = 4096;
 // Per-tile candidate lists of camera rays (culled scan): capacity and the "no list" mark.
 constexpr uint32_t kCandMax = 32;
+constexpr uint32_t kNoHint = 0xFFFFFFFFu;
 constexpr uint32_t kCandNone = 0xFFFFFFFFu;
 
 // Everything the `update` kernel needs, passed by value (kernarg -> SGPRs).
@@ -30,6 +31,7 @@ struct TraceParams {
     uint32_t reset_first;  // camera_has_moved > 0.5 applies to frame 0 only
     uint32_t lds_records;  // culled scan: records staged in LDS (0 = read from HBM/L2)
     uint32_t cand_k;       // per-tile candidate list capacity (0 = no lists)
+    uint32_t n_hint;       // expected sample count of `in` (kNoHint = unknown), see trace_pixel
     const uint32_t* cand_cnt;  // [tile] listed spheres, kCandNone = no list
     const uint32_t* cand_idx;  // [tile][cand_k] sphere indices, ascending
     const float4* cand_rec;    // [tile][cand_k] their scan records
@@ -46,6 +48,10 @@ hipError_t launch_candidates(const TraceParams& p, uint32_t* cnt, uint32_t* ids,
 hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t width,
                                uint32_t height, uint32_t nranks, uint32_t max_local_rows,
                                hipStream_t stream);
+// 8-bit presentation of a float image (rt_present_rgba8); srgb_t = device T[256] or null
+// for the linear encoding.
+hipError_t launch_present(const float4* in, uchar4* out, uint64_t texels,
+                          const float* srgb_t, hipStream_t stream);
 const char* trace_kernel_name();
 
 }  // namespace rtk

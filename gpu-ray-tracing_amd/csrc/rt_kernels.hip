@@ -402,23 +402,28 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
             live = false;
             continue;
         }
-        // Hit record of the winner (wgsl:205-218).
+        // Hit record of the winner (wgsl:205-218).  The two record loads are per-lane and
+        // depend on the scan; the scatter's random numbers do not depend on the material
+        // (lambertian and metal draw random_unit_vector(sb), dielectric draws rf(sb), its
+        // first component), so they are computed while the loads are in flight.
         const float4 pr = p.sph[2 * hit.idx];       // position, radius
         const float4 mat = p.sph[2 * hit.idx + 1];  // material color
-        const v3 C = mk(pr.x, pr.y, pr.z);
+        const uint32_t sb = hash(seed + i * 1000u);               // wgsl:268
+        const float r_sb = rf(sb);
+        const v3 ruv = random_unit_vector(r_sb, sb);
         const v3 hp = fmas(hit.t, d, o);
+        const v3 C = mk(pr.x, pr.y, pr.z);
         const v3 outward = divs(sub(hp, C), pr.w);
         const bool front = dot(d, outward) < 0.0f;
         const v3 n = front ? outward : neg(outward);
-        const uint32_t sb = hash(seed + i * 1000u);               // wgsl:268
         v3 att, nd;
         if (mat.w < -1.0f) {                                      // lambertian wgsl:84-93
-            v3 dir = add(n, random_unit_vector(sb));
+            v3 dir = add(n, ruv);
             if (dot(dir, dir) < 0x1.0c6f7ap-20f) dir = n;
             nd = dir;
             att = mk(mat.x, mat.y, mat.z);
         } else if (mat.w <= 1.0f) {                               // metal wgsl:95-100
-            const v3 refl = fmas(mat.w, random_unit_vector(sb), normalize(reflect(d, n)));
+            const v3 refl = fmas(mat.w, ruv, normalize(reflect(d, n)));
             if (!(dot(refl, n) > 0.0f)) {                         // wgsl:277-279
                 black = true;
                 live = false;
@@ -433,7 +438,7 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
             const float cos_t = fminf(dot(neg(u), n), 1.0f);
             const float sin_t = sqrtf(fmaf(-cos_t, cos_t, 1.0f));
             const bool cannot = ratio * sin_t > 1.0f;
-            const bool refl = cannot || reflectance(cos_t, ratio) > rf(sb);
+            const bool refl = cannot || reflectance(cos_t, ratio) > r_sb;
             const v3 dir = refl ? reflect(u, n) : refract(u, n, ratio);
             nd = normalize(dir);
         }
@@ -472,40 +477,66 @@ __device__ __forceinline__ TileCoord tile_coord(const TraceParams& p, uint32_t t
     return t;
 }
 
+// The accumulator's sample count n selects the pixel's random numbers (seed = 1 + n + B),
+// so the whole sample depends on the HBM load of `in`.  When the host knows the count the
+// image should hold (p.n_hint: every pixel of a progressive render has the same count),
+// frame 0 is traced with that count while the load is in flight and verified against the
+// loaded count afterwards; lanes whose count differs are traced again with the loaded
+// count (a second pass of the loop).  Results are identical to the non-speculative order.
 template <bool kCull>
 __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& cam,
                                               uint32_t tile, const TileCoord& tc, float4 acc) {
-    v3 c = mk(acc.x, acc.y, acc.z);                               // wgsl:339-341
-    uint32_t n = f2u(acc.w);
+    // st = the pixel's state: colour in xyz, f32(count) in w (wgsl:339-341, 362); it holds
+    // the loaded accumulator until `known`, then the accumulated state.
+    float4 st = acc;
+    bool known = false;
     const uint32_t spp = f2u(p.spp);                              // wgsl:343
     const uint32_t depth = f2u(p.max_depth);
     const uint32_t hxy = hash(tc.x * 73u) ^ hash(tc.y * 51u);     // wgsl:309-310
     for (uint32_t f = 0; f < p.frames; ++f) {
         const uint32_t B = f2u(p.seeds[f] * 4294967296.0f);      // wgsl:311,353
         if (f == 0 && p.reset_first) {                            // wgsl:345-350
-            c = mk(0.0f, 0.0f, 0.0f);
-            n = 0u;
+            st = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            known = true;
         }
-        const bool live = tc.valid && n < spp;                    // wgsl:352
-        if (__ballot(live) != 0ull) {
-            const uint32_t seed = 1u + n + B;
-            v3 o, d;
-            STAMP(0);
-            get_ray(cam, tc.x, tc.y, hxy, seed, B, o, d);
-            STAMP(1);
-            const v3 col = ray_color<kCull>(p, tile, depth, o, d, seed + 1u, live);
-            STAMP(4);
-            if (live) {
-                const float k = (float)(n + 1u);                  // wgsl:356
-                c = mk(c.x + (col.x - c.x) / k, c.y + (col.y - c.y) / k,
-                       c.z + (col.z - c.z) / k);
-                n += 1u;
+        if (p.n_hint == kNoHint) known = true;
+        uint32_t n_try = known ? f2u(st.w) : p.n_hint;
+        bool pending = tc.valid;
+        for (;;) {
+            const bool live = pending && n_try < spp;             // wgsl:352
+            v3 col = mk(0.0f, 0.0f, 0.0f);
+            if (__ballot(live) != 0ull) {
+                const uint32_t seed = 1u + n_try + B;
+                v3 o, d;
+                STAMP(0);
+                get_ray(cam, tc.x, tc.y, hxy, seed, B, o, d);
+                STAMP(1);
+                const v3 cl = ray_color<kCull>(p, tile, depth, o, d, seed + 1u, live);
+                STAMP(4);
+                if (live) col = cl;
             }
+            uint32_t n = f2u(st.w);
+            bool wrong = false;
+            if (!known) {                                         // verify the guess
+                known = true;
+                wrong = pending && n != n_try;
+            }
+            if (pending && !wrong) {
+                if (n < spp) {
+                    const float k = (float)(n + 1u);              // wgsl:356
+                    st.x = st.x + (col.x - st.x) / k;
+                    st.y = st.y + (col.y - st.y) / k;
+                    st.z = st.z + (col.z - st.z) / k;
+                    n += 1u;
+                }
+                st.w = (float)n;                                  // wgsl:362
+            }
+            if (__ballot(wrong) == 0ull) break;
+            pending = wrong;                                      // retrace these lanes
+            n_try = n;
         }
-        // The chained form stores f32(n) and reloads u32(.) each frame (wgsl:341,362).
-        n = f2u((float)n);
     }
-    return make_float4(c.x, c.y, c.z, (float)n);                  // wgsl:362
+    return st;
 }
 
 // One workgroup = 4 waves = 4 consecutive tiles.  (A persistent grid that walks tiles
@@ -522,10 +553,7 @@ __global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     const uint32_t tx = blockIdx.x * 4u + (threadIdx.x >> 6), lband = blockIdx.y;
     const bool wave_in = tx < tiles_x;
-    // Issue the accumulator load first: its HBM latency overlaps the rest of the setup.
     const TileCoord tc = tile_coord(p, tx, lband, lane);
-    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (wave_in && tc.valid) acc = p.in[tc.idx];                  // wgsl:339
     // Culled scan: the workgroup stages the scan records (count padded to 64) in LDS once;
     // the per-block cone test then reads them at LDS latency instead of L2 latency.
     if (kCull && p.lds_records) {
@@ -538,6 +566,9 @@ __global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const
         __syncthreads();
     }
     if (!wave_in) return;                                         // whole wave exits
+    // Unconditional load (texel 0 for lanes outside the image): no branch joins on it, so
+    // its first use — after the traced sample when p.n_hint is set — is where it is waited.
+    const float4 acc = p.in[tc.valid ? tc.idx : 0];               // wgsl:339
 
     Cam cam;
     cam.center = mk(p.center[0], p.center[1], p.center[2]);
@@ -618,6 +649,36 @@ __global__ __launch_bounds__(256) void rt_deinterleave_kernel(const float4* __re
     }
 }
 
+// rt_present_rgba8: one texel per lane per step, 16 B in / 4 B out.  The sRGB boundary
+// table (1 KB) is staged in LDS; each channel is a branch-free 8-step binary search.
+template <bool kSrgb>
+__global__ __launch_bounds__(256) void rt_present_kernel(const float4* __restrict__ in,
+                                                         uchar4* __restrict__ out,
+                                                         uint64_t texels,
+                                                         const float* __restrict__ srgb_t) {
+    __shared__ float T[256];
+    if (kSrgb) {
+        T[threadIdx.x] = srgb_t[threadIdx.x];
+        __syncthreads();
+    }
+    auto enc = [&](float c) -> uint32_t {
+        if (kSrgb) {
+            uint32_t k = 0;
+#pragma unroll
+            for (uint32_t s = 128; s >= 1; s >>= 1)
+                k += (c >= T[k + s]) ? s : 0u;   // NaN compares false -> 0
+            return k;
+        }
+        const float v = fminf(fmaxf(c, 0.0f), 1.0f);  // fmaxf(NaN, 0) = 0
+        return (uint32_t)(v * 255.0f + 0.5f);
+    };
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < texels;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const float4 v = in[i];
+        out[i] = make_uchar4((uint8_t)enc(v.x), (uint8_t)enc(v.y), (uint8_t)enc(v.z), 255);
+    }
+}
+
 // 256-thread workgroups: 4 waves = 4 tiles along a stripe band; grid (columns/4, bands).
 static dim3 tile_grid(const TraceParams& p) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
@@ -661,6 +722,20 @@ hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t wid
     if (blocks > 8192u) blocks = 8192u;
     hipLaunchKernelGGL(rt_deinterleave_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream,
                        gathered, out, width, height, nranks, max_local_rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_present(const float4* in, uchar4* out, uint64_t texels,
+                          const float* srgb_t, hipStream_t stream) {
+    if (texels == 0) return hipSuccess;
+    uint64_t blocks = (texels + 255u) / 256u;
+    if (blocks > 16384u) blocks = 16384u;
+    if (srgb_t)
+        hipLaunchKernelGGL(rt_present_kernel<true>, dim3((uint32_t)blocks), dim3(256), 0,
+                           stream, in, out, texels, srgb_t);
+    else
+        hipLaunchKernelGGL(rt_present_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0,
+                           stream, in, out, texels, srgb_t);
     return hipGetLastError();
 }
 

@@ -7,8 +7,9 @@ importing this package does not load it; the first call does, and raises if it i
 """
 from . import _lib
 from .camera import CameraSettings, SceneCamera
+from . import image_io
 from .compute_shader import (RT_STRIPE_ROWS, ComputeShaderImages, ComputeShaderNode,
-                             ComputeShaderPipeline, stripe_local_rows)
+                             ComputeShaderPipeline, srgb_thresholds, stripe_local_rows)
 from .scene import (SCENE_DEFAULT, SCENE_N, SCENE_THREE, SphereCollection,
                     create_default_spheres, frame_seeds, synthetic_scene, three_spheres)
 
@@ -18,5 +19,5 @@ __all__ = [
     "CameraSettings", "SceneCamera", "ComputeShaderPipeline", "ComputeShaderImages",
     "ComputeShaderNode", "SphereCollection", "create_default_spheres", "synthetic_scene",
     "three_spheres", "frame_seeds", "stripe_local_rows", "RT_STRIPE_ROWS", "RtError",
-    "SCENE_THREE", "SCENE_DEFAULT", "SCENE_N",
+    "SCENE_THREE", "SCENE_DEFAULT", "SCENE_N", "srgb_thresholds", "image_io",
 ]

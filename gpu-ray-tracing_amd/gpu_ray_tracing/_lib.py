@@ -44,6 +44,8 @@ STATUS_NAMES = {
 RT_STRIPE_ROWS = 8
 RT_SCAN_EXHAUSTIVE = 0
 RT_SCAN_CULLED = 1
+RT_ENCODE_LINEAR = 0
+RT_ENCODE_SRGB = 1
 
 
 class SceneCameraC(ctypes.Structure):
@@ -108,6 +110,8 @@ _SIGS = {
     "rt_driver_destroy": (ctypes.c_int, [P]),
     "rt_driver_frame": (ctypes.c_int, [P, P, P, U32, P, ctypes.POINTER(ctypes.c_int)]),
     "rt_driver_state": (ctypes.c_int, [P]),
+    "rt_present_rgba8": (ctypes.c_int, [P, P, P, U32, U32, ctypes.c_int, P]),
+    "rt_srgb_thresholds": (None, [P]),
 }
 
 _lib = None
@@ -123,6 +127,8 @@ def lib() -> ctypes.CDLL:
                                f"`make -C {PKG_ROOT}` (no CPU fallback exists)")
         handle = ctypes.CDLL(str(path))
         for name, (res, args) in _SIGS.items():
+            if "RT_HIP_LIB" in os.environ and not hasattr(handle, name):
+                continue  # an older experiment build (tools/ab_variants.py)
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

@@ -162,6 +162,28 @@ class ComputeShaderPipeline:
                   height, nranks, self._stream())
 
 
+    def present(self, image: torch.Tensor, width: int, height: int,
+                encoding: str = "srgb", out: torch.Tensor | None = None) -> torch.Tensor:
+        """8-bit RGBA of a float image (rt_present_rgba8), a (H, W, 4) uint8 device tensor:
+        what the reference's sprite shows (lib.rs:79-102), ready for a PNG."""
+        _check_image(image, width, height, "image")
+        code = {"linear": _lib.RT_ENCODE_LINEAR, "srgb": _lib.RT_ENCODE_SRGB}[encoding]
+        if out is None:
+            out = torch.empty((height, width, 4), dtype=torch.uint8, device=self.torch_device)
+        if out.dtype != torch.uint8 or not out.is_contiguous() or out.numel() < width * height * 4:
+            raise ValueError("out must be contiguous uint8 with width*height*4 elements")
+        _lib.call("rt_present_rgba8", self._ctx, _ptr(image), _ptr(out), width, height, code,
+                  self._stream())
+        return out
+
+
+def srgb_thresholds() -> np.ndarray:
+    """The 256-entry f32 boundary table of the sRGB encoding (rt_srgb_thresholds)."""
+    t = np.zeros(256, np.float32)
+    _lib.lib().rt_srgb_thresholds(t.ctypes.data_as(ctypes.c_void_p))
+    return t
+
+
 class ComputeShaderImages:
     """texture_a / texture_b (lib.rs:60-93, 138-142): two zero-filled RGBA32F images."""
 

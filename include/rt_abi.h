@@ -196,6 +196,22 @@ RT_API rt_status rt_deinterleave_stripes(rt_ctx* ctx, const float* gathered, flo
                                   uint32_t width, uint32_t height, uint32_t nranks,
                                   void* stream);
 
+/* Presentation (replaces the sprite of lib.rs:79-102, which shows the newest
+ * Rgba32Float image on the window): quantizes the accumulator's mean colour to 8-bit RGBA
+ * for an image file.  out_rgba8 is a device buffer of width*height*4 bytes, row 0 = top
+ * (the image's row order, wgsl:336).  Per channel c of (r, g, b):
+ *   RT_ENCODE_LINEAR: u8 = floor(min(max(c, 0), 1) * 255 + 0.5)   (f32 mul, then add)
+ *   RT_ENCODE_SRGB:   u8 = number of j in 1..255 with c >= T[j], T = rt_srgb_thresholds
+ *                     (sRGB transfer curve, exact quantization boundaries)
+ * NaN -> 0; alpha = 255.  The float image itself (.npy/PFM) needs no conversion. */
+#define RT_ENCODE_LINEAR 0
+#define RT_ENCODE_SRGB 1
+RT_API rt_status rt_present_rgba8(rt_ctx* ctx, const float* in_rgba, uint8_t* out_rgba8,
+                                  uint32_t width, uint32_t height, int encoding, void* stream);
+/* T[0] = 0 (unused); T[j], j = 1..255: the smallest f32 >= the linear value whose sRGB
+ * encoding is (j - 0.5) / 255, computed in double (IEC 61966-2-1 curve). */
+RT_API void rt_srgb_thresholds(float out[256]);
+
 /* ------------------------------------------------------------------------------------ */
 /* Host-side mirror of the reference's main-world code (C++ implementation, no device)   */
 /* ------------------------------------------------------------------------------------ */

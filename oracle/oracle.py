@@ -100,6 +100,28 @@ def update(inp: np.ndarray, camera: np.ndarray, spheres: np.ndarray,
     return out, int(segs)
 
 
+def update_parallel(inp: np.ndarray, camera: np.ndarray, spheres: np.ndarray, threads: int,
+                    rows: tuple[int, int] | None = None, band: int = 8) -> tuple[np.ndarray, int]:
+    """`update` over rows [y0, y1) with `threads` host threads pulling 8-row bands from a
+    shared queue (ctypes releases the GIL during each C call).  Same image as update()."""
+    from concurrent.futures import ThreadPoolExecutor
+    inp = _f32(inp)
+    h, w, _ = inp.shape
+    out = inp.copy()
+    cam = _f32(camera).reshape(44)
+    sph = _f32(spheres).reshape(-1, 8)
+    y0, y1 = rows if rows else (0, h)
+    L = lib()
+
+    def run(b0):
+        return int(L.oracle_update_rows(_p(inp), _p(out), w, h, b0, min(b0 + band, y1),
+                                        _p(cam), _p(sph), sph.shape[0]))
+
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
+        segs = sum(ex.map(run, range(y0, y1, band)))
+    return out, segs
+
+
 def render_pixels(state: np.ndarray, px, py, camera: np.ndarray, spheres: np.ndarray,
                   seeds) -> tuple[np.ndarray, int]:
     """`frames` chained updates for a list of pixels (contract of rt_render)."""

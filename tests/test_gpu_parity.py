@@ -419,3 +419,71 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks):
             if y < h:
                 got[y] = img[lr]
     assert_same(got, want)
+
+
+def test_stale_sample_count_hint_is_exact(rt, oracle, pipe):
+    """The library traces frame 0 with the sample count it expects `in` to hold and
+    retraces the lanes whose loaded count differs (rt_abi.cpp apply_hint, trace_pixel):
+    images written behind its back (wrong hint) and mixed per-pixel counts stay exact."""
+    w, h = 67, 45
+    sc = rt.create_default_spheres(3)
+    rng = np.random.default_rng(7)
+    a, b = pipe.new_image(w, h), pipe.new_image(w, h)
+    pipe.init_image(a, w, h)                      # the library now expects count 0 in `a`
+    counts = rng.integers(0, 6, (h, w, 1)).astype(np.float32)
+    counts[::3, ::2] = 0.0                        # some lanes match the hint, most do not
+    counts[5, 7], counts[6, 8], counts[7, 9] = np.nan, 2.5, -3.0
+    state = np.concatenate([rng.random((h, w, 3), np.float32), counts], axis=2)
+    a.copy_(to_dev(state))                        # written behind the library's back
+    cam = camera(rt, w, h, depth=3, spp=4, moved=False, seed=0.40625)
+    pipe.update(a, b, w, h, cam, sc)
+    want, _ = oracle.update(state, cam.blob, sc.spheres)
+    assert_same(host(b), want)
+    # b's hint (1) is wrong for every pixel; a fused 3-frame render continues from it
+    seeds = np.array([0.125, 0.5, 0.875], np.float32)
+    pipe.render(b, a, w, h, cam, sc, seeds)
+    cur = want
+    for s in seeds:
+        cur, _ = oracle.update(cur, cam.with_fields(random_seed=float(s)).blob, sc.spheres)
+    assert_same(host(a), cur)
+
+
+@pytest.mark.parametrize("encoding", ["linear", "srgb"])
+def test_present_matches_restatement(rt, pipe, encoding):
+    """rt_present_rgba8 == the numpy restatement: every threshold neighbour,
+    special values, and a rendered image."""
+    from oracle import present_ref as P
+    t = P.srgb_thresholds()
+    vals = np.concatenate([t, np.nextafter(t, np.float32(-1)), np.nextafter(t, np.float32(2)),
+                           np.float32([np.nan, np.inf, -np.inf, -0.0, 1.0, 1.5, -2.0]),
+                           np.linspace(-0.1, 1.1, 1000, dtype=np.float32)]).astype(np.float32)
+    n = vals.size
+    w = 64
+    h = (n + w * 3 - 1) // (w * 3)
+    img = np.zeros(h * w * 4, np.float32).reshape(h, w, 4)
+    flat = np.resize(vals, h * w * 3).reshape(h, w, 3)
+    img[..., :3] = flat
+    got = host(pipe.present(to_dev(img), w, h, encoding))
+    np.testing.assert_array_equal(got, P.present(img, encoding))
+    # a rendered frame
+    w, h = 96, 64
+    sc = rt.create_default_spheres(5)
+    cam = camera(rt, w, h, depth=4, seed=0.25)
+    a, b = pipe.new_image(w, h), pipe.new_image(w, h)
+    pipe.update(a, b, w, h, cam, sc)
+    np.testing.assert_array_equal(host(pipe.present(b, w, h, encoding)),
+                                  P.present(host(b), encoding))
+
+
+def test_image_files_from_device(rt, pipe, tmp_path):
+    w, h = 40, 24
+    sc = rt.three_spheres()
+    cam = camera(rt, w, h, depth=3, seed=0.75)
+    a, b = pipe.new_image(w, h), pipe.new_image(w, h)
+    pipe.update(a, b, w, h, cam, sc)
+    rt.image_io.save_png(tmp_path / "f.png", pipe.present(b, w, h))
+    rt.image_io.save_npy(tmp_path / "f.npy", b)
+    from oracle import present_ref as P
+    np.testing.assert_array_equal(rt.image_io.load_png(tmp_path / "f.png"),
+                                  P.present(host(b), "srgb"))
+    assert np.load(tmp_path / "f.npy").tobytes() == host(b).tobytes()

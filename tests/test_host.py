@@ -21,7 +21,7 @@ def header_functions():
 
 def test_library_exports_every_declared_symbol(rt):
     declared = header_functions()
-    assert len(declared) == 22
+    assert len(declared) == 24
     nm = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True,
                         text=True, check=True).stdout
     exported = set(re.findall(r" T (rt_\w+)$", nm, flags=re.M))
@@ -141,3 +141,19 @@ def test_argument_errors_without_device(rt):
     assert L.rt_driver_create(None, None, None, 8, 8, None) == 1
     assert L.rt_driver_state(None) == -1
     assert L.rt_stripe_local_rows(100, 3, 2) == 0
+    assert L.rt_present_rgba8(None, None, None, 8, 8, 0, None) == 6
+
+
+def test_srgb_thresholds_match_restatement(rt):
+    """The sRGB boundary table the present kernel uses (computed in C++ double) equals the
+    numpy float64 restatement, bit for bit, and is strictly increasing."""
+    from oracle import present_ref
+    t = rt.srgb_thresholds()
+    want = present_ref.srgb_thresholds()
+    assert t.tobytes() == want.tobytes()
+    assert np.all(np.diff(t[1:]) > 0) and t[255] < 1.0
+    # j is the nearest code: the encoded value of T[j] rounds up to j, of its predecessor
+    # down to j - 1
+    v = t[1:].astype(np.float64)
+    enc = np.where(v <= 0.0031308, v * 12.92, 1.055 * v ** (1 / 2.4) - 0.055) * 255
+    assert np.all(enc >= np.arange(1, 256) - 0.5 - 1e-9)

@@ -236,6 +236,16 @@ def test_golden_k1(oracle):
     assert segs == int(g["segments"]) == 256 * 256
 
 
+def test_parallel_update_is_the_same_image(oracle):
+    """The threaded CPU baseline (row bands from a queue) computes the same bits."""
+    g = load_golden("k1.npz")
+    out, segs = oracle.update_parallel(np.zeros((256, 256, 4), np.float32), g["camera"],
+                                       g["spheres"], threads=3)
+    ok, bad = bits_equal(out, g["image"])
+    assert ok, bad
+    assert segs == 256 * 256
+
+
 def test_golden_accumulator(oracle):
     g = load_golden("accum_default.npz")
     cur = g["state0"]
