@@ -30,20 +30,9 @@ struct rt_ctx {
     std::vector<rt_sphere> cached;  // bytes currently on the device
     uint64_t scene_gen = 0;         // bumped on every sphere upload
     // Per-tile candidate lists of camera rays (culled scan), valid for cand_key.
-    uint32_t* cand_cnt = nullptr;
-    uint32_t* cand_idx = nullptr;
-    float4* cand_rec = nullptr;
+    uint32_t* cand_line = nullptr;
     uint64_t cand_tiles = 0;        // allocated tiles
     std::vector<unsigned char> cand_key;
-    // Sample count each recently written image holds (if uniform), by device pointer: the
-    // trace kernel's speculation hint (TraceParams::n_hint).  Only a hint — a stale entry
-    // costs a second pass over the mismatching lanes, never a different image.
-    struct Hint {
-        const void* buf = nullptr;
-        uint32_t n = 0;
-    };
-    Hint hints[8];
-    uint32_t hint_next = 0;
     float* d_srgb = nullptr;  // rt_srgb_thresholds table on the device (256 floats)
 };
 
@@ -85,39 +74,14 @@ uint32_t host_f2u(float f) {
     return (uint32_t)f;
 }
 
-uint32_t hint_for(const rt_ctx* ctx, const void* buf) {
-    for (const auto& e : ctx->hints)
-        if (e.buf == buf && buf != nullptr) return e.n;
-    return rtk::kNoHint;
-}
-
-void set_hint(rt_ctx* ctx, const void* buf, uint32_t n) {
-    for (auto& e : ctx->hints)
-        if (e.buf == buf) {
-            e.n = n;
-            if (n == rtk::kNoHint) e.buf = nullptr;
-            return;
-        }
-    if (n == rtk::kNoHint) return;
-    auto& e = ctx->hints[ctx->hint_next++ % (sizeof(ctx->hints) / sizeof(ctx->hints[0]))];
-    e.buf = buf;
-    e.n = n;
-}
-
-// Count after `frames` updates of a pixel that held n (wgsl:352-362): +1 per frame below spp.
-uint32_t advance_count(uint32_t n, uint32_t frames, uint32_t spp) {
-    if (n == rtk::kNoHint || n >= spp) return n;
-    const uint64_t m = (uint64_t)n + frames;
-    const uint32_t r = m < spp ? (uint32_t)m : spp;
-    return r < (1u << 24) ? r : rtk::kNoHint;  // beyond 2^24 the f32 round trip differs
-}
-
-// Sets p.n_hint for a launch of nf frames reading `in` and records the count `out` will
-// hold.
-void apply_hint(rt_ctx* ctx, rtk::TraceParams& p, const void* in, const void* out, uint32_t nf) {
-    const uint32_t n_in = p.reset_first ? 0u : hint_for(ctx, in);
-    p.n_hint = p.reset_first ? rtk::kNoHint : n_in;
-    set_hint(ctx, out, advance_count(n_in, nf, host_f2u(p.spp)));
+// Kernel instance for a launch (rtk::kTrace*): without bounce rays (max_depth <= 1) the
+// culled mode needs only the candidate lists.
+int trace_kernel_for(const rt_ctx* ctx, const rtk::TraceParams& p) {
+    if (ctx->scan_mode == RT_SCAN_EXHAUSTIVE) return rtk::kTraceExhaustive;
+#ifndef RT_FORCE_CULLED_KERNEL
+    if (host_f2u(p.max_depth) <= 1u) return rtk::kTraceList;
+#endif
+    return rtk::kTraceCulled;
 }
 
 rt_status check_image(uint32_t w, uint32_t h) {
@@ -191,12 +155,8 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
 }
 
 void free_candidates(rt_ctx* ctx) {
-    (void)hipFree(ctx->cand_cnt);
-    (void)hipFree(ctx->cand_idx);
-    (void)hipFree(ctx->cand_rec);
-    ctx->cand_cnt = nullptr;
-    ctx->cand_idx = nullptr;
-    ctx->cand_rec = nullptr;
+    (void)hipFree(ctx->cand_line);
+    ctx->cand_line = nullptr;
     ctx->cand_tiles = 0;
     ctx->cand_key.clear();
 }
@@ -236,23 +196,18 @@ rt_status ensure_candidates(rt_ctx* ctx, rtk::TraceParams& p, hipStream_t stream
                 if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
             }
             free_candidates(ctx);
-            hipError_t e = hipMalloc(&ctx->cand_cnt, tiles * sizeof(uint32_t));
-            if (e == hipSuccess) e = hipMalloc(&ctx->cand_idx, tiles * rtk::kCandMax * sizeof(uint32_t));
-            if (e == hipSuccess) e = hipMalloc(&ctx->cand_rec, tiles * rtk::kCandMax * sizeof(float4));
+            hipError_t e = hipMalloc(&ctx->cand_line, tiles * rtk::kCandLine * sizeof(uint32_t));
             if (e != hipSuccess) {
                 free_candidates(ctx);
                 return hip_fail(e, "hipMalloc(candidate lists)");
             }
             ctx->cand_tiles = tiles;
         }
-        hipError_t e = rtk::launch_candidates(p, ctx->cand_cnt, ctx->cand_idx, ctx->cand_rec,
-                                              stream);
+        hipError_t e = rtk::launch_candidates(p, ctx->cand_line, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_candidates_kernel launch");
         ctx->cand_key.assign(kb, kb + sizeof(key));
     }
-    p.cand_cnt = ctx->cand_cnt;
-    p.cand_idx = ctx->cand_idx;
-    p.cand_rec = ctx->cand_rec;
+    p.cand_line = ctx->cand_line;
     return RT_OK;
 }
 
@@ -301,7 +256,9 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
         const uint32_t padded = (count + 63u) & ~63u;   // <= count + 63 < count + kScanPad
         const bool bounces = cam->max_depth >= 2.0f;
         p.lds_records = (bounces && padded <= rtk::kLdsMaxRecords) ? padded : 0u;
-        if (rt_status s = ensure_candidates(ctx, p, stream)) return s;
+        // A short list is scanned whole from the cache; per-tile lists pay off above that.
+        if (count > rtk::kCandMax)
+            if (rt_status s = ensure_candidates(ctx, p, stream)) return s;
     }
     return RT_OK;
 }
@@ -330,8 +287,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         p.frames = nf;
         p.reset_first = (f0 == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
         std::memcpy(p.seeds, seeds + f0, nf * sizeof(float));
-        apply_hint(ctx, p, src, dst, nf);
-        hipError_t e = rtk::launch_trace(p, ctx->scan_mode, stream);
+        hipError_t e = rtk::launch_trace(p, trace_kernel_for(ctx, p), stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         src = dst;  // later launches continue the accumulation in place
     }
@@ -369,7 +325,7 @@ rt_status rt_destroy(rt_ctx* ctx) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     {
         DeviceGuard guard(ctx->device);
-        if (ctx->d_geom || ctx->d_sph || ctx->cand_cnt) (void)hipDeviceSynchronize();
+        if (ctx->d_geom || ctx->d_sph || ctx->cand_line) (void)hipDeviceSynchronize();
         (void)hipFree(ctx->d_geom);
         (void)hipFree(ctx->d_sph);
         (void)hipFree(ctx->d_srgb);
@@ -402,9 +358,7 @@ rt_status rt_init_image(rt_ctx* ctx, float* out, uint32_t w, uint32_t h, void* s
     if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
     hipError_t e = rtk::launch_init(reinterpret_cast<float4*>(out), (uint64_t)w * h,
                                     static_cast<hipStream_t>(stream));
-    if (e != hipSuccess) return hip_fail(e, "rt_init_kernel launch");
-    set_hint(ctx, out, 0u);
-    return RT_OK;
+    return e == hipSuccess ? RT_OK : hip_fail(e, "rt_init_kernel launch");
 }
 
 rt_status rt_update(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h,
@@ -444,8 +398,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         p.out = img[1 - cur];
         p.reset_first = (f == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
         p.seeds[0] = seeds[f];
-        apply_hint(ctx, p, p.in, p.out, 1);
-        hipError_t e = rtk::launch_trace(p, ctx->scan_mode, stream);
+        hipError_t e = rtk::launch_trace(p, trace_kernel_for(ctx, p), stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         cur = 1 - cur;
     }
@@ -479,7 +432,6 @@ rt_status rt_deinterleave_stripes(rt_ctx* ctx, const float* gathered, float* out
     hipError_t e = rtk::launch_deinterleave(
         reinterpret_cast<const float4*>(gathered), reinterpret_cast<float4*>(out), w, h,
         nranks, rt_stripe_local_rows(h, 0, nranks), static_cast<hipStream_t>(stream));
-    set_hint(ctx, out, rtk::kNoHint);
     return e == hipSuccess ? RT_OK : hip_fail(e, "rt_deinterleave_kernel launch");
 }
 

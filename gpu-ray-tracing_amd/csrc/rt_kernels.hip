@@ -21,6 +21,13 @@ namespace rtk {
 
 using namespace rtd;
 
+// Knock-out builds for cost attribution only (tools; never the product): RT_KO bit 1 skips
+// the sphere scan, 2 the shading, 4 the random camera ray, 8 the accumulator load, 16 the
+// store.
+#ifndef RT_KO
+#define RT_KO 0
+#endif
+
 // ---- diagnostic phase stamps (RT_STAMPS=1 builds only; never in the product) ---------
 #ifndef RT_STAMPS
 #define RT_STAMPS 0
@@ -138,6 +145,35 @@ __device__ __forceinline__ Hit scan_exhaustive(const float4* __restrict__ geom, 
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) cur[k] = nxt[k];
+    }
+    return Hit{idx, tmax};
+}
+
+// Closest hit among a tile's listed spheres (its candidate line: ascending indices,
+// kCandMax slots, unused slots naming a zero record): the chunk loop of scan_exhaustive
+// over the listed records.  The line (one 64-B scalar load) and the records (8 KB for
+// 500 spheres) are read through the scalar cache.
+__device__ __forceinline__ Hit scan_line(const float4* __restrict__ geom,
+                                         const uint32_t* __restrict__ line, uint32_t n, v3 o,
+                                         v3 d) {
+    constexpr int K = 4;
+    const float a = dot(d, d);
+    float tmax = 0x1.05ed2ep+118f;
+    int idx = -1;
+    uint32_t ids[kCandMax];
+#pragma unroll
+    for (uint32_t j = 0; j < kCandMax; ++j) ids[j] = line[4 + j];
+#pragma unroll
+    for (uint32_t c = 0; c < kCandMax; c += K) {
+        if (c >= n) break;
+        float hh[K], dd[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) dd[k] = discriminant(geom[ids[c + k]], o, d, a, hh[k]);
+        if (max_bits<K>(dd) > (int)0xFF800000) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (c + k < n) consider(dd[k], hh[k], a, ids[c + k], tmax, idx);
+        }
     }
     return Hit{idx, tmax};
 }
@@ -329,27 +365,6 @@ __device__ __forceinline__ bool tile_cone(const TraceParams& p, uint32_t tx, uin
     return true;
 }
 
-// Closest hit among a tile's listed spheres (records in index order, zero-padded to a
-// multiple of 4): the exhaustive chunk loop restricted to the list.
-__device__ __forceinline__ Hit scan_list(const float4* __restrict__ rec,
-                                         const uint32_t* __restrict__ ids, uint32_t n, v3 o,
-                                         v3 d) {
-    const float a = dot(d, d);
-    float tmax = 0x1.05ed2ep+118f;
-    int slot = -1;
-    for (uint32_t c = 0; c < n; c += 4) {
-        float hh[4], dd[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) dd[k] = discriminant(rec[c + k], o, d, a, hh[k]);
-        if (max_bits<4>(dd) > (int)0xFF800000) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (c + k < n) consider(dd[k], hh[k], a, c + k, tmax, slot);
-        }
-    }
-    return Hit{slot < 0 ? -1 : (int)ids[slot], tmax};
-}
-
 struct Cam {
     v3 center, vul, pdu, pdv, ddu, ddv;
     float defocus_angle;
@@ -381,33 +396,42 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
 // is still being traced; the bounce loop runs while any lane is live, and a lane's
 // values are only updated while it is live, so each lane computes exactly its own
 // per-pixel result.
-template <bool kCull>
-__device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uint32_t depth,
-                                        v3 o, v3 d, uint32_t seed, bool live) {
-    // candidates of this tile's camera rays (kCandNone: no list, use the scans below)
-    const uint32_t ncand = (kCull && p.cand_k) ? p.cand_cnt[tile] : kCandNone;
+template <int kScan>
+__device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uint32_t ncand,
+                                        uint32_t depth, v3 o, v3 d, uint32_t seed, bool live) {
     v3 cf = mk(1.0f, 1.0f, 1.0f);
     bool black = false;
     for (uint32_t i = 0; i < depth; ++i) {
         if (__ballot(live) == 0ull) break;
+        // Camera rays of a tile with a candidate list (ncand != kCandNone) test only the
+        // listed spheres, in index order.
+        const bool listed = kScan != kTraceExhaustive && i == 0 && ncand != kCandNone;
+#if RT_KO & 1
+        const Hit hit = Hit{-1, 0.0f};
+#else
         const Hit hit =
-            !kCull ? scan_exhaustive(p.geom, p.count, o, d)
-            : (i == 0 && ncand != kCandNone)
-                ? scan_list(p.cand_rec + (size_t)tile * p.cand_k,
-                            p.cand_idx + (size_t)tile * p.cand_k, ncand, o, d)
+            listed ? scan_line(p.geom, p.cand_line + (size_t)tile * kCandLine, ncand, o, d)
+            : kScan != kTraceCulled ? scan_exhaustive(p.geom, p.count, o, d)
             : p.lds_records ? scan_culled<true>(p.geom, p.count, o, d, live)
                             : scan_culled<false>(p.geom, p.count, o, d, live);
+#endif
+        const float4* hs = p.sph;
         if (!live) continue;
         if (hit.idx < 0) {                                        // wgsl:288-290
             live = false;
             continue;
         }
+#if RT_KO & 2
+        cf = mk(hit.t, hit.t, hit.t);
+        live = false;
+        continue;
+#endif
         // Hit record of the winner (wgsl:205-218).  The two record loads are per-lane and
         // depend on the scan; the scatter's random numbers do not depend on the material
         // (lambertian and metal draw random_unit_vector(sb), dielectric draws rf(sb), its
         // first component), so they are computed while the loads are in flight.
-        const float4 pr = p.sph[2 * hit.idx];       // position, radius
-        const float4 mat = p.sph[2 * hit.idx + 1];  // material color
+        const float4 pr = hs[2 * hit.idx];          // position, radius
+        const float4 mat = hs[2 * hit.idx + 1];     // material color
         const uint32_t sb = hash(seed + i * 1000u);               // wgsl:268
         const float r_sb = rf(sb);
         const v3 ruv = random_unit_vector(r_sb, sb);
@@ -477,66 +501,46 @@ __device__ __forceinline__ TileCoord tile_coord(const TraceParams& p, uint32_t t
     return t;
 }
 
-// The accumulator's sample count n selects the pixel's random numbers (seed = 1 + n + B),
-// so the whole sample depends on the HBM load of `in`.  When the host knows the count the
-// image should hold (p.n_hint: every pixel of a progressive render has the same count),
-// frame 0 is traced with that count while the load is in flight and verified against the
-// loaded count afterwards; lanes whose count differs are traced again with the loaded
-// count (a second pass of the loop).  Results are identical to the non-speculative order.
-template <bool kCull>
+template <int kScan>
 __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& cam,
-                                              uint32_t tile, const TileCoord& tc, float4 acc) {
-    // st = the pixel's state: colour in xyz, f32(count) in w (wgsl:339-341, 362); it holds
-    // the loaded accumulator until `known`, then the accumulated state.
-    float4 st = acc;
-    bool known = false;
+                                              uint32_t tile, uint32_t ncand,
+                                              const TileCoord& tc, float4 acc) {
+    v3 c = mk(acc.x, acc.y, acc.z);                               // wgsl:339-341
+    uint32_t n = f2u(acc.w);
     const uint32_t spp = f2u(p.spp);                              // wgsl:343
     const uint32_t depth = f2u(p.max_depth);
     const uint32_t hxy = hash(tc.x * 73u) ^ hash(tc.y * 51u);     // wgsl:309-310
     for (uint32_t f = 0; f < p.frames; ++f) {
         const uint32_t B = f2u(p.seeds[f] * 4294967296.0f);      // wgsl:311,353
         if (f == 0 && p.reset_first) {                            // wgsl:345-350
-            st = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            known = true;
+            c = mk(0.0f, 0.0f, 0.0f);
+            n = 0u;
         }
-        if (p.n_hint == kNoHint) known = true;
-        uint32_t n_try = known ? f2u(st.w) : p.n_hint;
-        bool pending = tc.valid;
-        for (;;) {
-            const bool live = pending && n_try < spp;             // wgsl:352
-            v3 col = mk(0.0f, 0.0f, 0.0f);
-            if (__ballot(live) != 0ull) {
-                const uint32_t seed = 1u + n_try + B;
-                v3 o, d;
-                STAMP(0);
-                get_ray(cam, tc.x, tc.y, hxy, seed, B, o, d);
-                STAMP(1);
-                const v3 cl = ray_color<kCull>(p, tile, depth, o, d, seed + 1u, live);
-                STAMP(4);
-                if (live) col = cl;
+        const bool live = tc.valid && n < spp;                    // wgsl:352
+        if (__ballot(live) != 0ull) {
+            const uint32_t seed = 1u + n + B;
+            v3 o, d;
+            STAMP(0);
+#if RT_KO & 4
+            o = cam.center;
+            d = sub(fmas((float)tc.y, cam.pdv, fmas((float)tc.x, cam.pdu, cam.vul)), o);
+#else
+            get_ray(cam, tc.x, tc.y, hxy, seed, B, o, d);
+#endif
+            STAMP(1);
+            const v3 col = ray_color<kScan>(p, tile, ncand, depth, o, d, seed + 1u, live);
+            STAMP(4);
+            if (live) {
+                const float k = (float)(n + 1u);                  // wgsl:356
+                c = mk(c.x + (col.x - c.x) / k, c.y + (col.y - c.y) / k,
+                       c.z + (col.z - c.z) / k);
+                n += 1u;
             }
-            uint32_t n = f2u(st.w);
-            bool wrong = false;
-            if (!known) {                                         // verify the guess
-                known = true;
-                wrong = pending && n != n_try;
-            }
-            if (pending && !wrong) {
-                if (n < spp) {
-                    const float k = (float)(n + 1u);              // wgsl:356
-                    st.x = st.x + (col.x - st.x) / k;
-                    st.y = st.y + (col.y - st.y) / k;
-                    st.z = st.z + (col.z - st.z) / k;
-                    n += 1u;
-                }
-                st.w = (float)n;                                  // wgsl:362
-            }
-            if (__ballot(wrong) == 0ull) break;
-            pending = wrong;                                      // retrace these lanes
-            n_try = n;
         }
+        // The chained form stores f32(n) and reloads u32(.) each frame (wgsl:341,362).
+        n = f2u((float)n);
     }
-    return st;
+    return make_float4(c.x, c.y, c.z, (float)n);                  // wgsl:362
 }
 
 // One workgroup = 4 waves = 4 consecutive tiles.  (A persistent grid that walks tiles
@@ -546,17 +550,21 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 #ifndef RT_TRACE_MIN_WAVES
 #define RT_TRACE_MIN_WAVES 8
 #endif
-template <bool kCull>
+template <int kScan>
 __global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const TraceParams p) {
     STAMP(-2);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tiles_x = (p.width + 7u) >> 3;
-    const uint32_t tx = blockIdx.x * 4u + (threadIdx.x >> 6), lband = blockIdx.y;
+    // The wave index is uniform, but the compiler's divergence analysis does not know it;
+    // readfirstlane makes the tile (and the candidate-list pointers and counts derived from
+    // it) scalar, so list records are read with s_load into SGPRs.
+    const uint32_t tx = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lband = blockIdx.y;
     const bool wave_in = tx < tiles_x;
     const TileCoord tc = tile_coord(p, tx, lband, lane);
     // Culled scan: the workgroup stages the scan records (count padded to 64) in LDS once;
     // the per-block cone test then reads them at LDS latency instead of L2 latency.
-    if (kCull && p.lds_records) {
+    if (kScan == kTraceCulled && p.lds_records) {
         for (uint32_t j = threadIdx.x; j < p.lds_records; j += 512u) {
             const float4 g0 = p.geom[j];
             const float4 g1 = p.geom[j + 256u < p.lds_records ? j + 256u : j];
@@ -566,9 +574,15 @@ __global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const
         __syncthreads();
     }
     if (!wave_in) return;                                         // whole wave exits
-    // Unconditional load (texel 0 for lanes outside the image): no branch joins on it, so
-    // its first use — after the traced sample when p.n_hint is set — is where it is waited.
-    const float4 acc = p.in[tc.valid ? tc.idx : 0];               // wgsl:339
+    const uint32_t tile = lband * tiles_x + tx;
+    // the tile's candidate count (its line is read again by the scan, from the cache)
+    const uint32_t ncand = (kScan != kTraceExhaustive && p.cand_k)
+                               ? p.cand_line[(size_t)tile * kCandLine] : kCandNone;
+#if RT_KO & 8
+    const float4 acc = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+#else
+    const float4 acc = tc.valid ? p.in[tc.idx] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#endif
 
     Cam cam;
     cam.center = mk(p.center[0], p.center[1], p.center[2]);
@@ -579,25 +593,27 @@ __global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const
     cam.ddv = mk(p.ddv[0], p.ddv[1], p.ddv[2]);
     cam.defocus_angle = p.defocus_angle;
 
-    const float4 res = trace_pixel<kCull>(p, cam, lband * tiles_x + tx, tc, acc);
+    const float4 res = trace_pixel<kScan>(p, cam, tile, ncand, tc, acc);
+#if RT_KO & 16
+    if (res.x == 12345.678f) p.out[tc.idx] = res;
+#else
     if (tc.valid) p.out[tc.idx] = res;                            // wgsl:363
+#endif
     STAMP(5);
 }
 
-// One wave per tile: list the spheres the tile's camera rays can hit (see tile_cone).
+// One wave per tile: list the spheres the tile's camera rays can hit (see tile_cone) in
+// the tile's 64-B line {count, 0, 0, 0, id[0..kCandMax-1]}.
 __global__ __launch_bounds__(256) void rt_candidates_kernel(const TraceParams p,
-                                                            uint32_t* __restrict__ cnt,
-                                                            uint32_t* __restrict__ ids,
-                                                            float4* __restrict__ rec) {
+                                                            uint32_t* __restrict__ lines) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     const uint32_t tx = blockIdx.x * 4u + (threadIdx.x >> 6), lband = blockIdx.y;
     if (tx >= tiles_x) return;
-    const uint32_t tile = lband * tiles_x + tx;
-    const uint32_t K = p.cand_k;
+    uint32_t* line = lines + (size_t)(lband * tiles_x + tx) * kCandLine;
     Cone k;
     if (!tile_cone(p, tx, lband, k)) {
-        if (lane == 0) cnt[tile] = kCandNone;
+        if (lane == 0) line[0] = kCandNone;
         return;
     }
     uint32_t n = 0;
@@ -609,18 +625,15 @@ __global__ __launch_bounds__(256) void rt_candidates_kernel(const TraceParams p,
         if (keep) {
             const uint32_t pos = n + __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-            if (pos < K) {
-                ids[(size_t)tile * K + pos] = i;
-                rec[(size_t)tile * K + pos] = g;
-            }
+            if (pos < kCandMax) line[4 + pos] = i;
         }
         n += (uint32_t)__builtin_popcountll(mask);
     }
-    // zero the chunk padding after the last record
-    const uint32_t pad = ((n + 3u) & ~3u) - n;
-    if (n <= K && lane < pad && n + lane < K)
-        rec[(size_t)tile * K + n + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (lane == 0) cnt[tile] = n <= K ? n : kCandNone;
+    // unused slots name the first zero record after the list (rt_abi.cpp pads the list);
+    // every word of the line is written exactly once
+    if (lane >= 1 && lane < 4) line[lane] = 0u;
+    if (lane >= 4 && lane < kCandLine && lane - 4 >= n) line[lane] = p.count;
+    if (lane == 0) line[0] = n <= kCandMax ? n : kCandNone;
 }
 
 __global__ __launch_bounds__(256) void rt_init_kernel(float4* __restrict__ out, uint64_t n) {
@@ -685,22 +698,23 @@ static dim3 tile_grid(const TraceParams& p) {
     return dim3((tiles_x + 3u) / 4u, p.local_bands);
 }
 
-hipError_t launch_trace(const TraceParams& p, int scan_mode, hipStream_t stream) {
+hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
     const dim3 grid = tile_grid(p);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    if (scan_mode == RT_SCAN_CULLED)
-        hipLaunchKernelGGL(rt_trace_kernel<true>, grid, dim3(256),
+    if (kernel == kTraceCulled)
+        hipLaunchKernelGGL(rt_trace_kernel<kTraceCulled>, grid, dim3(256),
                            (size_t)p.lds_records * sizeof(float4), stream, p);
+    else if (kernel == kTraceList)
+        hipLaunchKernelGGL(rt_trace_kernel<kTraceList>, grid, dim3(256), 0, stream, p);
     else
-        hipLaunchKernelGGL(rt_trace_kernel<false>, grid, dim3(256), 0, stream, p);
+        hipLaunchKernelGGL(rt_trace_kernel<kTraceExhaustive>, grid, dim3(256), 0, stream, p);
     return hipGetLastError();
 }
 
-hipError_t launch_candidates(const TraceParams& p, uint32_t* cnt, uint32_t* ids, float4* rec,
-                             hipStream_t stream) {
+hipError_t launch_candidates(const TraceParams& p, uint32_t* lines, hipStream_t stream) {
     const dim3 grid = tile_grid(p);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    hipLaunchKernelGGL(rt_candidates_kernel, grid, dim3(256), 0, stream, p, cnt, ids, rec);
+    hipLaunchKernelGGL(rt_candidates_kernel, grid, dim3(256), 0, stream, p, lines);
     return hipGetLastError();
 }
 

@@ -346,16 +346,18 @@ def test_culled_scan_equals_exhaustive(rt, seed):
     assert_same(out["culled"], out["exhaustive"])
 
 
-def test_candidate_lists_follow_camera_and_scene(rt, oracle):
+@pytest.mark.parametrize("depth", [1, 2])
+def test_candidate_lists_follow_camera_and_scene(rt, oracle, depth):
     """The per-tile camera-ray candidate lists are rebuilt when the camera geometry, the
-    scene or the stripe partition change, and reused across frames (seed, reset, spp)."""
+    scene or the stripe partition change, and reused across frames (seed, reset, spp).
+    depth 1 runs the list-only kernel instance, depth 2 the list + cone-culling one."""
     w, h = 96, 64
     p = rt.ComputeShaderPipeline(0)
     p.set_scan_mode("culled")
     sc = rt.synthetic_scene(300, seed=3)
-    cams = [camera(rt, w, h, depth=2, seed=0.125),
+    cams = [camera(rt, w, h, depth=depth, seed=0.125),
             rt.SceneCamera.from_settings(rt.CameraSettings(look_from=(-9.0, 3.0, 7.0),
-                                                           max_depth=2), w, h, 0.625)]
+                                                           max_depth=depth), w, h, 0.625)]
     for cam in cams + cams[:1]:
         for seed in (0.25, 0.75):
             c = cam.with_fields(random_seed=seed)
@@ -366,7 +368,8 @@ def test_candidate_lists_follow_camera_and_scene(rt, oracle):
     p.close()
 
 
-def test_candidate_list_overflow_falls_back(rt):
+@pytest.mark.parametrize("depth", [1, 3])
+def test_candidate_list_overflow_falls_back(rt, depth):
     """A tile whose camera rays can reach more spheres than a list holds (a dense cluster
     straight ahead) uses the per-wave culled scan instead — still bit-exact."""
     rng = np.random.default_rng(7)
@@ -379,7 +382,7 @@ def test_candidate_list_overflow_falls_back(rt):
     s[0] = [0, -1000, 0, 1000, 0.5, 0.5, 0.5, -2]
     sc = rt.SphereCollection(s)
     w, h = 64, 64
-    cam = rt.SceneCamera.from_settings(rt.CameraSettings(field_of_view=3.0, max_depth=3), w, h, 0.5)
+    cam = rt.SceneCamera.from_settings(rt.CameraSettings(field_of_view=3.0, max_depth=depth), w, h, 0.5)
     out = {}
     for mode in ("culled", "exhaustive"):
         p = rt.ComputeShaderPipeline(0)
@@ -421,17 +424,16 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks):
     assert_same(got, want)
 
 
-def test_stale_sample_count_hint_is_exact(rt, oracle, pipe):
-    """The library traces frame 0 with the sample count it expects `in` to hold and
-    retraces the lanes whose loaded count differs (rt_abi.cpp apply_hint, trace_pixel):
-    images written behind its back (wrong hint) and mixed per-pixel counts stay exact."""
+def test_accumulator_written_outside_the_library(rt, oracle, pipe):
+    """Accumulators written behind the library's back (mixed per-pixel counts, NaN,
+    fractional and negative counts) after init_image and between fused frames."""
     w, h = 67, 45
     sc = rt.create_default_spheres(3)
     rng = np.random.default_rng(7)
     a, b = pipe.new_image(w, h), pipe.new_image(w, h)
-    pipe.init_image(a, w, h)                      # the library now expects count 0 in `a`
+    pipe.init_image(a, w, h)
     counts = rng.integers(0, 6, (h, w, 1)).astype(np.float32)
-    counts[::3, ::2] = 0.0                        # some lanes match the hint, most do not
+    counts[::3, ::2] = 0.0
     counts[5, 7], counts[6, 8], counts[7, 9] = np.nan, 2.5, -3.0
     state = np.concatenate([rng.random((h, w, 3), np.float32), counts], axis=2)
     a.copy_(to_dev(state))                        # written behind the library's back
@@ -439,7 +441,7 @@ def test_stale_sample_count_hint_is_exact(rt, oracle, pipe):
     pipe.update(a, b, w, h, cam, sc)
     want, _ = oracle.update(state, cam.blob, sc.spheres)
     assert_same(host(b), want)
-    # b's hint (1) is wrong for every pixel; a fused 3-frame render continues from it
+    # a fused 3-frame render continues from it
     seeds = np.array([0.125, 0.5, 0.875], np.float32)
     pipe.render(b, a, w, h, cam, sc, seeds)
     cur = want
