@@ -30,7 +30,9 @@ struct rt_ctx {
     std::vector<rt_sphere> cached;  // bytes currently on the device
     uint64_t scene_gen = 0;         // bumped on every sphere upload
     // Per-tile candidate lists of camera rays (culled scan), valid for cand_key.
-    uint32_t* cand_line = nullptr;
+    uint32_t* cand_cnt = nullptr;
+    float4* cand_rec = nullptr;
+    float4* cand_sph = nullptr;
     uint64_t cand_tiles = 0;        // allocated tiles
     std::vector<unsigned char> cand_key;
     float* d_srgb = nullptr;  // rt_srgb_thresholds table on the device (256 floats)
@@ -155,8 +157,12 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
 }
 
 void free_candidates(rt_ctx* ctx) {
-    (void)hipFree(ctx->cand_line);
-    ctx->cand_line = nullptr;
+    (void)hipFree(ctx->cand_cnt);
+    (void)hipFree(ctx->cand_rec);
+    (void)hipFree(ctx->cand_sph);
+    ctx->cand_cnt = nullptr;
+    ctx->cand_rec = nullptr;
+    ctx->cand_sph = nullptr;
     ctx->cand_tiles = 0;
     ctx->cand_key.clear();
 }
@@ -196,18 +202,25 @@ rt_status ensure_candidates(rt_ctx* ctx, rtk::TraceParams& p, hipStream_t stream
                 if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
             }
             free_candidates(ctx);
-            hipError_t e = hipMalloc(&ctx->cand_line, tiles * rtk::kCandLine * sizeof(uint32_t));
+            const uint64_t slots = tiles * rtk::kCandMax;
+            hipError_t e = hipMalloc(&ctx->cand_cnt, tiles * sizeof(uint32_t));
+            // + one chunk: the scan prefetches a chunk past the last tile's list
+            if (e == hipSuccess) e = hipMalloc(&ctx->cand_rec, (slots + 4) * sizeof(float4));
+            if (e == hipSuccess) e = hipMalloc(&ctx->cand_sph, slots * 2 * sizeof(float4));
             if (e != hipSuccess) {
                 free_candidates(ctx);
                 return hip_fail(e, "hipMalloc(candidate lists)");
             }
             ctx->cand_tiles = tiles;
         }
-        hipError_t e = rtk::launch_candidates(p, ctx->cand_line, stream);
+        hipError_t e = rtk::launch_candidates(p, ctx->cand_cnt, ctx->cand_rec, ctx->cand_sph,
+                                              stream);
         if (e != hipSuccess) return hip_fail(e, "rt_candidates_kernel launch");
         ctx->cand_key.assign(kb, kb + sizeof(key));
     }
-    p.cand_line = ctx->cand_line;
+    p.cand_cnt = ctx->cand_cnt;
+    p.cand_rec = ctx->cand_rec;
+    p.cand_sph = ctx->cand_sph;
     return RT_OK;
 }
 
@@ -256,9 +269,7 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
         const uint32_t padded = (count + 63u) & ~63u;   // <= count + 63 < count + kScanPad
         const bool bounces = cam->max_depth >= 2.0f;
         p.lds_records = (bounces && padded <= rtk::kLdsMaxRecords) ? padded : 0u;
-        // A short list is scanned whole from the cache; per-tile lists pay off above that.
-        if (count > rtk::kCandMax)
-            if (rt_status s = ensure_candidates(ctx, p, stream)) return s;
+        if (rt_status s = ensure_candidates(ctx, p, stream)) return s;
     }
     return RT_OK;
 }
@@ -325,7 +336,7 @@ rt_status rt_destroy(rt_ctx* ctx) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     {
         DeviceGuard guard(ctx->device);
-        if (ctx->d_geom || ctx->d_sph || ctx->cand_line) (void)hipDeviceSynchronize();
+        if (ctx->d_geom || ctx->d_sph || ctx->cand_cnt) (void)hipDeviceSynchronize();
         (void)hipFree(ctx->d_geom);
         (void)hipFree(ctx->d_sph);
         (void)hipFree(ctx->d_srgb);

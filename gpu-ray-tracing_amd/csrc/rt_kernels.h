@@ -14,11 +14,8 @@ namespace rtk {
 constexpr uint32_t kMaxFramesPerLaunch = 128;
 // Culled scan: lists up to this many spheres are staged in LDS (64 KiB per workgroup).
 constexpr uint32_t kLdsMaxRecords = 4096;
-// Per-tile candidate lists of camera rays (culled scan): one 64-B line per tile,
-// {count, 0, 0, 0, id[0..11]}: up to kCandMax sphere indices in increasing order, padded
-// with the index of a zero record; count = kCandNone marks a tile without a list.
-constexpr uint32_t kCandMax = 12;
-constexpr uint32_t kCandLine = 16;  // u32 words per tile
+// Per-tile candidate lists of camera rays (culled scan): capacity and the "no list" mark.
+constexpr uint32_t kCandMax = 32;
 constexpr uint32_t kCandNone = 0xFFFFFFFFu;
 
 // Everything the `update` kernel needs, passed by value (kernarg -> SGPRs).
@@ -32,8 +29,10 @@ struct TraceParams {
     uint32_t frames;       // accumulation frames in this launch (1 = one `update`)
     uint32_t reset_first;  // camera_has_moved > 0.5 applies to frame 0 only
     uint32_t lds_records;  // culled scan: records staged in LDS (0 = read from HBM/L2)
-    uint32_t cand_k;       // 0 = no candidate lists, else kCandMax
-    const uint32_t* cand_line;  // [tile][kCandLine]
+    uint32_t cand_k;       // per-tile candidate list capacity (0 = no lists)
+    const uint32_t* cand_cnt;  // [tile] listed spheres, kCandNone = no list
+    const float4* cand_rec;    // [tile][cand_k] their scan records, in index order, padded
+    const float4* cand_sph;    // [tile][cand_k][2] their 32-B GpuSphere records
     float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3];
     float defocus_angle, max_depth, spp;
     float seeds[kMaxFramesPerLaunch];
@@ -48,7 +47,8 @@ constexpr int kTraceList = 2;
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream);
 hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream);
 // Builds the per-tile candidate lists for p's camera/scene/stripes (p.cand_k slots each).
-hipError_t launch_candidates(const TraceParams& p, uint32_t* lines, hipStream_t stream);
+hipError_t launch_candidates(const TraceParams& p, uint32_t* cnt, float4* rec, float4* sph,
+                             hipStream_t stream);
 hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t width,
                                uint32_t height, uint32_t nranks, uint32_t max_local_rows,
                                hipStream_t stream);

@@ -149,35 +149,6 @@ __device__ __forceinline__ Hit scan_exhaustive(const float4* __restrict__ geom, 
     return Hit{idx, tmax};
 }
 
-// Closest hit among a tile's listed spheres (its candidate line: ascending indices,
-// kCandMax slots, unused slots naming a zero record): the chunk loop of scan_exhaustive
-// over the listed records.  The line (one 64-B scalar load) and the records (8 KB for
-// 500 spheres) are read through the scalar cache.
-__device__ __forceinline__ Hit scan_line(const float4* __restrict__ geom,
-                                         const uint32_t* __restrict__ line, uint32_t n, v3 o,
-                                         v3 d) {
-    constexpr int K = 4;
-    const float a = dot(d, d);
-    float tmax = 0x1.05ed2ep+118f;
-    int idx = -1;
-    uint32_t ids[kCandMax];
-#pragma unroll
-    for (uint32_t j = 0; j < kCandMax; ++j) ids[j] = line[4 + j];
-#pragma unroll
-    for (uint32_t c = 0; c < kCandMax; c += K) {
-        if (c >= n) break;
-        float hh[K], dd[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) dd[k] = discriminant(geom[ids[c + k]], o, d, a, hh[k]);
-        if (max_bits<K>(dd) > (int)0xFF800000) {
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (c + k < n) consider(dd[k], hh[k], a, ids[c + k], tmax, idx);
-        }
-    }
-    return Hit{idx, tmax};
-}
-
 // ---- Exact wave-level culling --------------------------------------------------------
 //
 // The 64 rays of a wave (one 8x8 tile, plus lens offsets) are nearly coherent.  Bound all
@@ -404,18 +375,22 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
     for (uint32_t i = 0; i < depth; ++i) {
         if (__ballot(live) == 0ull) break;
         // Camera rays of a tile with a candidate list (ncand != kCandNone) test only the
-        // listed spheres, in index order.
+        // listed spheres: their records are in index order and padded like the full list,
+        // so the same chunk loop applies; hit.idx then indexes the tile's copy of the
+        // sphere records.
         const bool listed = kScan != kTraceExhaustive && i == 0 && ncand != kCandNone;
+        const size_t lbase = (size_t)tile * p.cand_k;
 #if RT_KO & 1
         const Hit hit = Hit{-1, 0.0f};
 #else
         const Hit hit =
-            listed ? scan_line(p.geom, p.cand_line + (size_t)tile * kCandLine, ncand, o, d)
-            : kScan != kTraceCulled ? scan_exhaustive(p.geom, p.count, o, d)
+            (kScan != kTraceCulled || listed)
+                ? scan_exhaustive(listed ? p.cand_rec + lbase : p.geom,
+                                  listed ? ncand : p.count, o, d)
             : p.lds_records ? scan_culled<true>(p.geom, p.count, o, d, live)
                             : scan_culled<false>(p.geom, p.count, o, d, live);
 #endif
-        const float4* hs = p.sph;
+        const float4* hs = listed ? p.cand_sph + 2 * lbase : p.sph;
         if (!live) continue;
         if (hit.idx < 0) {                                        // wgsl:288-290
             live = false;
@@ -550,15 +525,26 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 #ifndef RT_TRACE_MIN_WAVES
 #define RT_TRACE_MIN_WAVES 8
 #endif
+// Waves (tiles) per workgroup: the culled instance shares the LDS copy of the records
+// among 4 waves; the others use one-wave workgroups, so a finished tile frees its slot
+// without waiting for slower neighbours.
+#ifndef RT_WG_WAVES
+#define RT_WG_WAVES 1
+#endif
 template <int kScan>
-__global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const TraceParams p) {
+constexpr uint32_t wg_waves() { return kScan == kTraceCulled ? 4u : RT_WG_WAVES; }
+
+template <int kScan>
+__global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt_trace_kernel(
+    const TraceParams p) {
     STAMP(-2);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     // The wave index is uniform, but the compiler's divergence analysis does not know it;
     // readfirstlane makes the tile (and the candidate-list pointers and counts derived from
     // it) scalar, so list records are read with s_load into SGPRs.
-    const uint32_t tx = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t tx =
+        blockIdx.x * wg_waves<kScan>() + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lband = blockIdx.y;
     const bool wave_in = tx < tiles_x;
     const TileCoord tc = tile_coord(p, tx, lband, lane);
@@ -575,13 +561,13 @@ __global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const
     }
     if (!wave_in) return;                                         // whole wave exits
     const uint32_t tile = lband * tiles_x + tx;
-    // the tile's candidate count (its line is read again by the scan, from the cache)
-    const uint32_t ncand = (kScan != kTraceExhaustive && p.cand_k)
-                               ? p.cand_line[(size_t)tile * kCandLine] : kCandNone;
+    // the tile's candidate count (kCandNone: no list)
+    const uint32_t ncand =
+        (kScan != kTraceExhaustive && p.cand_k) ? p.cand_cnt[tile] : kCandNone;
 #if RT_KO & 8
     const float4 acc = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
 #else
-    const float4 acc = tc.valid ? p.in[tc.idx] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const float4 acc = p.in[tc.valid ? tc.idx : 0];               // wgsl:339
 #endif
 
     Cam cam;
@@ -602,18 +588,20 @@ __global__ __launch_bounds__(256, RT_TRACE_MIN_WAVES) void rt_trace_kernel(const
     STAMP(5);
 }
 
-// One wave per tile: list the spheres the tile's camera rays can hit (see tile_cone) in
-// the tile's 64-B line {count, 0, 0, 0, id[0..kCandMax-1]}.
+// One wave per tile: list the spheres the tile's camera rays can hit (see tile_cone).
 __global__ __launch_bounds__(256) void rt_candidates_kernel(const TraceParams p,
-                                                            uint32_t* __restrict__ lines) {
+                                                            uint32_t* __restrict__ cnt,
+                                                            float4* __restrict__ rec,
+                                                            float4* __restrict__ sph) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     const uint32_t tx = blockIdx.x * 4u + (threadIdx.x >> 6), lband = blockIdx.y;
     if (tx >= tiles_x) return;
-    uint32_t* line = lines + (size_t)(lband * tiles_x + tx) * kCandLine;
+    const uint32_t tile = lband * tiles_x + tx;
+    const uint32_t K = p.cand_k;
     Cone k;
     if (!tile_cone(p, tx, lband, k)) {
-        if (lane == 0) line[0] = kCandNone;
+        if (lane == 0) cnt[tile] = kCandNone;
         return;
     }
     uint32_t n = 0;
@@ -625,15 +613,20 @@ __global__ __launch_bounds__(256) void rt_candidates_kernel(const TraceParams p,
         if (keep) {
             const uint32_t pos = n + __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-            if (pos < kCandMax) line[4 + pos] = i;
+            if (pos < K) {
+                const size_t slot = (size_t)tile * K + pos;
+                rec[slot] = g;
+                sph[2 * slot] = p.sph[2 * i];
+                sph[2 * slot + 1] = p.sph[2 * i + 1];
+            }
         }
         n += (uint32_t)__builtin_popcountll(mask);
     }
-    // unused slots name the first zero record after the list (rt_abi.cpp pads the list);
-    // every word of the line is written exactly once
-    if (lane >= 1 && lane < 4) line[lane] = 0u;
-    if (lane >= 4 && lane < kCandLine && lane - 4 >= n) line[lane] = p.count;
-    if (lane == 0) line[0] = n <= kCandMax ? n : kCandNone;
+    // zero the chunk padding after the last record
+    const uint32_t pad = ((n + 3u) & ~3u) - n;
+    if (n <= K && lane < pad && n + lane < K)
+        rec[(size_t)tile * K + n + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (lane == 0) cnt[tile] = n <= K ? n : kCandNone;
 }
 
 __global__ __launch_bounds__(256) void rt_init_kernel(float4* __restrict__ out, uint64_t n) {
@@ -693,28 +686,34 @@ __global__ __launch_bounds__(256) void rt_present_kernel(const float4* __restric
 }
 
 // 256-thread workgroups: 4 waves = 4 tiles along a stripe band; grid (columns/4, bands).
-static dim3 tile_grid(const TraceParams& p) {
+static dim3 tile_grid(const TraceParams& p, uint32_t waves = 4) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
-    return dim3((tiles_x + 3u) / 4u, p.local_bands);
+    return dim3((tiles_x + waves - 1u) / waves, p.local_bands);
+}
+
+template <int kScan>
+static void launch_trace_as(const TraceParams& p, size_t lds, hipStream_t stream) {
+    constexpr uint32_t w = wg_waves<kScan>();
+    const dim3 grid = tile_grid(p, w);
+    if (grid.x == 0 || grid.y == 0) return;
+    hipLaunchKernelGGL(rt_trace_kernel<kScan>, grid, dim3(64 * w), lds, stream, p);
 }
 
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
-    const dim3 grid = tile_grid(p);
-    if (grid.x == 0 || grid.y == 0) return hipSuccess;
     if (kernel == kTraceCulled)
-        hipLaunchKernelGGL(rt_trace_kernel<kTraceCulled>, grid, dim3(256),
-                           (size_t)p.lds_records * sizeof(float4), stream, p);
+        launch_trace_as<kTraceCulled>(p, (size_t)p.lds_records * sizeof(float4), stream);
     else if (kernel == kTraceList)
-        hipLaunchKernelGGL(rt_trace_kernel<kTraceList>, grid, dim3(256), 0, stream, p);
+        launch_trace_as<kTraceList>(p, 0, stream);
     else
-        hipLaunchKernelGGL(rt_trace_kernel<kTraceExhaustive>, grid, dim3(256), 0, stream, p);
+        launch_trace_as<kTraceExhaustive>(p, 0, stream);
     return hipGetLastError();
 }
 
-hipError_t launch_candidates(const TraceParams& p, uint32_t* lines, hipStream_t stream) {
+hipError_t launch_candidates(const TraceParams& p, uint32_t* cnt, float4* rec, float4* sph,
+                             hipStream_t stream) {
     const dim3 grid = tile_grid(p);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    hipLaunchKernelGGL(rt_candidates_kernel, grid, dim3(256), 0, stream, p, lines);
+    hipLaunchKernelGGL(rt_candidates_kernel, grid, dim3(256), 0, stream, p, cnt, rec, sph);
     return hipGetLastError();
 }
 
