@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "rt_abi.h"
+#include "rt_device.h"
 #include "rt_kernels.h"
 
 struct rt_ctx {
@@ -36,6 +37,17 @@ struct rt_ctx {
     uint64_t cand_tiles = 0;        // allocated tiles
     std::vector<unsigned char> cand_key;
     float* d_srgb = nullptr;  // rt_srgb_thresholds table on the device (256 floats)
+    // hash(x*73) for x < hx_len and hash(y*51) for y < hy_len (wgsl:309-310)
+    uint32_t* d_hx = nullptr;
+    uint32_t* d_hy = nullptr;
+    uint32_t hx_len = 0, hy_len = 0;
+    // Sample counts of images this context wrote, when every pixel holds the same count:
+    // the source of TraceParams::hint_n (a hint only: the kernel verifies it per pixel).
+    struct CountRecord {
+        const void* image;
+        uint32_t w, h, rank, nranks, n;
+    };
+    std::vector<CountRecord> counts;
 };
 
 namespace {
@@ -224,6 +236,105 @@ rt_status ensure_candidates(rt_ctx* ctx, rtk::TraceParams& p, hipStream_t stream
     return RT_OK;
 }
 
+// Per-column / per-row halves of the pixel-invariant seed hash (wgsl:309-310), built on
+// the host once per image size.
+rt_status ensure_hash_tables(rt_ctx* ctx, uint32_t w, uint32_t h, hipStream_t stream) {
+    struct Table {
+        uint32_t** dev;
+        uint32_t* len;
+        uint32_t need, mul;
+    } tabs[2] = {{&ctx->d_hx, &ctx->hx_len, w, 73u}, {&ctx->d_hy, &ctx->hy_len, h, 51u}};
+    for (Table& t : tabs) {
+        if (*t.dev && *t.len >= t.need) continue;
+        std::vector<uint32_t> v(t.need);
+        for (uint32_t i = 0; i < t.need; ++i) v[i] = rtd::hash(i * t.mul);
+        uint32_t* d = nullptr;
+        hipError_t e = hipMalloc(&d, t.need * sizeof(uint32_t));
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(hash table)");
+        e = hipMemcpyAsync(d, v.data(), t.need * sizeof(uint32_t), hipMemcpyHostToDevice,
+                           stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);  // also retires old readers
+        if (e != hipSuccess) {
+            (void)hipFree(d);
+            return hip_fail(e, "hipMemcpyAsync(hash table)");
+        }
+        (void)hipFree(*t.dev);
+        *t.dev = d;
+        *t.len = t.need;
+    }
+    return RT_OK;
+}
+
+// ---- sample-count hints (TraceParams::hint_n) ------------------------------------------
+bool lookup_count(const rt_ctx* ctx, const void* image, const rtk::TraceParams& p,
+                  uint32_t& n) {
+    for (const rt_ctx::CountRecord& r : ctx->counts)
+        if (r.image == image && r.w == p.width && r.h == p.height && r.rank == p.band_first &&
+            r.nranks == p.band_step) {
+            n = r.n;
+            return true;
+        }
+    return false;
+}
+
+void forget_count(rt_ctx* ctx, const void* image) {
+    for (size_t i = 0; i < ctx->counts.size(); ++i)
+        if (ctx->counts[i].image == image) {
+            ctx->counts.erase(ctx->counts.begin() + (long)i);
+            return;
+        }
+}
+
+void record_count(rt_ctx* ctx, const void* image, const rtk::TraceParams& p, uint32_t n) {
+    forget_count(ctx, image);
+    if (ctx->counts.size() >= 16) ctx->counts.erase(ctx->counts.begin());
+    ctx->counts.push_back({image, p.width, p.height, p.band_first, p.band_step, n});
+}
+
+// The count a pixel holds after frame f of the kernel's loop, given the count before it
+// (wgsl:352-362, including the f32 round trip of the stored count).
+uint32_t next_count(uint32_t n, uint32_t spp) {
+    return host_f2u((float)(n < spp ? n + 1u : n));
+}
+
+// Fills p.hint_* for a launch whose input pixels all hold count n_in (frame 0 of a reset
+// launch: 0) and returns the count every pixel holds after the launch.
+uint32_t fill_hint(rtk::TraceParams& p, uint32_t n_in) {
+    const uint32_t spp = host_f2u(p.spp), depth = host_f2u(p.max_depth);
+    uint32_t hf = std::min<uint32_t>(p.frames, rtk::kHintFrames);
+    if (depth > 0) hf = std::min<uint32_t>(hf, rtk::kHintEntries / depth);
+    p.hint_frames = hf;
+    uint32_t n = n_in;
+    for (uint32_t f = 0; f < p.frames; ++f) {
+        if (f < hf) {
+            p.hint_n[f] = n;
+            const uint32_t B = host_f2u(p.seeds[f] * 4294967296.0f);
+            for (uint32_t i = 0; i < depth; ++i) {
+                // wgsl:268 with seed + 1 = n + B + 2 (wgsl:353, 358)
+                const uint32_t sb = rtd::hash(n + B + 2u + i * 1000u);
+                const float r_sb = rtd::rf(sb);
+                const rtd::v3 u = rtd::random_unit_vector(r_sb, sb);
+                p.hint_rs[f * depth + i] = make_float4(r_sb, u.x, u.y, u.z);
+            }
+        }
+        n = next_count(n, spp);
+    }
+    return n;
+}
+
+// Sets the hint of one launch from what the context knows about `in` and records the
+// count of `out` afterwards (or forgets it when unknown).
+void plan_hint(rt_ctx* ctx, rtk::TraceParams& p, const void* in, const void* out) {
+    uint32_t n_in = 0;
+    const bool known = p.reset_first || lookup_count(ctx, in, p, n_in);
+    if (!known) {
+        p.hint_frames = 0;
+        forget_count(ctx, out);
+        return;
+    }
+    record_count(ctx, out, p, fill_hint(p, p.reset_first ? 0u : n_in));
+}
+
 void fill_camera(rtk::TraceParams& p, const rt_scene_camera& c) {
     for (int i = 0; i < 3; ++i) {
         p.center[i] = c.center[i];
@@ -262,6 +373,9 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
     p.band_step = nranks;
     p.local_bands = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
     fill_camera(p, *cam);
+    if (rt_status s = ensure_hash_tables(ctx, w, h, stream)) return s;
+    p.hx = ctx->d_hx;
+    p.hy = ctx->d_hy;
     if (ctx->scan_mode == RT_SCAN_CULLED) {
         // Camera rays use the per-tile candidate lists; the LDS copy of the records only
         // serves the per-wave cone culling of bounce rays, so it is skipped at depth <= 1
@@ -298,6 +412,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         p.frames = nf;
         p.reset_first = (f0 == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
         std::memcpy(p.seeds, seeds + f0, nf * sizeof(float));
+        plan_hint(ctx, p, src, dst);
         hipError_t e = rtk::launch_trace(p, trace_kernel_for(ctx, p), stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         src = dst;  // later launches continue the accumulation in place
@@ -340,6 +455,8 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->d_geom);
         (void)hipFree(ctx->d_sph);
         (void)hipFree(ctx->d_srgb);
+        (void)hipFree(ctx->d_hx);
+        (void)hipFree(ctx->d_hy);
         free_candidates(ctx);
     }
     delete ctx;
@@ -369,7 +486,15 @@ rt_status rt_init_image(rt_ctx* ctx, float* out, uint32_t w, uint32_t h, void* s
     if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
     hipError_t e = rtk::launch_init(reinterpret_cast<float4*>(out), (uint64_t)w * h,
                                     static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? RT_OK : hip_fail(e, "rt_init_kernel launch");
+    if (e != hipSuccess) return hip_fail(e, "rt_init_kernel launch");
+    // every pixel now holds count 0 (for a whole-image update of this size)
+    rtk::TraceParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.width = w;
+    p.height = h;
+    p.band_step = 1;
+    record_count(ctx, out, p, 0u);
+    return RT_OK;
 }
 
 rt_status rt_update(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h,
@@ -409,6 +534,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         p.out = img[1 - cur];
         p.reset_first = (f == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
         p.seeds[0] = seeds[f];
+        plan_hint(ctx, p, p.in, p.out);
         hipError_t e = rtk::launch_trace(p, trace_kernel_for(ctx, p), stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         cur = 1 - cur;
@@ -444,6 +570,24 @@ rt_status rt_deinterleave_stripes(rt_ctx* ctx, const float* gathered, float* out
         reinterpret_cast<const float4*>(gathered), reinterpret_cast<float4*>(out), w, h,
         nranks, rt_stripe_local_rows(h, 0, nranks), static_cast<hipStream_t>(stream));
     return e == hipSuccess ? RT_OK : hip_fail(e, "rt_deinterleave_kernel launch");
+}
+
+rt_status rt_selftest_fastmath(rt_ctx* ctx, uint64_t n_random, uint64_t out[4]) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!out) return fail(RT_ERR_INVALID_ARGUMENT, "out is NULL");
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    unsigned long long* d = nullptr;
+    hipError_t e = hipMalloc(&d, 4 * sizeof(unsigned long long));
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(selftest)");
+    unsigned long long h[4] = {0, 0, 0, 0};
+    e = hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rtk::launch_selftest(d, n_random, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "rt_selftest_kernel");
+    for (int i = 0; i < 4; ++i) out[i] = h[i];
+    return RT_OK;
 }
 
 void rt_srgb_thresholds(float out[256]) {

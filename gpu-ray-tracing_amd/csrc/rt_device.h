@@ -1,12 +1,16 @@
-// rt_device.h — device-side restatement of the reference shader's per-pixel math
+// rt_device.h — restatement of the reference shader's per-pixel math
 // (assets/compute_shader.wgsl) for gfx950, under the canonical float semantics of
 // DESIGN.md §3 (explicit fmaf, IEEE sqrt/div, fixed sin/cos polynomial).  Compiled with
 // -ffp-contract=off so that no other fusion happens: the image is bit-identical to the
-// CPU oracle's.
+// CPU oracle's.  The RT_HD functions are also compiled for the host (csrc/rt_abi.cpp
+// precomputes per-frame random numbers with them), where they give the same bits.
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
+
+#define RT_HD __host__ __device__ __forceinline__
 
 namespace rtd {
 
@@ -14,23 +18,23 @@ struct v3 {
     float x, y, z;
 };
 
-__device__ __forceinline__ v3 mk(float x, float y, float z) { return v3{x, y, z}; }
-__device__ __forceinline__ v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ v3 mul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ v3 divs(v3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+RT_HD v3 mk(float x, float y, float z) { return v3{x, y, z}; }
+RT_HD v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+RT_HD v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+RT_HD v3 mul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+RT_HD v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
+RT_HD v3 divs(v3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
 // p + s*q (contracted)
-__device__ __forceinline__ v3 fmas(float s, v3 q, v3 p) {
+RT_HD v3 fmas(float s, v3 q, v3 p) {
     return mk(fmaf(s, q.x, p.x), fmaf(s, q.y, p.y), fmaf(s, q.z, p.z));
 }
-__device__ __forceinline__ float dot(v3 a, v3 b) {
+RT_HD float dot(v3 a, v3 b) {
     return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x));
 }
-__device__ __forceinline__ v3 normalize(v3 v) { return divs(v, sqrtf(dot(v, v))); }
+RT_HD v3 normalize(v3 v) { return divs(v, sqrtf(dot(v, v))); }
 
 // wgsl:50-59.  Three v_mul_lo_u32 (quarter rate) — the RNG's cost per call.
-__device__ __forceinline__ uint32_t hash(uint32_t s) {
+RT_HD uint32_t hash(uint32_t s) {
     s ^= 2747636419u;
     s *= 2654435769u;
     s ^= s >> 16;
@@ -40,17 +44,17 @@ __device__ __forceinline__ uint32_t hash(uint32_t s) {
     return s;
 }
 // wgsl:61-63: f32(hash) / 4294967295.0 where the literal rounds to 2^32 in f32.
-__device__ __forceinline__ float rf(uint32_t v) { return (float)hash(v) * 0x1p-32f; }
+RT_HD float rf(uint32_t v) { return (float)hash(v) * 0x1p-32f; }
 
 // WGSL u32(f32): truncate, saturate, NaN -> 0 (what v_cvt_u32_f32 does).
 // Branch-free (selects only): NaN and negatives go through fmaxf to 0.
-__device__ __forceinline__ uint32_t f2u(float f) {
+RT_HD uint32_t f2u(float f) {
     const uint32_t t = (uint32_t)fminf(fmaxf(f, 0.0f), 4294967040.0f);  // largest f32 < 2^32
     return f >= 4294967296.0f ? 0xFFFFFFFFu : t;
 }
 
 // Canonical sin/cos: Cody-Waite by pi/2 in three parts, Cephes minimax.
-__device__ __forceinline__ void sincos_c(float x, float& s, float& c) {
+RT_HD void sincos_c(float x, float& s, float& c) {
     const float q = rintf(x * 0x1.45f306p-1f);
     const int k = (q == q) ? (int)q : 0;
     float r = fmaf(q, -0x1.921fb6p+0f, x);
@@ -69,7 +73,7 @@ __device__ __forceinline__ void sincos_c(float x, float& s, float& c) {
 }
 
 // wgsl:234-243; rf_seed = rf(seed)
-__device__ __forceinline__ v3 random_unit_vector(float rf_seed, uint32_t seed) {
+RT_HD v3 random_unit_vector(float rf_seed, uint32_t seed) {
     const float z = fmaf(2.0f, rf_seed, -1.0f);
     const float a = rf(seed + 1u) * 0x1.921fb6p+2f;  // 6.283185307 as f32
     const float r = sqrtf(fmaf(-z, z, 1.0f));
@@ -79,13 +83,13 @@ __device__ __forceinline__ v3 random_unit_vector(float rf_seed, uint32_t seed) {
 }
 
 // WGSL reflect(e1,e2) = e1 - 2*dot(e2,e1)*e2
-__device__ __forceinline__ v3 reflect(v3 e1, v3 e2) {
+RT_HD v3 reflect(v3 e1, v3 e2) {
     const float k = 2.0f * dot(e2, e1);
     return fmas(-k, e2, e1);
 }
 
 // WGSL refract(e1,e2,eta)
-__device__ __forceinline__ v3 refract(v3 e1, v3 e2, float eta) {
+RT_HD v3 refract(v3 e1, v3 e2, float eta) {
     const float d = dot(e2, e1);
     const float k = fmaf(-(eta * eta), fmaf(-d, d, 1.0f), 1.0f);
     if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
@@ -95,12 +99,51 @@ __device__ __forceinline__ v3 refract(v3 e1, v3 e2, float eta) {
 }
 
 // wgsl:137-141, pow(x, 5.0) = ((x*x)*(x*x))*x
-__device__ __forceinline__ float reflectance(float cos_t, float ri) {
+RT_HD float reflectance(float cos_t, float ri) {
     float r0 = (1.0f - ri) / (1.0f + ri);
     r0 = r0 * r0;
     const float x = 1.0f - cos_t;
     const float x2 = x * x;
     return fmaf(1.0f - r0, (x2 * x2) * x, r0);
+}
+
+// ---- Exact fast paths of the IEEE f32 division and square root ---------------------
+//
+// The compiler's correctly rounded a / b (the parity contract) on gfx950 is
+//   b' = v_div_scale(b), a' = v_div_scale(a), r = v_rcp(b'), y = fma(fma(-b', r, 1), r, r),
+//   q0 = a'*y, q1 = fma(fma(-b', q0, a'), y, q0), q2 = v_div_fmas(fma(-b', q1, a'), y, q1),
+//   result = v_div_fixup(q2, b, a).
+// When a and b are +-0 or have magnitudes in [2^-40, 2^40] (b nonzero), div_scale returns
+// its operand unchanged and asks for no rescaling (the exponent gap stays below 96, a/b,
+// 1/b and a stay far from the subnormal range), div_fmas is then a plain fma and div_fixup
+// only restores the quotient's sign for a == +-0.  div_core is that unscaled arithmetic,
+// so on this domain it returns exactly the bits of a / b — and y, which depends on b only,
+// is shared by every division by the same b.  sqrt_core is likewise the compiler's
+// correctly rounded sqrtf without its rescaling of x < 2^-96 and its +-0 / +inf fix-up,
+// exact for x == +0 and for x in [2^-96, 2^126].  Callers state why their operands are in
+// the domain (or test it); tests/test_gpu_parity.py::test_fastmath_selftest checks both
+// against the IEEE operations on the GPU.
+__device__ __forceinline__ float rcp_refined(float b) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    return fmaf(fmaf(-b, r, 1.0f), r, r);
+}
+// a / b for a != -0 (with b > 0) — the only case where the unscaled core gets the sign of a
+// zero quotient wrong; div_core_signed below covers every sign.
+__device__ __forceinline__ float div_core(float a, float b, float y) {
+    const float q0 = a * y;
+    const float q1 = fmaf(fmaf(-b, q0, a), y, q0);
+    return fmaf(fmaf(-b, q1, a), y, q1);
+}
+__device__ __forceinline__ float div_core_signed(float a, float b, float y) {
+    const float q0 = a * y;                       // carries sign(a) ^ sign(b), also for a == 0
+    return copysignf(div_core(a, b, y), q0);
+}
+__device__ __forceinline__ float sqrt_core(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float s_dn = __int_as_float(__float_as_int(s) - 1);
+    const float s_up = __int_as_float(__float_as_int(s) + 1);
+    const float t = fmaf(-s_dn, s, x) <= 0.0f ? s_dn : s;
+    return fmaf(-s_up, s, x) > 0.0f ? s_up : t;
 }
 
 }  // namespace rtd

@@ -17,6 +17,11 @@ constexpr uint32_t kLdsMaxRecords = 4096;
 // Per-tile candidate lists of camera rays (culled scan): capacity and the "no list" mark.
 constexpr uint32_t kCandMax = 32;
 constexpr uint32_t kCandNone = 0xFFFFFFFFu;
+// Sample-count hint (see TraceParams::hint_n): per-(frame, bounce) random numbers of the
+// scatter step for at most kHintEntries (frame, bounce) pairs of the first kHintFrames
+// frames of a launch.
+constexpr uint32_t kHintFrames = 16;
+constexpr uint32_t kHintEntries = 16;
 
 // Everything the `update` kernel needs, passed by value (kernarg -> SGPRs).
 struct TraceParams {
@@ -33,8 +38,22 @@ struct TraceParams {
     const uint32_t* cand_cnt;  // [tile] listed spheres, kCandNone = no list
     const float4* cand_rec;    // [tile][cand_k] their scan records, in index order, padded
     const float4* cand_sph;    // [tile][cand_k][2] their 32-B GpuSphere records
+    const uint32_t* hx;    // [width]  hash(x * 73)  (wgsl:309, pixel-invariant)
+    const uint32_t* hy;    // [height] hash(y * 51)  (wgsl:310)
     float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3];
     float defocus_angle, max_depth, spp;
+    // Sample-count hint.  The scatter step's random numbers depend only on the pixel's
+    // sample count n, the frame seed and the bounce (sb = hash(n + B + 2 + 1000 i),
+    // wgsl:268, 353), not on the pixel.  When the host knows the count every pixel of `in`
+    // holds (it wrote the image, or the frame resets it), hint_n[f] is that count at
+    // frame f and hint_rs[f * depth + i] = (rf(sb), random_unit_vector(sb)) for the
+    // first hint_frames frames.  Waves whose live pixels all hold hint_n[f] use these
+    // values and a scalar camera seed; the accumulator load is then only awaited after
+    // the sample is traced, and any pixel whose loaded count differs is traced again with
+    // its own count — so the hint never changes a bit of the result.
+    uint32_t hint_frames;  // 0 = no hint
+    uint32_t hint_n[kHintFrames];
+    float4 hint_rs[kHintEntries];
     float seeds[kMaxFramesPerLaunch];
 };
 
@@ -57,5 +76,7 @@ hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t wid
 hipError_t launch_present(const float4* in, uchar4* out, uint64_t texels,
                           const float* srgb_t, hipStream_t stream);
 const char* trace_kernel_name();
+// Exact fast-path self-test (rt_selftest_fastmath): cnt[4] device counters, zeroed.
+hipError_t launch_selftest(unsigned long long* cnt, uint64_t n_rand, hipStream_t stream);
 
 }  // namespace rtk

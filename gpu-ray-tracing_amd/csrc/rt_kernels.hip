@@ -342,10 +342,11 @@ struct Cam {
 };
 
 // get_ray (wgsl:305-325) with the pixel-invariant hash(hash(x*73) ^ hash(y*51)) part
-// precomputed per pixel: seed = hash(hxy ^ (sample_index*25 + B)).
+// precomputed per pixel: seed = hash(hxy ^ su), su = sample_index*25 + B (wave-uniform
+// when every pixel of the wave holds the same sample count).
 __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, uint32_t hxy,
-                                        uint32_t sample_index, uint32_t B, v3& o, v3& d) {
-    const uint32_t seed = hash(hxy ^ (sample_index * 25u + B));
+                                        uint32_t su, v3& o, v3& d) {
+    const uint32_t seed = hash(hxy ^ su);
     const float offx = rf(seed) - 0.5f;                 // sample_square wgsl:299-303
     const float offy = rf(seed * seed) - 0.5f;
     const float sx = ((float)x + 0.5f) + offx;
@@ -355,8 +356,13 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
         const float ang = 0x1.921fb4p+2f * rf(seed + 1u);  // 2.0*3.1415926 as f32
         float sa, ca;
         sincos_c(ang, sa, ca);
-        const float len = sqrtf(fmaf(sa, sa, ca * ca));
-        o = fmas(sa / len, cam.ddv, fmas(ca / len, cam.ddu, cam.center));
+        // normalize((ca, sa)): over all 2^32 values of hash(seed + 1), len2 lies in
+        // [1 - 6*2^-24, 1 + 2^-23], |sa| >= 2^-30 or sa == +0, |ca| >= 2^-27 (checked
+        // exhaustively, tests/test_gpu_parity.py::test_fastmath_selftest), inside the exact
+        // domain of sqrt_core / div_core: the same bits as sqrtf and the two IEEE divides.
+        const float len = sqrt_core(fmaf(sa, sa, ca * ca));
+        const float y = rcp_refined(len);
+        o = fmas(div_core(sa, len, y), cam.ddv, fmas(div_core(ca, len, y), cam.ddu, cam.center));
     } else {
         o = cam.center;
     }
@@ -367,9 +373,14 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
 // is still being traced; the bounce loop runs while any lane is live, and a lane's
 // values are only updated while it is live, so each lane computes exactly its own
 // per-pixel result.
+// uni (wave-uniform): every live lane of the wave holds the hinted sample count of frame
+// f, so the scatter step's random numbers (pixel-independent, see TraceParams::hint_n)
+// come from the host-computed hint_rs table instead of three hashes, a sqrt and a sincos
+// per lane.
 template <int kScan>
 __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uint32_t ncand,
-                                        uint32_t depth, v3 o, v3 d, uint32_t seed, bool live) {
+                                        uint32_t depth, v3 o, v3 d, uint32_t seed, bool live,
+                                        bool uni, uint32_t f) {
     v3 cf = mk(1.0f, 1.0f, 1.0f);
     bool black = false;
     for (uint32_t i = 0; i < depth; ++i) {
@@ -407,9 +418,17 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
         // first component), so they are computed while the loads are in flight.
         const float4 pr = hs[2 * hit.idx];          // position, radius
         const float4 mat = hs[2 * hit.idx + 1];     // material color
-        const uint32_t sb = hash(seed + i * 1000u);               // wgsl:268
-        const float r_sb = rf(sb);
-        const v3 ruv = random_unit_vector(r_sb, sb);
+        float r_sb;
+        v3 ruv;
+        if (uni) {
+            const float4 h = p.hint_rs[f * depth + i];
+            r_sb = h.x;
+            ruv = mk(h.y, h.z, h.w);
+        } else {
+            const uint32_t sb = hash(seed + i * 1000u);           // wgsl:268
+            r_sb = rf(sb);
+            ruv = random_unit_vector(r_sb, sb);
+        }
         const v3 hp = fmas(hit.t, d, o);
         const v3 C = mk(pr.x, pr.y, pr.z);
         const v3 outward = divs(sub(hp, C), pr.w);
@@ -476,41 +495,76 @@ __device__ __forceinline__ TileCoord tile_coord(const TraceParams& p, uint32_t t
     return t;
 }
 
+// One sample of one frame for the pixels with `live` set, traced with sample count n
+// (wgsl:352-358 without the accumulation).
+template <int kScan>
+__device__ __forceinline__ v3 sample(const TraceParams& p, const Cam& cam, uint32_t tile,
+                                     uint32_t ncand, const TileCoord& tc, uint32_t hxy,
+                                     uint32_t n, uint32_t B, uint32_t f, bool live, bool uni) {
+    const uint32_t depth = f2u(p.max_depth);
+    const uint32_t seed = 1u + n + B;                             // wgsl:353
+    v3 o, d;
+    STAMP(0);
+#if RT_KO & 4
+    o = cam.center;
+    d = sub(fmas((float)tc.y, cam.pdv, fmas((float)tc.x, cam.pdu, cam.vul)), o);
+#else
+    get_ray(cam, tc.x, tc.y, hxy, seed * 25u + B, o, d);          // wgsl:311
+#endif
+    STAMP(1);
+    const v3 col = ray_color<kScan>(p, tile, ncand, depth, o, d, seed + 1u, live, uni, f);
+    STAMP(4);
+    return col;
+}
+
+// acc: the pixel's loaded accumulator (unused when frame 0 resets it).  Without a hint the
+// count is taken from acc before the first sample; with a hint the first frame is traced
+// with the hinted count while the load is in flight and verified afterwards.
 template <int kScan>
 __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& cam,
                                               uint32_t tile, uint32_t ncand,
-                                              const TileCoord& tc, float4 acc) {
-    v3 c = mk(acc.x, acc.y, acc.z);                               // wgsl:339-341
-    uint32_t n = f2u(acc.w);
+                                              const TileCoord& tc, uint32_t hxy, float4 acc) {
     const uint32_t spp = f2u(p.spp);                              // wgsl:343
-    const uint32_t depth = f2u(p.max_depth);
-    const uint32_t hxy = hash(tc.x * 73u) ^ hash(tc.y * 51u);     // wgsl:309-310
+    v3 c = mk(0.0f, 0.0f, 0.0f);
+    uint32_t n = 0u;
+    bool known = p.reset_first != 0u;                             // wgsl:345-350
+    if (!known && p.hint_frames == 0u) {
+        c = mk(acc.x, acc.y, acc.z);                              // wgsl:339-341
+        n = f2u(acc.w);
+        known = true;
+    }
     for (uint32_t f = 0; f < p.frames; ++f) {
         const uint32_t B = f2u(p.seeds[f] * 4294967296.0f);      // wgsl:311,353
         if (f == 0 && p.reset_first) {                            // wgsl:345-350
             c = mk(0.0f, 0.0f, 0.0f);
             n = 0u;
         }
-        const bool live = tc.valid && n < spp;                    // wgsl:352
-        if (__ballot(live) != 0ull) {
-            const uint32_t seed = 1u + n + B;
-            v3 o, d;
-            STAMP(0);
-#if RT_KO & 4
-            o = cam.center;
-            d = sub(fmas((float)tc.y, cam.pdv, fmas((float)tc.x, cam.pdu, cam.vul)), o);
-#else
-            get_ray(cam, tc.x, tc.y, hxy, seed, B, o, d);
-#endif
-            STAMP(1);
-            const v3 col = ray_color<kScan>(p, tile, ncand, depth, o, d, seed + 1u, live);
-            STAMP(4);
-            if (live) {
+        const bool hinted = f < p.hint_frames;
+        uint32_t ng = known ? n : p.hint_n[0];   // count to trace with (unknown: f == 0)
+        bool pending = tc.valid;
+        for (;;) {
+            const bool live = pending && ng < spp;                // wgsl:352
+            v3 col = mk(0.0f, 0.0f, 0.0f);
+            if (__ballot(live) != 0ull) {
+                const bool uni = hinted && __ballot(live && ng != p.hint_n[f]) == 0ull;
+                col = sample<kScan>(p, cam, tile, ncand, tc, hxy, ng, B, f, live, uni);
+            }
+            bool wrong = false;
+            if (!known) {                                         // verify the hint
+                c = mk(acc.x, acc.y, acc.z);
+                n = f2u(acc.w);
+                known = true;
+                wrong = pending && n != ng;
+            }
+            if (pending && !wrong && n < spp) {
                 const float k = (float)(n + 1u);                  // wgsl:356
                 c = mk(c.x + (col.x - c.x) / k, c.y + (col.y - c.y) / k,
                        c.z + (col.z - c.z) / k);
                 n += 1u;
             }
+            if (__ballot(wrong) == 0ull) break;
+            pending = wrong;                                      // retrace these pixels
+            ng = n;
         }
         // The chained form stores f32(n) and reloads u32(.) each frame (wgsl:341,362).
         n = f2u((float)n);
@@ -567,8 +621,12 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
 #if RT_KO & 8
     const float4 acc = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
 #else
-    const float4 acc = p.in[tc.valid ? tc.idx : 0];               // wgsl:339
+    // wgsl:339 (a frame-0 reset discards the value: no load)
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (!p.reset_first) acc = p.in[tc.valid ? tc.idx : 0];
 #endif
+    // hash(x*73) ^ hash(y*51) (wgsl:309-310) from the per-column / per-row tables
+    const uint32_t hxy = p.hx[min(tc.x, p.width - 1u)] ^ p.hy[min(tc.y, p.height - 1u)];
 
     Cam cam;
     cam.center = mk(p.center[0], p.center[1], p.center[2]);
@@ -579,7 +637,7 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     cam.ddv = mk(p.ddv[0], p.ddv[1], p.ddv[2]);
     cam.defocus_angle = p.defocus_angle;
 
-    const float4 res = trace_pixel<kScan>(p, cam, tile, ncand, tc, acc);
+    const float4 res = trace_pixel<kScan>(p, cam, tile, ncand, tc, hxy, acc);
 #if RT_KO & 16
     if (res.x == 12345.678f) p.out[tc.idx] = res;
 #else
@@ -683,6 +741,63 @@ __global__ __launch_bounds__(256) void rt_present_kernel(const float4* __restric
         const float4 v = in[i];
         out[i] = make_uchar4((uint8_t)enc(v.x), (uint8_t)enc(v.y), (uint8_t)enc(v.z), 255);
     }
+}
+
+// ---- Self-test of the exact fast paths (rt_selftest_fastmath) ------------------------
+// cnt[0]: defocus normalisation, all 2^32 values of hash(seed + 1): fast vs IEEE bits.
+// cnt[1]: div_core_signed vs a / b on random a, b in the documented domain (a also +-0,
+//         b also small integers: the accumulator's n + 1).
+// cnt[2]: sqrt_core vs sqrtf on random x in [2^-96, 2^126], every f32 in [0.25, 4), +0.
+// cnt[3]: cases run.
+__device__ __forceinline__ uint32_t mix32(uint64_t i, uint32_t salt) {
+    return hash((uint32_t)i ^ hash((uint32_t)(i >> 32) + salt));
+}
+__device__ __forceinline__ float rand_in_domain(uint32_t r, uint32_t e) {
+    // sign from r's top bit, mantissa from r, exponent e in [-40, 39]
+    const uint32_t bits = (r & 0x807FFFFFu) | ((uint32_t)(127 - 40 + (int)(e % 80u)) << 23);
+    return __uint_as_float(bits);
+}
+__global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cnt, uint64_t n_rand) {
+    unsigned long long bad0 = 0, bad1 = 0, bad2 = 0, runs = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32);
+         i += stride) {
+        const float ang = 0x1.921fb4p+2f * rf((uint32_t)i);
+        float sa, ca;
+        sincos_c(ang, sa, ca);
+        const float len_ref = sqrtf(fmaf(sa, sa, ca * ca));
+        const float len = sqrt_core(fmaf(sa, sa, ca * ca));
+        const float y = rcp_refined(len);
+        bad0 += (__float_as_uint(div_core(sa, len, y)) != __float_as_uint(sa / len_ref)) ||
+                (__float_as_uint(div_core(ca, len, y)) != __float_as_uint(ca / len_ref));
+        ++runs;
+    }
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_rand; i += stride) {
+        const uint32_t r0 = mix32(i, 1u), r1 = mix32(i, 2u), r2 = mix32(i, 3u);
+        float a = rand_in_domain(r0, r2 & 0xFFFFu);
+        float b = rand_in_domain(r1, r2 >> 16);
+        if ((r2 & 0x700u) == 0) a = (r0 & 1u) ? -0.0f : 0.0f;
+        if ((r2 & 0x3800u) == 0) b = (float)(1u + (r1 & 0xFFFFFFu));   // n + 1 counts
+        const float yb = rcp_refined(b);
+        bad1 += __float_as_uint(div_core_signed(a, b, yb)) != __float_as_uint(a / b);
+        const float x = __uint_as_float((r0 & 0x7FFFFFu) |
+                                        ((uint32_t)(127 - 96 + (int)(r1 % 222u)) << 23));
+        bad2 += __float_as_uint(sqrt_core(x)) != __float_as_uint(sqrtf(x));
+        const float z = __uint_as_float(0x3E800000u + (uint32_t)(i & 0x1FFFFFFu));  // [0.25, 4)
+        bad2 += __float_as_uint(sqrt_core(z)) != __float_as_uint(sqrtf(z));
+        ++runs;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        bad2 += __float_as_uint(sqrt_core(0.0f)) != __float_as_uint(sqrtf(0.0f));
+    atomicAdd(&cnt[0], bad0);
+    atomicAdd(&cnt[1], bad1);
+    atomicAdd(&cnt[2], bad2);
+    atomicAdd(&cnt[3], runs);
+}
+
+hipError_t launch_selftest(unsigned long long* cnt, uint64_t n_rand, hipStream_t stream) {
+    hipLaunchKernelGGL(rt_selftest_kernel, dim3(8192), dim3(256), 0, stream, cnt, n_rand);
+    return hipGetLastError();
 }
 
 // 256-thread workgroups: 4 waves = 4 tiles along a stripe band; grid (columns/4, bands).

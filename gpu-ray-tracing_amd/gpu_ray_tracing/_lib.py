@@ -112,6 +112,7 @@ _SIGS = {
     "rt_driver_state": (ctypes.c_int, [P]),
     "rt_present_rgba8": (ctypes.c_int, [P, P, P, U32, U32, ctypes.c_int, P]),
     "rt_srgb_thresholds": (None, [P]),
+    "rt_selftest_fastmath": (ctypes.c_int, [P, ctypes.c_uint64, P]),
 }
 
 _lib = None

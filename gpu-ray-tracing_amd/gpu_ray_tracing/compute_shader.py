@@ -63,6 +63,12 @@ class ComputeShaderPipeline:
             _lib.call("rt_destroy", self._ctx)
             self._ctx = ctypes.c_void_p()
 
+    def selftest_fastmath(self, n_random: int = 1 << 26) -> list[int]:
+        """rt_selftest_fastmath: [defocus, division, sqrt mismatches, cases run]."""
+        out = (ctypes.c_uint64 * 4)()
+        _lib.call("rt_selftest_fastmath", self._ctx, n_random, out)
+        return list(out)
+
     def __del__(self):
         try:
             self.close()

@@ -212,6 +212,14 @@ RT_API rt_status rt_present_rgba8(rt_ctx* ctx, const float* in_rgba, uint8_t* ou
  * encoding is (j - 0.5) / 255, computed in double (IEC 61966-2-1 curve). */
 RT_API void rt_srgb_thresholds(float out[256]);
 
+/* Diagnostic (no reference counterpart): checks on the device that the exact fast paths
+ * of f32 division and sqrt used by the trace kernel (rt_device.h: div_core, sqrt_core)
+ * return the IEEE bits on their documented domains — exhaustively for the defocus-disk
+ * normalisation (all 2^32 values of its random input) and on n_random random cases for
+ * division and sqrt.  out[0..2] = mismatches (defocus, division, sqrt), out[3] = cases.
+ * Synchronous. */
+RT_API rt_status rt_selftest_fastmath(rt_ctx* ctx, uint64_t n_random, uint64_t out[4]);
+
 /* ------------------------------------------------------------------------------------ */
 /* Host-side mirror of the reference's main-world code (C++ implementation, no device)   */
 /* ------------------------------------------------------------------------------------ */

@@ -489,3 +489,40 @@ def test_image_files_from_device(rt, pipe, tmp_path):
     np.testing.assert_array_equal(rt.image_io.load_png(tmp_path / "f.png"),
                                   P.present(host(b), "srgb"))
     assert np.load(tmp_path / "f.npy").tobytes() == host(b).tobytes()
+
+
+def test_fastmath_selftest(rt):
+    """The exact fast paths of division / sqrt (rt_device.h) return the IEEE bits: all 2^32
+    inputs of the defocus-disk normalisation, 2^26 random division and sqrt cases."""
+    p = rt.ComputeShaderPipeline(0)
+    out = p.selftest_fastmath(1 << 26)
+    p.close()
+    assert out[:3] == [0, 0, 0], out
+    assert out[3] == (1 << 32) + (1 << 26)
+
+
+@pytest.mark.parametrize("depth,spp", [(1, 500), (3, 3), (8, 500)])
+def test_hinted_chain_matches_oracle(rt, oracle, pipe, depth, spp):
+    """Chained updates the library can hint (init, reset, then its own outputs), including
+    the spp cap, and an image rewritten behind the library's back mid-chain (all pixels,
+    then some pixels, with counts other than the hinted one)."""
+    w, h = 40, 24
+    sc = rt.synthetic_scene(500)
+    seeds = rt.frame_seeds(5, 6)
+    cur, nxt = pipe.new_image(w, h), pipe.new_image(w, h)
+    pipe.init_image(cur, w, h)
+    ref = np.zeros((h, w, 4), np.float32)
+    for f in range(6):
+        cam = camera(rt, w, h, depth=depth, spp=spp, moved=(f == 2), seed=float(seeds[f]))
+        if f == 3:   # every pixel: a count the hint does not expect
+            ref = ref.copy()
+            ref[..., 3] += 1.0
+            cur.copy_(to_dev(ref))
+        if f == 4:   # one pixel only
+            ref = ref.copy()
+            ref[3, 5, 3] = 0.0
+            cur.copy_(to_dev(ref))
+        pipe.update(cur, nxt, w, h, cam, sc)
+        ref, _ = oracle.update(ref, cam.blob, sc.spheres)
+        cur, nxt = nxt, cur
+        assert_same(host(cur), ref)
