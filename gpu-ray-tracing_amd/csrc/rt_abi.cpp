@@ -93,7 +93,7 @@ uint32_t host_f2u(float f) {
 int trace_kernel_for(const rt_ctx* ctx, const rtk::TraceParams& p) {
     if (ctx->scan_mode == RT_SCAN_EXHAUSTIVE) return rtk::kTraceExhaustive;
 #ifndef RT_FORCE_CULLED_KERNEL
-    if (host_f2u(p.max_depth) <= 1u) return rtk::kTraceList;
+    if (p.depth <= 1u) return rtk::kTraceList;
 #endif
     return rtk::kTraceCulled;
 }
@@ -300,7 +300,7 @@ uint32_t next_count(uint32_t n, uint32_t spp) {
 // Fills p.hint_* for a launch whose input pixels all hold count n_in (frame 0 of a reset
 // launch: 0) and returns the count every pixel holds after the launch.
 uint32_t fill_hint(rtk::TraceParams& p, uint32_t n_in) {
-    const uint32_t spp = host_f2u(p.spp), depth = host_f2u(p.max_depth);
+    const uint32_t spp = p.spp, depth = p.depth;
     uint32_t hf = std::min<uint32_t>(p.frames, rtk::kHintFrames);
     if (depth > 0) hf = std::min<uint32_t>(hf, rtk::kHintEntries / depth);
     p.hint_frames = hf;
@@ -308,7 +308,7 @@ uint32_t fill_hint(rtk::TraceParams& p, uint32_t n_in) {
     for (uint32_t f = 0; f < p.frames; ++f) {
         if (f < hf) {
             p.hint_n[f] = n;
-            const uint32_t B = host_f2u(p.seeds[f] * 4294967296.0f);
+            const uint32_t B = p.seed_b[f];
             for (uint32_t i = 0; i < depth; ++i) {
                 // wgsl:268 with seed + 1 = n + B + 2 (wgsl:353, 358)
                 const uint32_t sb = rtd::hash(n + B + 2u + i * 1000u);
@@ -345,8 +345,8 @@ void fill_camera(rtk::TraceParams& p, const rt_scene_camera& c) {
         p.ddv[i] = c.defocus_disk_v[i];
     }
     p.defocus_angle = c.defocus_angle;
-    p.max_depth = c.max_depth;
-    p.spp = c.samples_per_pixel;
+    p.depth = host_f2u(c.max_depth);
+    p.spp = host_f2u(c.samples_per_pixel);
 }
 
 // Common setup of every trace launch: argument checks, scene upload, kernel parameters
@@ -411,7 +411,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         p.out = dst;
         p.frames = nf;
         p.reset_first = (f0 == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
-        std::memcpy(p.seeds, seeds + f0, nf * sizeof(float));
+        for (uint32_t f = 0; f < nf; ++f) p.seed_b[f] = host_f2u(seeds[f0 + f] * 4294967296.0f);
         plan_hint(ctx, p, src, dst);
         hipError_t e = rtk::launch_trace(p, trace_kernel_for(ctx, p), stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
@@ -533,7 +533,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         p.in = img[cur];
         p.out = img[1 - cur];
         p.reset_first = (f == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
-        p.seeds[0] = seeds[f];
+        p.seed_b[0] = host_f2u(seeds[f] * 4294967296.0f);
         plan_hint(ctx, p, p.in, p.out);
         hipError_t e = rtk::launch_trace(p, trace_kernel_for(ctx, p), stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");

@@ -120,15 +120,16 @@ RT_HD float reflectance(float cos_t, float ri) {
 // so on this domain it returns exactly the bits of a / b — and y, which depends on b only,
 // is shared by every division by the same b.  sqrt_core is likewise the compiler's
 // correctly rounded sqrtf without its rescaling of x < 2^-96 and its +-0 / +inf fix-up,
-// exact for x == +0 and for x in [2^-96, 2^126].  Callers state why their operands are in
-// the domain (or test it); tests/test_gpu_parity.py::test_fastmath_selftest checks both
-// against the IEEE operations on the GPU.
+// exact for x == +0 and for x in [2^-96, +inf].  Used where the operands are in the domain
+// by construction (the defocus-disk normalisation, get_ray);
+// tests/test_gpu_parity.py::test_fastmath_selftest checks both against the IEEE operations
+// on the GPU.
 __device__ __forceinline__ float rcp_refined(float b) {
     const float r = __builtin_amdgcn_rcpf(b);
     return fmaf(fmaf(-b, r, 1.0f), r, r);
 }
-// a / b for a != -0 (with b > 0) — the only case where the unscaled core gets the sign of a
-// zero quotient wrong; div_core_signed below covers every sign.
+// a / b except for a == -0 with b > 0 (the one case where the unscaled core gets the sign
+// of a zero quotient wrong); div_core_signed below covers every sign.
 __device__ __forceinline__ float div_core(float a, float b, float y) {
     const float q0 = a * y;
     const float q1 = fmaf(fmaf(-b, q0, a), y, q0);
@@ -145,5 +146,7 @@ __device__ __forceinline__ float sqrt_core(float x) {
     const float t = fmaf(-s_dn, s, x) <= 0.0f ? s_dn : s;
     return fmaf(-s_up, s, x) > 0.0f ? s_up : t;
 }
+
+
 
 }  // namespace rtd

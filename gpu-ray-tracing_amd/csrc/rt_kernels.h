@@ -41,7 +41,11 @@ struct TraceParams {
     const uint32_t* hx;    // [width]  hash(x * 73)  (wgsl:309, pixel-invariant)
     const uint32_t* hy;    // [height] hash(y * 51)  (wgsl:310)
     float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3];
-    float defocus_angle, max_depth, spp;
+    float defocus_angle;
+    // u32(max_depth), u32(samples_per_pixel) (camera.rs:343, wgsl:343, 268) and per frame
+    // B = u32(random_seed * 4294967296.0) (wgsl:311, 353), converted on the host with the
+    // kernel's own f32 -> u32 rule.
+    uint32_t depth, spp;
     // Sample-count hint.  The scatter step's random numbers depend only on the pixel's
     // sample count n, the frame seed and the bounce (sb = hash(n + B + 2 + 1000 i),
     // wgsl:268, 353), not on the pixel.  When the host knows the count every pixel of `in`
@@ -54,7 +58,7 @@ struct TraceParams {
     uint32_t hint_frames;  // 0 = no hint
     uint32_t hint_n[kHintFrames];
     float4 hint_rs[kHintEntries];
-    float seeds[kMaxFramesPerLaunch];
+    uint32_t seed_b[kMaxFramesPerLaunch];
 };
 
 // Trace kernel instances: the reference's exhaustive scan; per-tile candidate lists for

@@ -85,7 +85,9 @@ __device__ __forceinline__ float discriminant(const float4 g, v3 o, v3 d, float 
 }
 
 // Root selection of wgsl:189-201 for sphere i, given its discriminant.  (Callers only
-// pass indices < count.)
+// pass indices < count.)  The IEEE sqrt and divisions are kept as the compiler emits them:
+// exact unscaled fast paths with per-lane domain checks measured slower here (the checks
+// and their branches cost more SALU/VALU issue than the shorter sequences save).
 __device__ __forceinline__ void consider(float disc, float h, float a, uint32_t i, float& tmax,
                                          int& idx) {
     if (!(disc < 0.0f)) {                                               // wgsl:189
@@ -106,9 +108,6 @@ __device__ __forceinline__ void consider(float disc, float h, float a, uint32_t 
 // compare per chunk (max_bits below).
 
 // Exhaustive scan: the reference's linear walk over every sphere (wgsl:169-177).
-#ifndef RT_SCAN_CHUNK
-#define RT_SCAN_CHUNK 4
-#endif
 
 // max over the int32 views of K discriminants
 template <int K>
@@ -119,15 +118,29 @@ __device__ __forceinline__ int max_bits(const float (&dd)[K]) {
     return m;
 }
 
+// Chunk sizes: a full-list walk is 4 spheres per s_load_dwordx16 (267 us at K3 against
+// 330 us one sphere at a time).  The list-only kernel (max_depth <= 1) walks the short
+// per-tile candidate lists (2.7 spheres on average at K3) 2 at a time, testing fewer
+// padding records (-2 % at K3; mixing both sizes in one kernel measured slower).
+#ifndef RT_SCAN_CHUNK
+#define RT_SCAN_CHUNK 4
+#endif
+#ifndef RT_LIST_CHUNK
+#define RT_LIST_CHUNK 2
+#endif
+template <int kScan>
+constexpr int scan_chunk() { return kScan == kTraceList ? RT_LIST_CHUNK : RT_SCAN_CHUNK; }
+
+template <int K>
 __device__ __forceinline__ Hit scan_exhaustive(const float4* __restrict__ geom, uint32_t count,
                                                v3 o, v3 d) {
-    constexpr int K = RT_SCAN_CHUNK;
-    const float a = dot(d, d);                 // wgsl:184 (ray-invariant)
     float tmax = 0x1.05ed2ep+118f;             // 3.4e35 (wgsl:266)
     int idx = -1;
+    if (count == 0) return Hit{idx, tmax};
+    const float a = dot(d, d);                 // wgsl:184 (ray-invariant)
     // The record list is zero-padded to whole chunks plus one chunk more (rt_abi.cpp), so
-    // every chunk (and the one-ahead prefetch) is a full s_load_dwordx16; padding records
-    // are never accepted (consider() bounds the index).
+    // every chunk (and the one-ahead prefetch) is a full scalar load; padding records are
+    // never accepted (consider() is only called for indices < count).
     float4 cur[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) cur[k] = geom[k];
@@ -257,7 +270,7 @@ __device__ __forceinline__ Hit scan_culled(const float4* __restrict__ geom, uint
     const float4* recs = kLds ? lds_recs : geom;
     Cone k;
     if (count < kCullMinSpheres || !wave_cone(o, d, live, k))
-        return scan_exhaustive(geom, count, o, d);
+        return scan_exhaustive<RT_SCAN_CHUNK>(geom, count, o, d);
     STAMP(2);
     const uint32_t lane = threadIdx.x & 63u;
     const float a = dot(d, d);
@@ -360,9 +373,14 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
         // [1 - 6*2^-24, 1 + 2^-23], |sa| >= 2^-30 or sa == +0, |ca| >= 2^-27 (checked
         // exhaustively, tests/test_gpu_parity.py::test_fastmath_selftest), inside the exact
         // domain of sqrt_core / div_core: the same bits as sqrtf and the two IEEE divides.
+#ifdef RT_DEFOCUS_IEEE
+        const float len = sqrtf(fmaf(sa, sa, ca * ca));
+        o = fmas(sa / len, cam.ddv, fmas(ca / len, cam.ddu, cam.center));
+#else
         const float len = sqrt_core(fmaf(sa, sa, ca * ca));
         const float y = rcp_refined(len);
         o = fmas(div_core(sa, len, y), cam.ddv, fmas(div_core(ca, len, y), cam.ddu, cam.center));
+#endif
     } else {
         o = cam.center;
     }
@@ -395,12 +413,12 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
         const Hit hit = Hit{-1, 0.0f};
 #else
         const Hit hit =
-            (kScan != kTraceCulled || listed)
-                ? scan_exhaustive(listed ? p.cand_rec + lbase : p.geom,
-                                  listed ? ncand : p.count, o, d)
+            listed ? scan_exhaustive<scan_chunk<kScan>()>(p.cand_rec + lbase, ncand, o, d)
+            : kScan != kTraceCulled ? scan_exhaustive<scan_chunk<kScan>()>(p.geom, p.count, o, d)
             : p.lds_records ? scan_culled<true>(p.geom, p.count, o, d, live)
                             : scan_culled<false>(p.geom, p.count, o, d, live);
 #endif
+        if (kScan != kTraceCulled) STAMP(2);                      // (culled: inside the scan)
         const float4* hs = listed ? p.cand_sph + 2 * lbase : p.sph;
         if (!live) continue;
         if (hit.idx < 0) {                                        // wgsl:288-290
@@ -501,7 +519,7 @@ template <int kScan>
 __device__ __forceinline__ v3 sample(const TraceParams& p, const Cam& cam, uint32_t tile,
                                      uint32_t ncand, const TileCoord& tc, uint32_t hxy,
                                      uint32_t n, uint32_t B, uint32_t f, bool live, bool uni) {
-    const uint32_t depth = f2u(p.max_depth);
+    const uint32_t depth = p.depth;
     const uint32_t seed = 1u + n + B;                             // wgsl:353
     v3 o, d;
     STAMP(0);
@@ -524,7 +542,7 @@ template <int kScan>
 __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& cam,
                                               uint32_t tile, uint32_t ncand,
                                               const TileCoord& tc, uint32_t hxy, float4 acc) {
-    const uint32_t spp = f2u(p.spp);                              // wgsl:343
+    const uint32_t spp = p.spp;                                   // wgsl:343
     v3 c = mk(0.0f, 0.0f, 0.0f);
     uint32_t n = 0u;
     bool known = p.reset_first != 0u;                             // wgsl:345-350
@@ -534,7 +552,7 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
         known = true;
     }
     for (uint32_t f = 0; f < p.frames; ++f) {
-        const uint32_t B = f2u(p.seeds[f] * 4294967296.0f);      // wgsl:311,353
+        const uint32_t B = p.seed_b[f];                           // wgsl:311,353
         if (f == 0 && p.reset_first) {                            // wgsl:345-350
             c = mk(0.0f, 0.0f, 0.0f);
             n = 0u;
@@ -587,6 +605,7 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 #endif
 template <int kScan>
 constexpr uint32_t wg_waves() { return kScan == kTraceCulled ? 4u : RT_WG_WAVES; }
+
 
 template <int kScan>
 __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt_trace_kernel(
@@ -745,17 +764,21 @@ __global__ __launch_bounds__(256) void rt_present_kernel(const float4* __restric
 
 // ---- Self-test of the exact fast paths (rt_selftest_fastmath) ------------------------
 // cnt[0]: defocus normalisation, all 2^32 values of hash(seed + 1): fast vs IEEE bits.
-// cnt[1]: div_core_signed vs a / b on random a, b in the documented domain (a also +-0,
-//         b also small integers: the accumulator's n + 1).
-// cnt[2]: sqrt_core vs sqrtf on random x in [2^-96, 2^126], every f32 in [0.25, 4), +0.
+// cnt[1]: div_core_signed on random a, b with magnitudes in [2^-40, 2^40) (a also +-0,
+//         b also the accumulator's n + 1), vs a / b.
+// cnt[2]: sqrt_core on random x in [2^-96, 2^128), every f32 in [0.25, 4), +0 and +inf,
+//         vs sqrtf.
 // cnt[3]: cases run.
 __device__ __forceinline__ uint32_t mix32(uint64_t i, uint32_t salt) {
     return hash((uint32_t)i ^ hash((uint32_t)(i >> 32) + salt));
 }
-__device__ __forceinline__ float rand_in_domain(uint32_t r, uint32_t e) {
+__device__ __forceinline__ float rand_in_box(uint32_t r, uint32_t e) {
     // sign from r's top bit, mantissa from r, exponent e in [-40, 39]
     const uint32_t bits = (r & 0x807FFFFFu) | ((uint32_t)(127 - 40 + (int)(e % 80u)) << 23);
     return __uint_as_float(bits);
+}
+__device__ __forceinline__ bool same_bits(float x, float y) {   // NaN == NaN
+    return __float_as_uint(x) == __float_as_uint(y) || (x != x && y != y);
 }
 __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cnt, uint64_t n_rand) {
     unsigned long long bad0 = 0, bad1 = 0, bad2 = 0, runs = 0;
@@ -774,21 +797,22 @@ __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cn
     }
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_rand; i += stride) {
         const uint32_t r0 = mix32(i, 1u), r1 = mix32(i, 2u), r2 = mix32(i, 3u);
-        float a = rand_in_domain(r0, r2 & 0xFFFFu);
-        float b = rand_in_domain(r1, r2 >> 16);
+        float a = rand_in_box(r0, r2 & 0xFFFFu);
+        float b = rand_in_box(r1, r2 >> 16);
         if ((r2 & 0x700u) == 0) a = (r0 & 1u) ? -0.0f : 0.0f;
         if ((r2 & 0x3800u) == 0) b = (float)(1u + (r1 & 0xFFFFFFu));   // n + 1 counts
-        const float yb = rcp_refined(b);
-        bad1 += __float_as_uint(div_core_signed(a, b, yb)) != __float_as_uint(a / b);
+        bad1 += !same_bits(div_core_signed(a, b, rcp_refined(b)), a / b);
         const float x = __uint_as_float((r0 & 0x7FFFFFu) |
-                                        ((uint32_t)(127 - 96 + (int)(r1 % 222u)) << 23));
-        bad2 += __float_as_uint(sqrt_core(x)) != __float_as_uint(sqrtf(x));
+                                        ((uint32_t)(127 - 96 + (int)(r1 % 224u)) << 23));
+        bad2 += !same_bits(sqrt_core(x), sqrtf(x));
         const float z = __uint_as_float(0x3E800000u + (uint32_t)(i & 0x1FFFFFFu));  // [0.25, 4)
-        bad2 += __float_as_uint(sqrt_core(z)) != __float_as_uint(sqrtf(z));
+        bad2 += !same_bits(sqrt_core(z), sqrtf(z));
         ++runs;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        bad2 += __float_as_uint(sqrt_core(0.0f)) != __float_as_uint(sqrtf(0.0f));
+    if (blockIdx.x == 0 && threadIdx.x < 3) {
+        const float sp[3] = {0.0f, __uint_as_float(0x7F800000u), 0x1p-96f};
+        bad2 += !same_bits(sqrt_core(sp[threadIdx.x]), sqrtf(sp[threadIdx.x]));
+    }
     atomicAdd(&cnt[0], bad0);
     atomicAdd(&cnt[1], bad1);
     atomicAdd(&cnt[2], bad2);
