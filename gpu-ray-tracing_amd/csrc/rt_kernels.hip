@@ -412,9 +412,11 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
 #if RT_KO & 1
         const Hit hit = Hit{-1, 0.0f};
 #else
+        // (one inlined walk for both pointers: two copies measured slower)
         const Hit hit =
-            listed ? scan_exhaustive<scan_chunk<kScan>()>(p.cand_rec + lbase, ncand, o, d)
-            : kScan != kTraceCulled ? scan_exhaustive<scan_chunk<kScan>()>(p.geom, p.count, o, d)
+            (kScan != kTraceCulled || listed)
+                ? scan_exhaustive<scan_chunk<kScan>()>(listed ? p.cand_rec + lbase : p.geom,
+                                                       listed ? ncand : p.count, o, d)
             : p.lds_records ? scan_culled<true>(p.geom, p.count, o, d, live)
                             : scan_culled<false>(p.geom, p.count, o, d, live);
 #endif
