@@ -23,7 +23,7 @@ using namespace rtd;
 
 // Knock-out builds for cost attribution only (tools; never the product): RT_KO bit 1 skips
 // the sphere scan, 2 the shading, 4 the random camera ray, 8 the accumulator load, 16 the
-// store.
+// store, 32 the accumulator load (keeping the hinted count).
 #ifndef RT_KO
 #define RT_KO 0
 #endif
@@ -641,6 +641,9 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
         (kScan != kTraceExhaustive && p.cand_k) ? p.cand_cnt[tile] : kCandNone;
 #if RT_KO & 8
     const float4 acc = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+#elif RT_KO & 32
+    // knock-out: no accumulator load; the count the hint expects (so no retrace)
+    const float4 acc = make_float4(0.0f, 0.0f, 0.0f, (float)p.hint_n[0]);
 #else
     // wgsl:339 (a frame-0 reset discards the value: no load)
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);

@@ -1,0 +1,49 @@
+"""Per-rank frame time of the stripe partition on ONE GPU (diagnostic, not the bench): times
+rank 0's share of a W x H progressive render for world sizes 1, 2, 4, 8, i.e. what each rank
+of `bench.py --gpus N` computes per step, to predict strong-scaling efficiency without an
+8-GPU node.  usage: python tools/rank_sim.py [K3|K2|K5] [steps]"""
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT / "gpu-ray-tracing_amd"), str(ROOT)]
+import torch  # noqa: E402
+
+import gpu_ray_tracing as rt  # noqa: E402
+from gpu_ray_tracing.distributed import StripeRenderer  # noqa: E402
+
+CONF = {"K2": (1920, 1080, rt.SCENE_THREE, 3, 1), "K3": (1920, 1080, rt.SCENE_N, 500, 1),
+        "K5": (3840, 2160, rt.SCENE_N, 500, 8)}
+
+
+def main(cfg="K3", steps=50):
+    w, h, kind, n, depth = CONF[cfg]
+    sc = rt.SphereCollection.generate(kind, n, 1)
+    seeds = rt.frame_seeds(0x5EED, steps + 5)
+    settings = rt.CameraSettings(max_depth=depth, samples_per_pixel=1000)
+    cam = rt.SceneCamera.from_settings(settings, w, h, float(seeds[0]))
+    pipe = rt.ComputeShaderPipeline(0)
+    pipe.set_spheres(sc)
+    base = None
+    for world in (1, 2, 4, 8):
+        r = StripeRenderer(pipe, w, h, 0, world)
+        r.frames(cam, sc, seeds[:5])                       # reset frame + warmup
+        cam_t = cam.with_fields(camera_has_moved=0.0)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r.frames(cam_t, sc, seeds[5:5 + steps])
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / steps
+        base = base or us
+        print(json.dumps({"cfg": cfg, "world": world, "rank0_rows": r.rows,
+                          "us_per_step": round(us, 2), "ideal_us": round(base / world, 2),
+                          "predicted_efficiency": round(base / world / us, 3)}), flush=True)
+    pipe.close()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "K3",
+         int(sys.argv[2]) if len(sys.argv) > 2 else 50)
