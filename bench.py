@@ -10,9 +10,17 @@ GPU, launched by torch.distributed.run) the image is split into 8-row bands deal
 round-robin, and after the K timed steps the finished tiles are gathered to rank 0 with
 ONE RCCL gather + the de-interleave kernel — both inside the timed region.
 
+The K steps are issued by one rt_update_frames call per rank: at max_depth <= 1 it runs up
+to 16 frames per launch, each wave carrying its pixels' accumulator in registers from frame
+to frame and storing every frame's image to the ping-pong buffers — both buffers end exactly
+as K chained `update` dispatches leave them (tests/test_gpu_parity.py); per_frame_dispatch
+times the same frames with one launch per frame (the reference's dispatch structure).
+
 value = W*H*K camera rays / max-over-ranks wall time (Mrays/s, whole job).
 roofline (trace kernel, average launch time from HIP events): for the default culled scan
-the algorithmic HBM bytes (32 B/pixel/step) against 8 TB/s; for --scan exhaustive the
+the algorithmic HBM bytes of the reference's progressive update (32 B/pixel/frame, SURVEY
+§8d) against 8 TB/s — the fused launches move 16 B/pixel/frame + 16 B/pixel/launch
+(moved_bytes_per_launch; PMC traffic beside it); for --scan exhaustive the
 algorithmic FP32 work (23 FLOP per ray-sphere test) against the 157.3 TFLOP/s
 FP32 vector peak.  The exhaustive kernel is also timed on the same frames
 (fp32_exhaustive_scan) so both rooflines appear in one line.
@@ -63,6 +71,8 @@ def parse():
                          "reference's exhaustive linear walk; images are bit-identical")
     ap.add_argument("--exhaustive-steps", type=int, default=20,
                     help="also time the exhaustive-scan kernel for its FP32 roofline")
+    ap.add_argument("--per-frame-steps", type=int, default=20,
+                    help="also time frames with one launch each (the reference's structure)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="CPU baseline budget in seconds (0 = skip)")
     return ap.parse_args()
@@ -121,12 +131,14 @@ def cpu_baseline(cam, spheres, w, h, seconds):
             "cpu_model": cpu_model()}
 
 
-def load_pmc(config):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC passes, if present."""
+def load_pmc(config, frames_per_launch=1):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC passes, if present and taken
+    at the same frames per launch."""
     p = ROOT / "profiles" / f"pmc_{config}.json"
     if p.exists():
         d = json.loads(p.read_text())
-        return d.get("hbm_bytes_per_launch")
+        if d.get("frames_per_launch", 1) == frames_per_launch:
+            return d.get("hbm_bytes_per_launch")
     return None
 
 
@@ -145,10 +157,11 @@ def main():
     w, h, kind, nsph, depth, desc = CONFIGS[args.config]
     spheres = rt.SphereCollection.generate(kind, nsph, 1)
     frames = args.warmup + args.steps
-    seeds = rt.frame_seeds(FRAME_SEED, frames + args.exhaustive_steps)
+    extra = max(args.exhaustive_steps, args.per_frame_steps)
+    seeds = rt.frame_seeds(FRAME_SEED, frames + extra)
     # spp cap above every frame this run traces (so no frame is a no-op)
     settings = rt.CameraSettings(max_depth=depth,
-                                 samples_per_pixel=max(500, frames + args.exhaustive_steps))
+                                 samples_per_pixel=max(500, frames + extra))
     cam0 = rt.SceneCamera.from_settings(settings, w, h, float(seeds[0]))
     cams = [cam0.with_fields(camera_has_moved=1.0 if f == 0 else 0.0) for f in range(2)]
 
@@ -187,8 +200,11 @@ def main():
 
     # every pixel of the gathered image must hold exactly warmup + steps samples
     sample_ok = image is not None and bool(torch.all(image[..., 3] == frames).item())
-    # HIP events around the timed dispatches: average per launch, inter-kernel gaps included
-    launch_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
+    # HIP events around the timed dispatches: per step and per launch, gaps included
+    fpl = r.frames_per_launch(cam_t)
+    launches = -(-args.steps // fpl)
+    step_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
+    launch_s = ev0.elapsed_time(ev1) / 1e3 / launches
     local_px = w * min(r.rows, h)
     # SURVEY §8d algorithmic units: the reference's exhaustive scan does N tests of 23 FLOP
     # per segment; at max_depth 1 every sample is exactly one segment.
@@ -211,7 +227,7 @@ def main():
                "achieved": round(flops / t_exh / 1e12, 3), "peak": PEAK_FP32_TFLOPS,
                "unit": "TFLOP/s", "frac": round(flops / t_exh / 1e12 / PEAK_FP32_TFLOPS, 4),
                "flop_per_launch": flops,
-               "speedup_of_culled": round(t_exh / launch_s, 2)}
+               "speedup_of_culled": round(t_exh / step_s, 2)}
 
     # Presentation kernel on the gathered image: 16 B read + 4 B written per
     # pixel, HBM-bound.
@@ -231,20 +247,40 @@ def main():
                    "unit": "GB/s", "frac": round(w * h * 20 / t_p / 1e9 / PEAK_HBM_GBS, 4),
                    "bytes_per_launch": w * h * 20}
 
+    # The reference's dispatch structure on the same frames: one launch per frame.
+    per_frame = None
+    if fpl > 1 and args.per_frame_steps > 0:
+        pipe.set_frames_per_launch(1)
+        q0, q1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        q0.record(stream)
+        r.frames(cam_t, spheres, seeds[frames:frames + args.per_frame_steps])
+        q1.record(stream)
+        torch.cuda.synchronize()
+        pipe.set_frames_per_launch(0)
+        t_pf = q0.elapsed_time(q1) / 1e3 / args.per_frame_steps
+        per_frame = {"frames_per_launch": 1, "us_per_step": round(t_pf * 1e6, 2),
+                     "Mrays_per_s": round(local_px / t_pf / 1e6, 1),
+                     "hbm_frac": round(hbm_bytes / t_pf / 1e9 / PEAK_HBM_GBS, 4)}
+
+    avg_frames = args.steps / launches
     if args.scan == "exhaustive" and flops:
-        roof = {"bound": "valu", "achieved": round(flops / launch_s / 1e12, 3),
+        roof = {"bound": "valu", "achieved": round(flops / step_s / 1e12, 3),
                 "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(flops / launch_s / 1e12 / PEAK_FP32_TFLOPS, 4),
-                "traffic": load_pmc(f"{args.config}_exhaustive"),
-                "kernel_avg_us": round(launch_s * 1e6, 2), "flop_per_launch": flops}
+                "frac": round(flops / step_s / 1e12 / PEAK_FP32_TFLOPS, 4),
+                "traffic": load_pmc(f"{args.config}_exhaustive", fpl),
+                "kernel_avg_us": round(launch_s * 1e6, 2), "frames_per_launch": fpl,
+                "flop_per_launch": round(flops * avg_frames)}
     else:
         # Culled scan: the redundant ray-sphere tests are gone (exactly), so
-        # the algorithm-independent unit left is the accumulator's 32 B/pixel of HBM.
-        roof = {"bound": "hbm", "achieved": round(hbm_bytes / launch_s / 1e9, 1),
+        # the algorithm-independent unit left is the progressive update's 32 B/pixel.
+        roof = {"bound": "hbm", "achieved": round(hbm_bytes / step_s / 1e9, 1),
                 "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(hbm_bytes / launch_s / 1e9 / PEAK_HBM_GBS, 4),
-                "traffic": load_pmc(f"{args.config}_culled"),
-                "kernel_avg_us": round(launch_s * 1e6, 2), "bytes_per_launch": hbm_bytes}
+                "frac": round(hbm_bytes / step_s / 1e9 / PEAK_HBM_GBS, 4),
+                "traffic": load_pmc(f"{args.config}_culled", fpl),
+                "kernel_avg_us": round(launch_s * 1e6, 2), "frames_per_launch": fpl,
+                "bytes_per_launch": round(hbm_bytes * avg_frames),
+                "moved_bytes_per_launch": round(local_px * 16 * (avg_frames + 1)),
+                "us_per_step": round(step_s * 1e6, 2)}
 
     if rank == 0:
         line = {
@@ -268,6 +304,7 @@ def main():
             "roofline": roof,
             "fp32_exhaustive_scan": exh,
             "present_rgba8": present,
+            "per_frame_dispatch": per_frame,
             "accumulated_spp_ok": sample_ok,
         }
         if world == 1 and args.cpu_seconds > 0:

@@ -27,6 +27,11 @@ constexpr uint32_t kHintEntries = 16;
 struct TraceParams {
     const float4* in;    // local image (compact stripes), row pitch = width
     float4* out;
+    // store_each (rt_update_frames): every frame f of the launch stores its image, to out
+    // for even f and to out2 (the input buffer) for odd f — the ping-pong of chained
+    // `update` dispatches (lib.rs:366-374), with the accumulator kept in registers.
+    float4* out2;
+    uint32_t store_each;
     const float4* geom;  // per sphere: (cx, cy, cz, r*r) — the scan's 16-B record
     const float4* sph;   // per sphere: the 32-B GpuSphere as two float4 (pos+r, color)
     uint32_t width, height, count;

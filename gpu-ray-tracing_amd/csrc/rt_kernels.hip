@@ -130,6 +130,11 @@ __device__ __forceinline__ int max_bits(const float (&dd)[K]) {
 #endif
 template <int kScan>
 constexpr int scan_chunk() { return kScan == kTraceList ? RT_LIST_CHUNK : RT_SCAN_CHUNK; }
+// Per-frame stores of fused launches (TraceParams::store_each) exist in the camera-ray-only
+// instance alone: the bounce instances would spill registers for them (rt_abi.cpp runs
+// their rt_update_frames one frame per launch).
+template <int kScan>
+constexpr bool kStoreEach = kScan == kTraceList;
 
 template <int K>
 __device__ __forceinline__ Hit scan_exhaustive(const float4* __restrict__ geom, uint32_t count,
@@ -586,7 +591,11 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
             pending = wrong;                                      // retrace these pixels
             ng = n;
         }
-        // The chained form stores f32(n) and reloads u32(.) each frame (wgsl:341,362).
+        // Chained updates: frame f's image (wgsl:362-363) lands in the other ping-pong
+        // buffer; the next frame would read it back (u32(f32(n)), wgsl:341) — here the
+        // registers already hold it.
+        if (kStoreEach<kScan> && p.store_each && tc.valid)
+            ((f & 1u) ? p.out2 : p.out)[tc.idx] = make_float4(c.x, c.y, c.z, (float)n);
         n = f2u((float)n);
     }
     return make_float4(c.x, c.y, c.z, (float)n);                  // wgsl:362
@@ -665,7 +674,7 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
 #if RT_KO & 16
     if (res.x == 12345.678f) p.out[tc.idx] = res;
 #else
-    if (tc.valid) p.out[tc.idx] = res;                            // wgsl:363
+    if (tc.valid && !(kStoreEach<kScan> && p.store_each)) p.out[tc.idx] = res;  // wgsl:363
 #endif
     STAMP(5);
 }

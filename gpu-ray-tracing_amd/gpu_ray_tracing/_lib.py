@@ -113,6 +113,8 @@ _SIGS = {
     "rt_present_rgba8": (ctypes.c_int, [P, P, P, U32, U32, ctypes.c_int, P]),
     "rt_srgb_thresholds": (None, [P]),
     "rt_selftest_fastmath": (ctypes.c_int, [P, ctypes.c_uint64, P]),
+    "rt_set_frames_per_launch": (ctypes.c_int, [P, U32]),
+    "rt_get_frames_per_launch": (ctypes.c_int, [P, P, ctypes.POINTER(U32)]),
 }
 
 _lib = None

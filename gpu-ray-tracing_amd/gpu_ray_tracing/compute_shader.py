@@ -63,6 +63,18 @@ class ComputeShaderPipeline:
             _lib.call("rt_destroy", self._ctx)
             self._ctx = ctypes.c_void_p()
 
+    def set_frames_per_launch(self, n: int) -> None:
+        """rt_set_frames_per_launch: update_frames' frames per launch (0 = automatic,
+        1 = one `update` dispatch per frame, n = up to n)."""
+        _lib.call("rt_set_frames_per_launch", self._ctx, int(n))
+
+    def frames_per_launch(self, camera) -> int:
+        """rt_get_frames_per_launch: frames update_frames fuses per launch for `camera`."""
+        out = _lib.U32(0)
+        cam = camera.to_c()
+        _lib.call("rt_get_frames_per_launch", self._ctx, ctypes.byref(cam), ctypes.byref(out))
+        return int(out.value)
+
     def selftest_fastmath(self, n_random: int = 1 << 26) -> list[int]:
         """rt_selftest_fastmath: [defocus, division, sqrt mismatches, cases run]."""
         out = (ctypes.c_uint64 * 4)()

@@ -67,6 +67,10 @@ class StripeRenderer:
         elif len(seeds) % 2:
             self.cur = 1 - self.cur
 
+    def frames_per_launch(self, camera) -> int:
+        """Frames rt_update_frames fuses per launch for this pipeline and camera."""
+        return self.pipe.frames_per_launch(camera)
+
     @property
     def local(self) -> torch.Tensor:
         return self.buf[self.cur]

@@ -166,13 +166,24 @@ RT_API rt_status rt_render(rt_ctx* ctx, const float* in_rgba, float* out_rgba, u
                     const float* random_seeds, void* stream);
 
 /* The reference's per-frame loop (ComputeShaderNode ping-pong, lib.rs:366-374, 408-417)
- * driven from C: `frames` separate progressive `update` dispatches alternating between
- * image_a and image_b (frame f reads the image frame f-1 wrote; frame 0 reads image_a).
- * Frame f uses random_seeds[f] and camera_has_moved = (f == 0 ? camera->camera_has_moved
- * : 0).  Restricted to the stripe bands of rank/nranks (nranks = 1: whole image; images
- * are then compact local buffers as for rt_render_stripes).  *out_newest receives 0 if
- * image_a holds the result, 1 for image_b.  One call = `frames` kernel launches with no
- * per-frame host round trip. */
+ * driven from C: `frames` progressive `update`s alternating between image_a and image_b
+ * (frame f reads the image frame f-1 wrote; frame 0 reads image_a; frame f writes its
+ * image to image_b for even f, image_a for odd f).  Frame f uses random_seeds[f] and
+ * camera_has_moved = (f == 0 ? camera->camera_has_moved : 0).  Restricted to the stripe
+ * bands of rank/nranks (nranks = 1: whole image; images are then compact local buffers as
+ * for rt_render_stripes).  *out_newest receives 0 if image_a holds the result, 1 for
+ * image_b.  Afterwards BOTH images hold exactly what `frames` chained rt_update calls leave
+ * (the newest frame and the one before).  Frames run in launches of
+ * rt_set_frames_per_launch frames (default: 16 at max_depth <= 1, else 1); within a
+ * launch each wave carries its pixels' accumulator in registers from frame to frame and
+ * stores every frame's image.  No per-frame host round trip. */
+/* Frames rt_update_frames runs per launch at max_depth <= 1: 0 = automatic (up to 16),
+ * 1 = one `update` dispatch per frame, exactly the reference's dispatch structure, n = up
+ * to n (at most 128).  Launches with bounce rays always run one frame each. */
+RT_API rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launch);
+/* The frames per launch rt_update_frames would use for `camera` (its max_depth) now. */
+RT_API rt_status rt_get_frames_per_launch(const rt_ctx* ctx, const rt_scene_camera* camera,
+                                          uint32_t* out_frames);
 RT_API rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t width,
                                   uint32_t height, uint32_t rank, uint32_t nranks,
                                   const rt_scene_camera* camera, const rt_sphere* spheres,

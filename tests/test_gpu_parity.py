@@ -395,33 +395,46 @@ def test_candidate_list_overflow_falls_back(rt, depth):
 
 
 @pytest.mark.parametrize("nranks", [1, 3])
-def test_update_frames_equals_chained_updates(rt, pipe, nranks):
-    """rt_update_frames (the per-frame dispatch loop in C) == chained rt_update calls, for
-    the whole image and for stripe ranks (compact local buffers)."""
+@pytest.mark.parametrize("frames,depth,spp,per", [(5, 2, 500, 0), (20, 1, 500, 0), (3, 8, 500, 0),
+                                                  (7, 1, 4, 0), (4, 1, 500, 1), (6, 3, 500, 4),
+                                                  (5, 8, 500, 4), (9, 2, 3, 3)])
+def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, spp, per):
+    """rt_update_frames (frames fused per launch, every frame's image stored to the
+    ping-pong buffers; or one dispatch per frame) leaves BOTH buffers exactly as chained
+    rt_update calls do: the newest frame and the one before, for the whole image and for
+    stripe ranks (compact local buffers), across launch boundaries and the spp cap."""
     w, h = 56, 40
     sc = rt.synthetic_scene(120)
-    seeds = rt.frame_seeds(21, 5)
-    cam = camera(rt, w, h, depth=2)
+    seeds = rt.frame_seeds(21, frames)
+    cam = camera(rt, w, h, depth=depth, spp=spp)
     full_a, full_b = pipe.new_image(w, h), pipe.new_image(w, h)
     cur, nxt = full_a, full_b
-    for f in range(5):
+    for f in range(frames):
         pipe.update(cur, nxt, w, h, cam.with_fields(random_seed=float(seeds[f]),
                                                    camera_has_moved=1.0 if f == 0 else 0.0), sc)
         cur, nxt = nxt, cur
-    want = host(cur)
+    want_new, want_prev = host(cur), host(nxt)
     rows0 = rt.stripe_local_rows(h, 0, nranks)
-    got = np.zeros((h, w, 4), np.float32)
-    for r in range(nranks):
-        a, b = pipe.new_image(w, rows0), pipe.new_image(w, rows0)
-        newest = pipe.update_frames(a, b, w, h, cam, sc, seeds, r, nranks)
-        img = host(a if newest == 0 else b)
-        rows = rt.stripe_local_rows(h, r, nranks)
-        for lr in range(rows):
-            band = r + (lr // 8) * nranks
-            y = band * 8 + lr % 8
-            if y < h:
-                got[y] = img[lr]
-    assert_same(got, want)
+    got_new = np.zeros((h, w, 4), np.float32)
+    got_prev = np.zeros((h, w, 4), np.float32)
+    pipe.set_frames_per_launch(per)
+    try:
+        for r in range(nranks):
+            a, b = pipe.new_image(w, rows0), pipe.new_image(w, rows0)
+            newest = pipe.update_frames(a, b, w, h, cam, sc, seeds, r, nranks)
+            img_new, img_prev = (host(a), host(b)) if newest == 0 else (host(b), host(a))
+            rows = rt.stripe_local_rows(h, r, nranks)
+            for lr in range(rows):
+                band = r + (lr // 8) * nranks
+                y = band * 8 + lr % 8
+                if y < h:
+                    got_new[y], got_prev[y] = img_new[lr], img_prev[lr]
+    finally:
+        pipe.set_frames_per_launch(0)
+    assert (newest == 0) == (frames % 2 == 0)
+    assert_same(got_new, want_new)
+    if frames >= 2:
+        assert_same(got_prev, want_prev)
 
 
 def test_accumulator_written_outside_the_library(rt, oracle, pipe):

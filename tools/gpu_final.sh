@@ -21,9 +21,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 head -4 $O/prof/bench_kernel_stats.csv
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc -o culled_$c \
-    -- python3 bench.py --cpu-seconds 0 --exhaustive-steps 0 --steps 20 > $O/pmc_$c.log 2>&1 \
+    -- python3 bench.py --cpu-seconds 0 --exhaustive-steps 0 --per-frame-steps 0 --steps 32 > $O/pmc_$c.log 2>&1 \
     || { echo "pmc $c failed"; tail -5 $O/pmc_$c.log; exit 1; }
 done
-python3 tools/pmc_summary.py $O/pmc_K3_culled.json trace_kernel $O/pmc/culled_FETCH_SIZE_counter_collection.csv $O/pmc/culled_WRITE_SIZE_counter_collection.csv | tail -8
+FRAMES_PER_LAUNCH=16 python3 tools/pmc_summary.py $O/pmc_K3_culled.json trace_kernel $O/pmc/culled_FETCH_SIZE_counter_collection.csv $O/pmc/culled_WRITE_SIZE_counter_collection.csv | tail -8
 timeout -k 10 300 python tools/rank_sim.py K3 50 > $O/rank_k3.jsonl 2>&1 || exit 1
 cat $O/rank_k3.jsonl

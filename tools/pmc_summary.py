@@ -4,8 +4,9 @@ HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
 KiB, collected in separate passes; on gfx950 FETCH_SIZE reports half the bytes of a wide
 (16 B/lane) coalesced streaming read, so it is doubled before adding WRITE_SIZE.
 usage: python tools/pmc_summary.py OUT.json KERNEL_SUBSTR file1.csv [file2.csv ...]
+(env FRAMES_PER_LAUNCH=F records the frames each profiled launch ran)
 """
-import collections, csv, json, statistics, sys
+import collections, csv, json, os, statistics, sys
 
 out, ksub, files = sys.argv[1], sys.argv[2], sys.argv[3:]
 vals = collections.defaultdict(list)
@@ -18,7 +19,8 @@ for f in files:
     for (d, c), v in per.items():
         vals[c].append(v)
 summ = {c: statistics.median(v) for c, v in vals.items()}
-res = {"kernel": ksub, "dispatches": {c: len(v) for c, v in vals.items()}, "median_per_launch": summ}
+res = {"kernel": ksub, "dispatches": {c: len(v) for c, v in vals.items()}, "median_per_launch": summ,
+       "frames_per_launch": int(os.environ.get("FRAMES_PER_LAUNCH", "1"))}
 if "FETCH_SIZE" in summ and "WRITE_SIZE" in summ:
     res["hbm_read_bytes_per_launch"] = summ["FETCH_SIZE"] * 2 * 1024
     res["hbm_write_bytes_per_launch"] = summ["WRITE_SIZE"] * 1024
