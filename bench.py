@@ -11,7 +11,7 @@ round-robin, and after the K timed steps the finished tiles are gathered to rank
 ONE RCCL gather + the de-interleave kernel — both inside the timed region.
 
 The K steps are issued by one rt_update_frames call per rank: at max_depth <= 1 it runs up
-to 16 frames per launch, each wave carrying its pixels' accumulator in registers from frame
+to 64 frames per launch, each wave carrying its pixels' accumulator in registers from frame
 to frame and storing every frame's image to the ping-pong buffers — both buffers end exactly
 as K chained `update` dispatches leave them (tests/test_gpu_parity.py); per_frame_dispatch
 times the same frames with one launch per frame (the reference's dispatch structure).

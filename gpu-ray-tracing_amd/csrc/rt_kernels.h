@@ -20,8 +20,11 @@ constexpr uint32_t kCandNone = 0xFFFFFFFFu;
 // Sample-count hint (see TraceParams::hint_n): per-(frame, bounce) random numbers of the
 // scatter step for at most kHintEntries (frame, bounce) pairs of the first kHintFrames
 // frames of a launch.
-constexpr uint32_t kHintFrames = 16;
-constexpr uint32_t kHintEntries = 16;
+#ifndef RT_HINT_FRAMES
+#define RT_HINT_FRAMES 64   // 16 / 32 / 64: 24.4 / 24.1 / 24.0 us per K3 frame
+#endif
+constexpr uint32_t kHintFrames = RT_HINT_FRAMES;
+constexpr uint32_t kHintEntries = RT_HINT_FRAMES;
 
 // Everything the `update` kernel needs, passed by value (kernarg -> SGPRs).
 struct TraceParams {

@@ -174,10 +174,10 @@ RT_API rt_status rt_render(rt_ctx* ctx, const float* in_rgba, float* out_rgba, u
  * for rt_render_stripes).  *out_newest receives 0 if image_a holds the result, 1 for
  * image_b.  Afterwards BOTH images hold exactly what `frames` chained rt_update calls leave
  * (the newest frame and the one before).  Frames run in launches of
- * rt_set_frames_per_launch frames (default: 16 at max_depth <= 1, else 1); within a
+ * rt_set_frames_per_launch frames (default: 64 at max_depth <= 1, else 1); within a
  * launch each wave carries its pixels' accumulator in registers from frame to frame and
  * stores every frame's image.  No per-frame host round trip. */
-/* Frames rt_update_frames runs per launch at max_depth <= 1: 0 = automatic (up to 16),
+/* Frames rt_update_frames runs per launch at max_depth <= 1: 0 = automatic (up to 64),
  * 1 = one `update` dispatch per frame, exactly the reference's dispatch structure, n = up
  * to n (at most 128).  Launches with bounce rays always run one frame each. */
 RT_API rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launch);

@@ -16,14 +16,18 @@ timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo benc
 cat $O/bench.json
 timeout -k 10 300 python bench.py --config K2 --cpu-seconds 0 > $O/bench_k2.json 2>> $O/bench.err || exit 1
 timeout -k 10 300 python bench.py --config K5 --steps 5 --warmup 2 --cpu-seconds 0 > $O/bench_k5.json 2>> $O/bench.err || exit 1
+# profiled command: whole 64-frame launches only (warmup 64 + 128 timed), so rocprofv3's
+# per-launch average and the line's kernel_avg_us describe the same launches
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench \
-  -- python3 bench.py --cpu-seconds 0 > $O/prof.log 2>&1 || { echo prof failed; tail $O/prof.log; exit 1; }
+  -- python3 bench.py --cpu-seconds 0 --exhaustive-steps 0 --per-frame-steps 0 --warmup 64 --steps 128 \
+  > $O/prof.log 2>&1 || { echo prof failed; tail $O/prof.log; exit 1; }
+grep '^{' $O/prof.log > $O/bench_profiled.json; cat $O/bench_profiled.json
 head -4 $O/prof/bench_kernel_stats.csv
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc -o culled_$c \
-    -- python3 bench.py --cpu-seconds 0 --exhaustive-steps 0 --per-frame-steps 0 --steps 32 > $O/pmc_$c.log 2>&1 \
+    -- python3 bench.py --cpu-seconds 0 --exhaustive-steps 0 --per-frame-steps 0 --steps 128 > $O/pmc_$c.log 2>&1 \
     || { echo "pmc $c failed"; tail -5 $O/pmc_$c.log; exit 1; }
 done
-FRAMES_PER_LAUNCH=16 python3 tools/pmc_summary.py $O/pmc_K3_culled.json trace_kernel $O/pmc/culled_FETCH_SIZE_counter_collection.csv $O/pmc/culled_WRITE_SIZE_counter_collection.csv | tail -8
+FRAMES_PER_LAUNCH=64 python3 tools/pmc_summary.py $O/pmc_K3_culled.json trace_kernel $O/pmc/culled_FETCH_SIZE_counter_collection.csv $O/pmc/culled_WRITE_SIZE_counter_collection.csv | tail -8
 timeout -k 10 300 python tools/rank_sim.py K3 50 > $O/rank_k3.jsonl 2>&1 || exit 1
 cat $O/rank_k3.jsonl
