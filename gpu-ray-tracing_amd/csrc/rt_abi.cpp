@@ -49,6 +49,7 @@ struct rt_ctx {
     };
     std::vector<CountRecord> counts;
     uint32_t frames_per_launch = 0;  // rt_update_frames fusion cap (0 = automatic)
+    int frame_pairs = RT_FRAME_PAIRS_AUTO;
 };
 
 namespace {
@@ -488,6 +489,14 @@ rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launch) {
     return RT_OK;
 }
 
+rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (mode != RT_FRAME_PAIRS_AUTO && mode != RT_FRAME_PAIRS_OFF && mode != RT_FRAME_PAIRS_ON)
+        return fail(RT_ERR_INVALID_ARGUMENT, "unknown frame-pair mode");
+    ctx->frame_pairs = mode;
+    return RT_OK;
+}
+
 rt_status rt_get_frames_per_launch(const rt_ctx* ctx, const rt_scene_camera* cam,
                                    uint32_t* out) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
@@ -585,7 +594,13 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         } else {
             p.hint_frames = 0;
         }
-        hipError_t e = rtk::launch_trace(p, trace_kernel_for(ctx, p), stream);
+        // Frame groups (several waves per tile, alternate frames) whenever every frame of
+        // the launch is hinted: faster at every rank count measured.
+        int kernel = trace_kernel_for(ctx, p);
+        const bool pairable = kernel == rtk::kTraceList && p.store_each && known &&
+                              p.hint_frames == nf;
+        if (pairable && ctx->frame_pairs != RT_FRAME_PAIRS_OFF) kernel = rtk::kTraceListPair;
+        hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         // frame f of the launch wrote img[(cur + 1 + f) % 2]
         const int newest = (nf & 1u) ? 1 - cur : cur;

@@ -75,6 +75,10 @@ struct TraceParams {
 constexpr int kTraceExhaustive = 0;
 constexpr int kTraceCulled = 1;
 constexpr int kTraceList = 2;
+// Camera-ray-only, two waves per tile tracing alternate frames (rt_update_frames on small
+// per-rank images; see rt_kernels.hip, trace_pair).
+constexpr int kTraceListPair = 3;
+constexpr bool is_list_kernel(int k) { return k == kTraceList || k == kTraceListPair; }
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream);
 hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream);
 // Builds the per-tile candidate lists for p's camera/scene/stripes (p.cand_k slots each).

@@ -115,6 +115,7 @@ _SIGS = {
     "rt_selftest_fastmath": (ctypes.c_int, [P, ctypes.c_uint64, P]),
     "rt_set_frames_per_launch": (ctypes.c_int, [P, U32]),
     "rt_get_frames_per_launch": (ctypes.c_int, [P, P, ctypes.POINTER(U32)]),
+    "rt_set_frame_pairs": (ctypes.c_int, [P, ctypes.c_int]),
 }
 
 _lib = None

@@ -68,6 +68,10 @@ class ComputeShaderPipeline:
         1 = one `update` dispatch per frame, n = up to n)."""
         _lib.call("rt_set_frames_per_launch", self._ctx, int(n))
 
+    def set_frame_pairs(self, mode: str) -> None:
+        """rt_set_frame_pairs: 'auto' | 'off' | 'on' (two waves per tile, alternate frames)."""
+        _lib.call("rt_set_frame_pairs", self._ctx, {"auto": 0, "off": 1, "on": 2}[mode])
+
     def frames_per_launch(self, camera) -> int:
         """rt_get_frames_per_launch: frames update_frames fuses per launch for `camera`."""
         out = _lib.U32(0)

@@ -181,6 +181,15 @@ RT_API rt_status rt_render(rt_ctx* ctx, const float* in_rgba, float* out_rgba, u
  * 1 = one `update` dispatch per frame, exactly the reference's dispatch structure, n = up
  * to n (at most 128).  Launches with bounce rays always run one frame each. */
 RT_API rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launch);
+/* rt_update_frames at max_depth <= 1 traces with several waves per 8x8 tile, each taking
+ * a different frame of each group of frames (the others hand their colours to wave 0,
+ * which accumulates and stores every frame in order: the same bits).  AUTO (default) and
+ * ON do so whenever every pixel holds the sample count the context expects (otherwise the
+ * launch falls back to one wave per tile); OFF always uses one wave per tile. */
+#define RT_FRAME_PAIRS_AUTO 0
+#define RT_FRAME_PAIRS_OFF 1
+#define RT_FRAME_PAIRS_ON 2
+RT_API rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode);
 /* The frames per launch rt_update_frames would use for `camera` (its max_depth) now. */
 RT_API rt_status rt_get_frames_per_launch(const rt_ctx* ctx, const rt_scene_camera* camera,
                                           uint32_t* out_frames);

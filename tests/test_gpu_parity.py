@@ -398,11 +398,13 @@ def test_candidate_list_overflow_falls_back(rt, depth):
 @pytest.mark.parametrize("frames,depth,spp,per", [(5, 2, 500, 0), (20, 1, 500, 0), (3, 8, 500, 0),
                                                   (7, 1, 4, 0), (4, 1, 500, 1), (6, 3, 500, 4),
                                                   (5, 8, 500, 4), (9, 2, 3, 3)])
-def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, spp, per):
+@pytest.mark.parametrize("pairs", ["off", "on"])
+def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, spp, per, pairs):
     """rt_update_frames (frames fused per launch, every frame's image stored to the
     ping-pong buffers; or one dispatch per frame) leaves BOTH buffers exactly as chained
     rt_update calls do: the newest frame and the one before, for the whole image and for
-    stripe ranks (compact local buffers), across launch boundaries and the spp cap."""
+    stripe ranks (compact local buffers), across launch boundaries and the spp cap, with
+    and without frame pairs (two waves per tile on alternate frames)."""
     w, h = 56, 40
     sc = rt.synthetic_scene(120)
     seeds = rt.frame_seeds(21, frames)
@@ -418,6 +420,7 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, s
     got_new = np.zeros((h, w, 4), np.float32)
     got_prev = np.zeros((h, w, 4), np.float32)
     pipe.set_frames_per_launch(per)
+    pipe.set_frame_pairs(pairs)
     try:
         for r in range(nranks):
             a, b = pipe.new_image(w, rows0), pipe.new_image(w, rows0)
@@ -431,6 +434,7 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, s
                     got_new[y], got_prev[y] = img_new[lr], img_prev[lr]
     finally:
         pipe.set_frames_per_launch(0)
+        pipe.set_frame_pairs("auto")
     assert (newest == 0) == (frames % 2 == 0)
     assert_same(got_new, want_new)
     if frames >= 2:
@@ -539,3 +543,32 @@ def test_hinted_chain_matches_oracle(rt, oracle, pipe, depth, spp):
         ref, _ = oracle.update(ref, cam.blob, sc.spheres)
         cur, nxt = nxt, cur
         assert_same(host(cur), ref)
+
+
+@pytest.mark.parametrize("pairs", ["off", "on"])
+def test_update_frames_with_foreign_counts(rt, oracle, pipe, pairs):
+    """rt_update_frames on an image whose counts the library did not write (mixed per-pixel
+    counts behind its back, after init_image): the hinted / frame-pair launch falls back to
+    per-pixel counts and still equals the oracle's chain, both buffers."""
+    w, h = 40, 24
+    sc = rt.synthetic_scene(200)
+    rng = np.random.default_rng(3)
+    a, b = pipe.new_image(w, h), pipe.new_image(w, h)
+    pipe.init_image(a, w, h)                      # the library now expects count 0
+    counts = rng.integers(0, 3, (h, w, 1)).astype(np.float32)
+    state = np.concatenate([rng.random((h, w, 3), np.float32), counts], axis=2)
+    a.copy_(to_dev(state))
+    seeds = rt.frame_seeds(9, 5)
+    cam = camera(rt, w, h, depth=1, spp=500, moved=False)
+    pipe.set_frame_pairs(pairs)
+    try:
+        newest = pipe.update_frames(a, b, w, h, cam, sc, seeds, 0, 1)
+    finally:
+        pipe.set_frame_pairs("auto")
+    ref, prev = state, None
+    for s_ in seeds:
+        prev = ref
+        ref, _ = oracle.update(ref, cam.with_fields(random_seed=float(s_)).blob, sc.spheres)
+    assert newest == 1
+    assert_same(host(b), ref)
+    assert_same(host(a), prev)

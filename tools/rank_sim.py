@@ -1,7 +1,7 @@
 """Per-rank frame time of the stripe partition on ONE GPU (diagnostic, not the bench): times
 rank 0's share of a W x H progressive render for world sizes 1, 2, 4, 8, i.e. what each rank
 of `bench.py --gpus N` computes per step, to predict strong-scaling efficiency without an
-8-GPU node.  usage: python tools/rank_sim.py [K3|K2|K5] [steps]"""
+8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] python tools/rank_sim.py [K3|K2|K5] [steps]"""
 import json
 import sys
 from pathlib import Path
@@ -25,6 +25,8 @@ def main(cfg="K3", steps=50):
     cam = rt.SceneCamera.from_settings(settings, w, h, float(seeds[0]))
     pipe = rt.ComputeShaderPipeline(0)
     pipe.set_spheres(sc)
+    import os
+    pipe.set_frame_pairs(os.environ.get("RT_FRAME_PAIRS", "auto"))
     base = None
     for world in (1, 2, 4, 8):
         r = StripeRenderer(pipe, w, h, 0, world)
