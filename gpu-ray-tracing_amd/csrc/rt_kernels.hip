@@ -607,10 +607,10 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 // n + f, verified up front), waves 1.. hand their colours to wave 0 through LDS, and wave 0
 // accumulates the group's frames in order and stores every frame's image (wgsl:352-363) —
 // bit-identical to one wave doing every frame.  More waves, each with a shorter sequential
-// chain: 22.1 vs 24.0 µs per K3 frame on one GPU, 3.6 vs 4.3 µs for an 8-rank share.
+// chain: 22.2 vs 24.0 µs per K3 frame on one GPU, 3.3 vs 4.3 µs for an 8-rank share.
 // Returns false (nothing done) when some pixel's loaded count differs from the hint.
 #ifndef RT_FRAME_GROUP
-#define RT_FRAME_GROUP 2
+#define RT_FRAME_GROUP 4   // 2 / 4 / 8: K3 22.2 / 22.2 / 24.6 us per frame, 8-rank share 3.5 / 3.3 / 3.4
 #endif
 constexpr uint32_t kFrameGroup = RT_FRAME_GROUP;
 template <int kScan>
