@@ -142,6 +142,10 @@ def test_argument_errors_without_device(rt):
     assert L.rt_driver_state(None) == -1
     assert L.rt_stripe_local_rows(100, 3, 2) == 0
     assert L.rt_present_rgba8(None, None, None, 8, 8, 0, None) == 6
+    assert L.rt_set_frames_per_launch(None, 4) == 6
+    assert L.rt_set_frame_pairs(None, 0) == 6
+    assert L.rt_get_frames_per_launch(None, None, None) == 6
+    assert L.rt_selftest_fastmath(None, 0, None) == 6
 
 
 def test_srgb_thresholds_match_restatement(rt):
