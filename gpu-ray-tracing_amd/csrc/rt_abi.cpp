@@ -30,6 +30,10 @@ struct rt_ctx {
     bool valid = false;
     std::vector<rt_sphere> cached;  // bytes currently on the device
     uint64_t scene_gen = 0;         // bumped on every sphere upload
+    // max over spheres of |C| + |R| (inf if any value is not finite) and whether every
+    // |R| lies in [2^-20, 2^20]: the scene half of camera_rays_bounded
+    double scene_bound = 0.0;
+    bool radii_ok = true;
     // Per-tile candidate lists of camera rays (culled scan), valid for cand_key.
     uint32_t* cand_cnt = nullptr;
     float4* cand_rec = nullptr;
@@ -90,12 +94,60 @@ uint32_t host_f2u(float f) {
     return (uint32_t)f;
 }
 
+double norm3(const float* v) {
+    return std::sqrt((double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2]);
+}
+
+// Whether every camera ray of p's camera, image and stripes, against the context's scene,
+// stays inside the domain where the camera-ray-only instances use the exact fast division
+// and sqrt cores (rt_kernels.hip consider_fast / fast_core): a = |d|^2 in [2^-11, 2^20],
+// |O| + max(|C| + |R|) <= 2^40 (so |h|, sqrt(D) <= 2^53 and the hit-point numerators of
+// the normal <= 2^43), and every |R| in [2^-20, 2^20].  d = pc - O (get_ray,
+// wgsl:305-325) with pc = vul + sx pdu + sy pdv, sx in [0, W + 8], sy in [0, H + 8] (lanes
+// past a ragged edge included), and O = center, or center + (cos, sin) (ddu, ddv) with a
+// unit (cos, sin) when defocus_angle > 0.  |d| is bounded above by the sum of the parts and
+// below by the distance along the normal of the pixel-delta plane, each widened by
+// 1e-5 x the magnitudes entering the f32 evaluation (its rounding is < 1e-6 of them).
+// Cameras or scenes outside the domain (degenerate, huge, non-finite, zero radii) run the
+// IEEE operations in the culled instance instead.  Evaluated in double; NaN fails.
+bool camera_rays_bounded(const rt_ctx* ctx, const rtk::TraceParams& p) {
+    if (!ctx->radii_ok) return false;
+    const bool defocus = p.defocus_angle > 0.0f;
+    const double W = (double)p.width + 8.0, H = (double)p.height + 8.0;
+    double e[3], nrm[3];
+    for (int i = 0; i < 3; ++i) e[i] = (double)p.vul[i] - p.center[i];
+    nrm[0] = (double)p.pdu[1] * p.pdv[2] - (double)p.pdu[2] * p.pdv[1];
+    nrm[1] = (double)p.pdu[2] * p.pdv[0] - (double)p.pdu[0] * p.pdv[2];
+    nrm[2] = (double)p.pdu[0] * p.pdv[1] - (double)p.pdu[1] * p.pdv[0];
+    const double nn = std::sqrt(nrm[0] * nrm[0] + nrm[1] * nrm[1] + nrm[2] * nrm[2]);
+    if (!(nn > 0.0) || !std::isfinite(nn)) return false;
+    auto along = [&](const double* v) {
+        return std::fabs(v[0] * nrm[0] + v[1] * nrm[1] + v[2] * nrm[2]) / nn;
+    };
+    double du[3], dv[3];
+    for (int i = 0; i < 3; ++i) {
+        du[i] = defocus ? p.ddu[i] : 0.0;
+        dv[i] = defocus ? p.ddv[i] : 0.0;
+    }
+    const double lens = std::sqrt(du[0] * du[0] + du[1] * du[1] + du[2] * du[2]) +
+                        std::sqrt(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]);
+    const double span = W * norm3(p.pdu) + H * norm3(p.pdv);
+    const double mag = norm3(p.vul) + norm3(p.center) + span + lens;
+    const double dmax = std::sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]) + span + lens +
+                        1e-5 * mag;
+    const double dmin = along(e) - along(du) - along(dv) - 1e-5 * mag;
+    if (!(dmin > 0.0 && dmin * dmin >= 0x1p-11 && dmax * dmax <= 0x1p20)) return false;
+    const double origin = norm3(p.center) + lens * (1.0 + 1e-5);
+    return origin + ctx->scene_bound <= 0x1p40;
+}
+
 // Kernel instance for a launch (rtk::kTrace*): without bounce rays (max_depth <= 1) the
-// culled mode needs only the candidate lists.
+// culled mode needs only the candidate lists; the camera-ray-only instance also requires
+// camera_rays_bounded (its fast cores).
 int trace_kernel_for(const rt_ctx* ctx, const rtk::TraceParams& p) {
     if (ctx->scan_mode == RT_SCAN_EXHAUSTIVE) return rtk::kTraceExhaustive;
 #ifndef RT_FORCE_CULLED_KERNEL
-    if (p.depth <= 1u) return rtk::kTraceList;
+    if (p.depth <= 1u && camera_rays_bounded(ctx, p)) return rtk::kTraceList;
 #endif
     return rtk::kTraceCulled;
 }
@@ -173,6 +225,16 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
         e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     }
+    double bound = 0.0;
+    bool radii_ok = true;
+    for (uint32_t i = 0; i < count; ++i) {
+        const double r = std::fabs((double)spheres[i].radius);
+        const double b = norm3(spheres[i].position) + r;
+        bound = std::isfinite(b) ? std::max(bound, b) : INFINITY;
+        radii_ok = radii_ok && r >= 0x1p-20 && r <= 0x1p20;
+    }
+    ctx->scene_bound = bound;
+    ctx->radii_ok = radii_ok;
     ctx->cached.assign(spheres, spheres + count);
     ctx->count = count;
     ctx->valid = true;
@@ -646,21 +708,21 @@ rt_status rt_deinterleave_stripes(rt_ctx* ctx, const float* gathered, float* out
     return e == hipSuccess ? RT_OK : hip_fail(e, "rt_deinterleave_kernel launch");
 }
 
-rt_status rt_selftest_fastmath(rt_ctx* ctx, uint64_t n_random, uint64_t out[4]) {
+rt_status rt_selftest_fastmath(rt_ctx* ctx, uint64_t n_random, uint64_t out[5]) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     if (!out) return fail(RT_ERR_INVALID_ARGUMENT, "out is NULL");
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
     unsigned long long* d = nullptr;
-    hipError_t e = hipMalloc(&d, 4 * sizeof(unsigned long long));
+    hipError_t e = hipMalloc(&d, 5 * sizeof(unsigned long long));
     if (e != hipSuccess) return hip_fail(e, "hipMalloc(selftest)");
-    unsigned long long h[4] = {0, 0, 0, 0};
+    unsigned long long h[5] = {0, 0, 0, 0, 0};
     e = hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = rtk::launch_selftest(d, n_random, nullptr);
     if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
     (void)hipFree(d);
     if (e != hipSuccess) return hip_fail(e, "rt_selftest_kernel");
-    for (int i = 0; i < 4; ++i) out[i] = h[i];
+    for (int i = 0; i < 5; ++i) out[i] = h[i];
     return RT_OK;
 }
 

@@ -113,17 +113,22 @@ RT_HD float reflectance(float cos_t, float ri) {
 //   b' = v_div_scale(b), a' = v_div_scale(a), r = v_rcp(b'), y = fma(fma(-b', r, 1), r, r),
 //   q0 = a'*y, q1 = fma(fma(-b', q0, a'), y, q0), q2 = v_div_fmas(fma(-b', q1, a'), y, q1),
 //   result = v_div_fixup(q2, b, a).
-// When a and b are +-0 or have magnitudes in [2^-40, 2^40] (b nonzero), div_scale returns
-// its operand unchanged and asks for no rescaling (the exponent gap stays below 96, a/b,
-// 1/b and a stay far from the subnormal range), div_fmas is then a plain fma and div_fixup
-// only restores the quotient's sign for a == +-0.  div_core is that unscaled arithmetic,
-// so on this domain it returns exactly the bits of a / b — and y, which depends on b only,
-// is shared by every division by the same b.  sqrt_core is likewise the compiler's
-// correctly rounded sqrtf without its rescaling of x < 2^-96 and its +-0 / +inf fix-up,
-// exact for x == +0 and for x in [2^-96, +inf].  Used where the operands are in the domain
-// by construction (the defocus-disk normalisation, get_ray);
+// div_scale rescales only when b or 1/b is subnormal, |a| < 2^-103, or the exponent gap
+// e(a) - e(b) reaches 96 or -126.  On the domain
+//     |b| in [2^-20, 2^33),  |a| in [2^-100, 2^91),  e(a) - e(b) in [-120, 88]
+// (and for a == +-0, b in that range) it returns its operand unchanged and asks for no
+// rescaling, div_fmas is then a plain fma, and div_fixup only restores the sign of a zero
+// quotient.  div_core is that unscaled arithmetic, so on this domain it returns exactly the
+// bits of a / b — and y, which depends on b only, is shared by every division by the same
+// b.  sqrt_core is one residual correction of x * rsq(x), g + (x - g^2) * rsq(x) / 2: five
+// VALU operations against the compiler's sixteen (rescaling of x < 2^-96, v_sqrt, a
+// two-sided +-1 ulp residual test, the +-0 / +inf fix-up).  It returns the bits of sqrtf
+// for every finite x >= 2^-96 — all 1.88e9 of them are compared on the device by the
+// self-test — and NaN for +0 and +inf, which are outside its domain.
+// Used where the operands are in the domain by construction or by a wave-wide check
+// (rt_kernels.hip: defocus disk, roots, normal, sky, metal / dielectric normalisations);
 // tests/test_gpu_parity.py::test_fastmath_selftest checks both against the IEEE operations
-// on the GPU.
+// on the GPU over that domain, and the root selection built on them against consider().
 __device__ __forceinline__ float rcp_refined(float b) {
     const float r = __builtin_amdgcn_rcpf(b);
     return fmaf(fmaf(-b, r, 1.0f), r, r);
@@ -140,13 +145,14 @@ __device__ __forceinline__ float div_core_signed(float a, float b, float y) {
     return copysignf(div_core(a, b, y), q0);
 }
 __device__ __forceinline__ float sqrt_core(float x) {
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float s_dn = __int_as_float(__float_as_int(s) - 1);
-    const float s_up = __int_as_float(__float_as_int(s) + 1);
-    const float t = fmaf(-s_dn, s, x) <= 0.0f ? s_dn : s;
-    return fmaf(-s_up, s, x) > 0.0f ? s_up : t;
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float g = x * y, h = 0.5f * y;
+    return fmaf(fmaf(-g, g, x), h, g);
 }
-
-
+// |x| as its bit pattern (domain checks on the integer view)
+__device__ __forceinline__ uint32_t abs_bits(float x) { return __float_as_uint(x) & 0x7FFFFFFFu; }
+constexpr uint32_t kBits2m100 = 0x0D800000u;   // 2^-100
+constexpr uint32_t kBits2m20 = 0x35800000u;    // 2^-20
+constexpr uint32_t kBits2p40 = 0x53800000u;    // 2^40
 
 }  // namespace rtd

@@ -92,7 +92,7 @@ hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t wid
 hipError_t launch_present(const float4* in, uchar4* out, uint64_t texels,
                           const float* srgb_t, hipStream_t stream);
 const char* trace_kernel_name();
-// Exact fast-path self-test (rt_selftest_fastmath): cnt[4] device counters, zeroed.
+// Exact fast-path self-test (rt_selftest_fastmath): cnt[5] device counters, zeroed.
 hipError_t launch_selftest(unsigned long long* cnt, uint64_t n_rand, hipStream_t stream);
 
 }  // namespace rtk

@@ -102,6 +102,33 @@ __device__ __forceinline__ void consider(float disc, float h, float a, uint32_t 
     }
 }
 
+// consider() for camera rays whose domain the host has proven (camera_rays_bounded in
+// rt_abi.cpp): a = |d|^2 in [2^-11, 2^20] and |h|, sqrt(D) <= 2^53 for every sphere.  Then
+// sqrt_core(D + 2^-126) and div_core (ya = the shared reciprocal of a) give the IEEE bits
+// wherever the bits matter: for D >= 2^-96 adding 2^-126 (< half an ulp of D) changes
+// nothing; for D in [0, 2^-96) both sqrt(D) and sqrt_core(D + 2^-126) are below 2^-47, so
+// h -+ q rounds to h when |h| >= 2^-22, and below that both roots are under 0.001 (rejected)
+// with either q; |h -+ q| < 2^-100 gives a root under 2^-89 (rejected) with either quotient;
+// every other quotient is inside div_core's exact domain.  A first root above 0.001 and at
+// or beyond tmax also rejects the second: h + q >= h - q and a > 0 make that root larger
+// still.  The device self-test replays both functions on random grazing and ordinary
+// cases (rt_selftest_fastmath, out[4]).
+__device__ __forceinline__ void consider_fast(float disc, float h, float a, float ya,
+                                              uint32_t i, float& tmax, int& idx) {
+    if (!(disc < 0.0f)) {                                               // wgsl:189
+        const float q = sqrt_core(disc + 0x1p-126f);
+        float root = div_core(h - q, a, ya);
+        if (root <= 0x1.0624dep-10f) {                                  // wgsl:196
+            root = div_core(h + q, a, ya);
+            if (root <= 0x1.0624dep-10f || tmax <= root) return;        // wgsl:198
+        } else if (tmax <= root) {
+            return;
+        }
+        tmax = root;
+        idx = (int)i;
+    }
+}
+
 // "!(D < 0)" for any of K discriminants, on the bit patterns: a float is < 0 exactly
 // when its int32 view is <= 0xFF800000 (-inf) and it is not -0.  D = fma(h, h, -(a*c))
 // with h*h >= +0 and a >= +0 cannot round to -0, so the test is one max-tree and one
@@ -135,14 +162,28 @@ constexpr int scan_chunk() { return is_list_kernel(kScan) ? RT_LIST_CHUNK : RT_S
 // their rt_update_frames one frame per launch).
 template <int kScan>
 constexpr bool kStoreEach = is_list_kernel(kScan);
+// Exact fast division / sqrt cores (rt_device.h) in the camera-ray-only instances, which
+// rt_abi.cpp selects only for cameras and scenes inside the proven domain
+// (camera_rays_bounded): bit 1 the roots of the scan, 2 the normal, 4 the sky, 8 the
+// metal / dielectric normalisations (the last three behind a wave-wide check of their
+// operands).  K3 per frame (fused): 21.7 us without, 20.9 / 20.1 / 20.1 us with bits
+// 1 / 1-2 / 1-4; the accumulator's three divisions by f32(n + 1) the same way (checked
+// numerators in [2^-88, 2^88)) measured +0.75 us and are left to the compiler.
+#ifndef RT_FAST_CORES
+#define RT_FAST_CORES 15
+#endif
+template <int kScan>
+constexpr bool fast_core(int bit) { return is_list_kernel(kScan) && (RT_FAST_CORES & bit) != 0; }
 
-template <int K>
+// kFast: camera rays in the host-proven domain (consider_fast).
+template <int K, bool kFast = false>
 __device__ __forceinline__ Hit scan_exhaustive(const float4* __restrict__ geom, uint32_t count,
                                                v3 o, v3 d) {
     float tmax = 0x1.05ed2ep+118f;             // 3.4e35 (wgsl:266)
     int idx = -1;
     if (count == 0) return Hit{idx, tmax};
     const float a = dot(d, d);                 // wgsl:184 (ray-invariant)
+    const float ya = kFast ? rcp_refined(a) : 0.0f;
     // The record list is zero-padded to whole chunks plus one chunk more (rt_abi.cpp), so
     // every chunk (and the one-ahead prefetch) is a full scalar load; padding records are
     // never accepted (consider() is only called for indices < count).
@@ -159,7 +200,12 @@ __device__ __forceinline__ Hit scan_exhaustive(const float4* __restrict__ geom, 
         if (__builtin_expect(max_bits<K>(dd) > (int)0xFF800000, 0)) {
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (i + k < count) consider(dd[k], hh[k], a, i + k, tmax, idx);
+                if (i + k < count) {
+                    if (kFast)
+                        consider_fast(dd[k], hh[k], a, ya, i + k, tmax, idx);
+                    else
+                        consider(dd[k], hh[k], a, i + k, tmax, idx);
+                }
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) cur[k] = nxt[k];
@@ -392,6 +438,25 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
     d = sub(pc, o);
 }
 
+// normalize(v) = v / sqrt(v.v) (WGSL normalize).  kFast: when every active lane's |v|^2 is
+// in [2^-20, 2^40] (NaN, 0 and inf are not) and its components are >= 2^-100 in
+// magnitude, sqrt_core and div_core with the shared reciprocal of |v| in [2^-10, 2^20]
+// (components <= |v|: inside div_core's exact domain); otherwise the IEEE operations.
+template <bool kFast>
+__device__ __forceinline__ v3 normalize_w(v3 v) {
+    if (kFast) {
+        const float dd = dot(v, v);
+        const bool in = __float_as_uint(dd) - kBits2m20 < kBits2p40 - kBits2m20 &&
+                        min(min(abs_bits(v.x), abs_bits(v.y)), abs_bits(v.z)) >= kBits2m100;
+        if (__ballot(!in) == 0ull) {
+            const float len = sqrt_core(dd);
+            const float y = rcp_refined(len);
+            return mk(div_core(v.x, len, y), div_core(v.y, len, y), div_core(v.z, len, y));
+        }
+    }
+    return normalize(v);
+}
+
 // ray_color (wgsl:261-297), executed by the whole wave: `live` marks the lanes whose path
 // is still being traced; the bounce loop runs while any lane is live, and a lane's
 // values are only updated while it is live, so each lane computes exactly its own
@@ -420,8 +485,8 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
         // (one inlined walk for both pointers: two copies measured slower)
         const Hit hit =
             (kScan != kTraceCulled || listed)
-                ? scan_exhaustive<scan_chunk<kScan>()>(listed ? p.cand_rec + lbase : p.geom,
-                                                       listed ? ncand : p.count, o, d)
+                ? scan_exhaustive<scan_chunk<kScan>(), fast_core<kScan>(1)>(
+                      listed ? p.cand_rec + lbase : p.geom, listed ? ncand : p.count, o, d)
             : p.lds_records ? scan_culled<true>(p.geom, p.count, o, d, live)
                             : scan_culled<false>(p.geom, p.count, o, d, live);
 #endif
@@ -456,7 +521,20 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
         }
         const v3 hp = fmas(hit.t, d, o);
         const v3 C = mk(pr.x, pr.y, pr.z);
-        const v3 outward = divs(sub(hp, C), pr.w);
+        // wgsl:209: (p - C) / R.  Fast core: |R| in [2^-20, 2^20] (host-proven) and every
+        // hit lane's three numerators >= 2^-100 in magnitude (they are <= 2^43: the hit
+        // lies on a sphere of the bounded scene).
+        const v3 rel = sub(hp, C);
+        v3 outward;
+        if (fast_core<kScan>(2) &&
+            __ballot(min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z)) <
+                     kBits2m100) == 0ull) {
+            const float y = rcp_refined(pr.w);
+            outward = mk(div_core(rel.x, pr.w, y), div_core(rel.y, pr.w, y),
+                         div_core(rel.z, pr.w, y));
+        } else {
+            outward = divs(rel, pr.w);
+        }
         const bool front = dot(d, outward) < 0.0f;
         const v3 n = front ? outward : neg(outward);
         v3 att, nd;
@@ -466,32 +544,45 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
             nd = dir;
             att = mk(mat.x, mat.y, mat.z);
         } else if (mat.w <= 1.0f) {                               // metal wgsl:95-100
-            const v3 refl = fmas(mat.w, ruv, normalize(reflect(d, n)));
+            constexpr bool kF = fast_core<kScan>(8);
+            const v3 refl = fmas(mat.w, ruv, normalize_w<kF>(reflect(d, n)));
             if (!(dot(refl, n) > 0.0f)) {                         // wgsl:277-279
                 black = true;
                 live = false;
                 continue;
             }
-            nd = normalize(refl);
+            nd = normalize_w<kF>(refl);
             att = mk(mat.x, mat.y, mat.z);
         } else {                                                  // dielectric wgsl:102-135
             att = mk(1.0f, 1.0f, 1.0f);
             const float ratio = front ? 1.0f / mat.x : mat.x;
-            const v3 u = normalize(d);
+            constexpr bool kF = fast_core<kScan>(8);
+            const v3 u = normalize_w<kF>(d);
             const float cos_t = fminf(dot(neg(u), n), 1.0f);
             const float sin_t = sqrtf(fmaf(-cos_t, cos_t, 1.0f));
             const bool cannot = ratio * sin_t > 1.0f;
             const bool refl = cannot || reflectance(cos_t, ratio) > r_sb;
             const v3 dir = refl ? reflect(u, n) : refract(u, n, ratio);
-            nd = normalize(dir);
+            nd = normalize_w<kF>(dir);
         }
         cf = mul(cf, att);                                        // wgsl:285-286
         o = hp;
         d = nd;
     }
     if (black) return mk(0.0f, 0.0f, 0.0f);
-    // Sky (wgsl:293-296): only normalize(d).y is used.
-    const float uy = d.y / sqrtf(dot(d, d));
+    // Sky (wgsl:293-296): only normalize(d).y is used.  Fast core when every lane's |d|^2
+    // is in [2^-20, 2^40] (NaN and 0 are not): sqrt_core is exact there, and so is
+    // div_core(d.y, |d|) for |d.y| >= 2^-100; below that |uy| < 2^-80 and uy + 1 == 1
+    // with either quotient.
+    const float dd = dot(d, d);
+    float uy;
+    if (fast_core<kScan>(4) &&
+        __ballot(__float_as_uint(dd) - kBits2m20 >= kBits2p40 - kBits2m20) == 0ull) {
+        const float len = sqrt_core(dd);
+        uy = div_core(d.y, len, rcp_refined(len));
+    } else {
+        uy = d.y / sqrtf(dd);
+    }
     const float a = 0.5f * (uy + 1.0f);
     const float om = 1.0f - a;
     return mul(cf, mk(fmaf(a, 0.5f, om), fmaf(a, 0x1.666666p-1f, om), fmaf(a, 1.0f, om)));
@@ -610,7 +701,7 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 // chain: 22.2 vs 24.0 µs per K3 frame on one GPU, 3.3 vs 4.3 µs for an 8-rank share.
 // Returns false (nothing done) when some pixel's loaded count differs from the hint.
 #ifndef RT_FRAME_GROUP
-#define RT_FRAME_GROUP 4   // 2 / 4 / 8: K3 22.2 / 22.2 / 24.6 us per frame, 8-rank share 3.5 / 3.3 / 3.4
+#define RT_FRAME_GROUP 2   // 2 / 4: K3 19.7 / 20.5 us per frame, 8-rank share 3.36 / 3.45
 #endif
 constexpr uint32_t kFrameGroup = RT_FRAME_GROUP;
 template <int kScan>
@@ -850,24 +941,61 @@ __global__ __launch_bounds__(256) void rt_present_kernel(const float4* __restric
 
 // ---- Self-test of the exact fast paths (rt_selftest_fastmath) ------------------------
 // cnt[0]: defocus normalisation, all 2^32 values of hash(seed + 1): fast vs IEEE bits.
-// cnt[1]: div_core_signed on random a, b with magnitudes in [2^-40, 2^40) (a also +-0,
-//         b also the accumulator's n + 1), vs a / b.
-// cnt[2]: sqrt_core on random x in [2^-96, 2^128), every f32 in [0.25, 4), +0 and +inf,
-//         vs sqrtf.
-// cnt[3]: cases run.
+// cnt[1]: div_core_signed vs a / b on random a, b over div_core's domain (rt_device.h:
+//         |b| in [2^-20, 2^33), |a| in [2^-100, 2^91), exponent gap in [-120, 88]; a also
+//         +-0, b also the accumulator's n + 1 up to 2^32) and over [2^-40, 2^40]^2.
+// cnt[2]: sqrt_core vs sqrtf on every finite x >= 2^-96 (exhaustive).
+// cnt[3]: consider_fast vs consider (root selection, tmax and index) on random rays and
+//         spheres of the camera-ray domain (|d|^2 in [2^-11, 2^20], |O|, |C| + |R| <= 2^39),
+//         half of them grazing (D near 0), with random incoming tmax.
+// cnt[4]: cases run.
 __device__ __forceinline__ uint32_t mix32(uint64_t i, uint32_t salt) {
     return hash((uint32_t)i ^ hash((uint32_t)(i >> 32) + salt));
 }
-__device__ __forceinline__ float rand_in_box(uint32_t r, uint32_t e) {
-    // sign from r's top bit, mantissa from r, exponent e in [-40, 39]
-    const uint32_t bits = (r & 0x807FFFFFu) | ((uint32_t)(127 - 40 + (int)(e % 80u)) << 23);
-    return __uint_as_float(bits);
+// sign from r's top bit, mantissa from r, exponent e (unbiased)
+__device__ __forceinline__ float with_exp(uint32_t r, int e) {
+    return __uint_as_float((r & 0x807FFFFFu) | ((uint32_t)(127 + e) << 23));
+}
+__device__ __forceinline__ float unit_rand(uint32_t r) {   // [-1, 1)
+    return (float)(int32_t)r * 0x1p-31f;
 }
 __device__ __forceinline__ bool same_bits(float x, float y) {   // NaN == NaN
     return __float_as_uint(x) == __float_as_uint(y) || (x != x && y != y);
 }
+__device__ __forceinline__ bool root_case(uint64_t i) {
+    const uint32_t r0 = mix32(i, 11u), r1 = mix32(i, 12u), r2 = mix32(i, 13u),
+                   r3 = mix32(i, 14u), r4 = mix32(i, 15u), r5 = mix32(i, 16u);
+    const float ds = with_exp(0u, -5 + (int)(r0 % 15u));          // |d| up to ~2^10
+    const v3 d = mk(unit_rand(r1) * ds, unit_rand(r2) * ds, unit_rand(r3) * ds);
+    const float os = with_exp(0u, -10 + (int)((r0 >> 8) % 48u));  // |O| up to ~2^38
+    const v3 o = mk(unit_rand(r4) * os, unit_rand(r5) * os, unit_rand(r1 ^ r5) * os);
+    const float R = with_exp(r2 & 0x7FFFFFu, -20 + (int)((r0 >> 16) % 40u));
+    // a point on the ray at parameter t0, then sideways by ~R (grazing) or anywhere
+    const float t0 = unit_rand(r3 ^ r4) * with_exp(0u, -12 + (int)((r0 >> 24) % 30u));
+    v3 side = mk(unit_rand(r4 ^ r2), unit_rand(r5 ^ r3), unit_rand(r1 ^ r4));
+    const float sd = dot(side, d) / dot(d, d);
+    side = sub(side, mk(sd * d.x, sd * d.y, sd * d.z));           // ~perpendicular to d
+    const float sl = sqrtf(dot(side, side));
+    const float jitter = 1.0f + unit_rand(r5) * with_exp(0u, -(int)(r1 % 31u));
+    const float k = (r2 & 1u) ? R * jitter / sl : unit_rand(r3) * os / sl;
+    const v3 C = mk(fmaf(t0, d.x, o.x) + k * side.x, fmaf(t0, d.y, o.y) + k * side.y,
+                    fmaf(t0, d.z, o.z) + k * side.z);
+    const float a = dot(d, d);
+    if (!(a >= 0x1p-11f && a <= 0x1p20f) || !(sqrtf(dot(o, o)) <= 0x1p39f) ||
+        !(sqrtf(dot(C, C)) + R <= 0x1p39f) || !(sl > 0.0f))
+        return true;                                  // outside the domain: not a case
+    float h;
+    const float disc = discriminant(make_float4(C.x, C.y, C.z, R * R), o, d, a, h);
+    const uint32_t tk = r4 % 3u;
+    const float t_in = tk == 0 ? 0x1.05ed2ep+118f : tk == 1 ? fabsf(t0) : fabsf(t0) * 0.5f;
+    float t1 = t_in, t2 = t_in;
+    int i1 = 7, i2 = 7;
+    consider(disc, h, a, 3u, t1, i1);
+    consider_fast(disc, h, a, rcp_refined(a), 3u, t2, i2);
+    return same_bits(t1, t2) && i1 == i2;
+}
 __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cnt, uint64_t n_rand) {
-    unsigned long long bad0 = 0, bad1 = 0, bad2 = 0, runs = 0;
+    unsigned long long bad0 = 0, bad1 = 0, bad2 = 0, bad3 = 0, runs = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32);
          i += stride) {
@@ -879,30 +1007,36 @@ __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cn
         const float y = rcp_refined(len);
         bad0 += (__float_as_uint(div_core(sa, len, y)) != __float_as_uint(sa / len_ref)) ||
                 (__float_as_uint(div_core(ca, len, y)) != __float_as_uint(ca / len_ref));
+        const float x = __uint_as_float((uint32_t)i);
+        if ((uint32_t)i >= 0x0F800000u && (uint32_t)i < 0x7F800000u)   // [2^-96, +inf)
+            bad2 += __float_as_uint(sqrt_core(x)) != __float_as_uint(sqrtf(x));
         ++runs;
     }
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_rand; i += stride) {
         const uint32_t r0 = mix32(i, 1u), r1 = mix32(i, 2u), r2 = mix32(i, 3u);
-        float a = rand_in_box(r0, r2 & 0xFFFFu);
-        float b = rand_in_box(r1, r2 >> 16);
-        if ((r2 & 0x700u) == 0) a = (r0 & 1u) ? -0.0f : 0.0f;
-        if ((r2 & 0x3800u) == 0) b = (float)(1u + (r1 & 0xFFFFFFu));   // n + 1 counts
+        float a, b;
+        if (r2 & 0x40000000u) {                       // the general domain
+            const int eb = -20 + (int)(r2 % 53u);
+            int ea = -100 + (int)((r2 >> 8) % 191u);
+            ea = max(eb - 120, min(eb + 88, ea));
+            a = with_exp(r0, ea);
+            b = with_exp(r1, eb);
+        } else {                                      // [2^-40, 2^40]^2
+            a = with_exp(r0, -40 + (int)(r2 % 80u));
+            b = with_exp(r1, -40 + (int)((r2 >> 8) % 80u));
+        }
+        if ((r2 & 0x70000u) == 0) a = (r0 & 1u) ? -0.0f : 0.0f;
+        if ((r2 & 0x380000u) == 0)                    // n + 1 counts, n < 2^32 - 1
+            b = (float)((r2 & 0x400000u) ? 1u + (r1 & 0xFFFFFFu) : max(r1, 1u));
         bad1 += !same_bits(div_core_signed(a, b, rcp_refined(b)), a / b);
-        const float x = __uint_as_float((r0 & 0x7FFFFFu) |
-                                        ((uint32_t)(127 - 96 + (int)(r1 % 224u)) << 23));
-        bad2 += !same_bits(sqrt_core(x), sqrtf(x));
-        const float z = __uint_as_float(0x3E800000u + (uint32_t)(i & 0x1FFFFFFu));  // [0.25, 4)
-        bad2 += !same_bits(sqrt_core(z), sqrtf(z));
+        bad3 += !root_case(i);
         ++runs;
-    }
-    if (blockIdx.x == 0 && threadIdx.x < 3) {
-        const float sp[3] = {0.0f, __uint_as_float(0x7F800000u), 0x1p-96f};
-        bad2 += !same_bits(sqrt_core(sp[threadIdx.x]), sqrtf(sp[threadIdx.x]));
     }
     atomicAdd(&cnt[0], bad0);
     atomicAdd(&cnt[1], bad1);
     atomicAdd(&cnt[2], bad2);
-    atomicAdd(&cnt[3], runs);
+    atomicAdd(&cnt[3], bad3);
+    atomicAdd(&cnt[4], runs);
 }
 
 hipError_t launch_selftest(unsigned long long* cnt, uint64_t n_rand, hipStream_t stream) {

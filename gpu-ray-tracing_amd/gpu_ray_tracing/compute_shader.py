@@ -80,8 +80,9 @@ class ComputeShaderPipeline:
         return int(out.value)
 
     def selftest_fastmath(self, n_random: int = 1 << 26) -> list[int]:
-        """rt_selftest_fastmath: [defocus, division, sqrt mismatches, cases run]."""
-        out = (ctypes.c_uint64 * 4)()
+        """rt_selftest_fastmath: [defocus, division, sqrt, root-selection mismatches,
+        cases run]."""
+        out = (ctypes.c_uint64 * 5)()
         _lib.call("rt_selftest_fastmath", self._ctx, n_random, out)
         return list(out)
 

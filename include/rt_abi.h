@@ -236,9 +236,10 @@ RT_API void rt_srgb_thresholds(float out[256]);
  * of f32 division and sqrt used by the trace kernel (rt_device.h: div_core, sqrt_core)
  * return the IEEE bits on their documented domains — exhaustively for the defocus-disk
  * normalisation (all 2^32 values of its random input) and on n_random random cases for
- * division and sqrt.  out[0..2] = mismatches (defocus, division, sqrt), out[3] = cases.
- * Synchronous. */
-RT_API rt_status rt_selftest_fastmath(rt_ctx* ctx, uint64_t n_random, uint64_t out[4]);
+ * division, sqrt and the scan's root selection built on them (random camera-domain rays
+ * and spheres, half grazing).  out[0..3] = mismatches (defocus, division, sqrt, roots),
+ * out[4] = cases.  Synchronous. */
+RT_API rt_status rt_selftest_fastmath(rt_ctx* ctx, uint64_t n_random, uint64_t out[5]);
 
 /* ------------------------------------------------------------------------------------ */
 /* Host-side mirror of the reference's main-world code (C++ implementation, no device)   */

@@ -510,12 +510,14 @@ def test_image_files_from_device(rt, pipe, tmp_path):
 
 def test_fastmath_selftest(rt):
     """The exact fast paths of division / sqrt (rt_device.h) return the IEEE bits: all 2^32
-    inputs of the defocus-disk normalisation, 2^26 random division and sqrt cases."""
+    inputs of the defocus-disk normalisation, 2^26 random division and sqrt cases, and
+    the scan's root selection on them (consider_fast) picks the same root and sphere as
+    the IEEE one on 2^26 random camera-domain rays and spheres."""
     p = rt.ComputeShaderPipeline(0)
     out = p.selftest_fastmath(1 << 26)
     p.close()
-    assert out[:3] == [0, 0, 0], out
-    assert out[3] == (1 << 32) + (1 << 26)
+    assert out[:4] == [0, 0, 0, 0], out
+    assert out[4] == (1 << 32) + (1 << 26)
 
 
 @pytest.mark.parametrize("depth,spp", [(1, 500), (3, 3), (8, 500)])

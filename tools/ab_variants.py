@@ -4,6 +4,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 cfg, rounds, libs = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
 res = {l: [] for l in libs}
+fres = {l: [] for l in libs}
 def spec(l):
     """lib[:K=V,K=V] -> (lib path, extra env)"""
     path, _, rest = l.partition(":")
@@ -19,7 +20,9 @@ for r in range(rounds):
         line = [x for x in out.stdout.splitlines() if x.startswith("{")]
         if not line:
             print(l, "FAILED", out.stderr[-2000:], flush=True); sys.exit(1)
-        d = json.loads(line[-1]); res[l].append(d["median_us"])
+        d = json.loads(line[-1]); res[l].append(d["median_us"]); fres[l].append(d.get("fused_us", 0.0))
         print(r, Path(l).name, d, flush=True)
 for l in libs:
-    v = sorted(res[l]); print(f"{Path(l).name:48s} median {v[len(v)//2]:8.1f} us  min {v[0]:8.1f}")
+    v = sorted(res[l]); fv = sorted(fres[l])
+    print(f"{Path(l).name:40s} median {v[len(v)//2]:8.2f} us  min {v[0]:8.2f}  "
+          f"fused {fv[len(fv)//2]:7.2f} us/frame  min {fv[0]:7.2f}")

@@ -25,6 +25,16 @@ def main(cfg="k3", iters=40):
         evs[k][0].record(st); pipe.update(a, b, w, h, c2, sc); evs[k][1].record(st); a, b = b, a
     torch.cuda.synchronize()
     t = sorted(x.elapsed_time(y) * 1e3 for x, y in evs)
+    # fused: rt_update_frames calls of 64 frames (frame groups when hinted), us per frame
+    seeds = rt.frame_seeds(0x5EED, 64)
+    fev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(6)]
+    for k in range(6):
+        fev[k][0].record(st)
+        newest = pipe.update_frames(a, b, w, h, c2, sc, seeds)
+        fev[k][1].record(st)
+        if newest == 1: a, b = b, a
+    torch.cuda.synchronize()
+    ft = sorted(x.elapsed_time(y) * 1e3 / 64 for x, y in fev[1:])
     L = rt._lib.lib()
     stamps = None
     if hasattr(L, "rt_diag_stamps"):
@@ -34,6 +44,7 @@ def main(cfg="k3", iters=40):
         L.rt_diag_stamps(buf, ctypes.c_uint(waves))
         stamps = [round(buf[k] / waves, 1) for k in range(1, 8)]
     print(json.dumps({"cfg": cfg, "median_us": t[len(t) // 2], "min_us": t[0], "hash_ok": ok,
+                      "fused_us": ft[len(ft) // 2],
                       "stamps_cycles_per_wave": stamps}))
 
 if __name__ == "__main__":
