@@ -40,6 +40,15 @@ struct rt_ctx {
     float4* cand_sph = nullptr;
     uint64_t cand_tiles = 0;        // allocated tiles
     std::vector<unsigned char> cand_key;
+    uint64_t cand_gen = 0;          // bumped whenever the lists are rebuilt
+    // Cost-ordered tiles (TraceParams::tile_order): per-tile durations recorded by the
+    // first camera-ray-only launch of a list generation, and the order derived from them.
+    uint32_t* tile_cost = nullptr;
+    uint32_t* tile_order = nullptr;
+    uint64_t order_tiles = 0;       // allocated tiles
+    uint64_t order_gen = ~0ull;     // cand_gen the order was measured for
+    uint32_t order_frames = 0;      // frames of the launch that measured it
+    int tile_order_mode = RT_TILE_ORDER_AUTO;
     float* d_srgb = nullptr;  // rt_srgb_thresholds table on the device (256 floats)
     // hash(x*73) for x < hx_len and hash(y*51) for y < hy_len (wgsl:309-310)
     uint32_t* d_hx = nullptr;
@@ -303,10 +312,63 @@ rt_status ensure_candidates(rt_ctx* ctx, rtk::TraceParams& p, hipStream_t stream
                                               stream);
         if (e != hipSuccess) return hip_fail(e, "rt_candidates_kernel launch");
         ctx->cand_key.assign(kb, kb + sizeof(key));
+        ctx->cand_gen++;
     }
     p.cand_cnt = ctx->cand_cnt;
     p.cand_rec = ctx->cand_rec;
     p.cand_sph = ctx->cand_sph;
+    return RT_OK;
+}
+
+// Cost-ordered tiles for the camera-ray-only instances: the first such launch of a
+// candidate-list generation (same camera geometry, image, stripes and scene) records each
+// tile's duration; rtk::launch_tile_order then sorts the tiles by it on the stream, and
+// later launches of the generation start the costliest tiles first so that the cheap ones
+// fill the tail.  Only the workgroup -> tile assignment changes, never a pixel's result.
+rt_status plan_tile_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t stream) {
+    p.tile_order = nullptr;
+    p.tile_cost = nullptr;
+    // (single-frame launches keep raster order: their accumulator traffic is a large part
+    // of the frame, and scattered tiles cost more in HBM than the tail they save)
+    if (!rtk::is_list_kernel(kernel) || ctx->tile_order_mode == RT_TILE_ORDER_OFF ||
+        p.cand_k == 0 || p.frames < 2)
+        return RT_OK;
+    // A launch of a few frames measures mostly start-up and placement noise: launches keep
+    // re-measuring (in the current order) until one of kOrderFrames frames or more has.
+    constexpr uint32_t kOrderFrames = 16;
+    const bool have = ctx->order_gen == ctx->cand_gen;
+    if (have) p.tile_order = ctx->tile_order;
+    if (have && ctx->order_frames >= std::min(kOrderFrames, p.frames)) return RT_OK;
+    const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
+    if (tiles > ctx->order_tiles) {
+        if (ctx->order_tiles) {
+            hipError_t e = hipStreamSynchronize(stream);   // old order may be in use
+            if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+        }
+        (void)hipFree(ctx->tile_cost);
+        (void)hipFree(ctx->tile_order);
+        ctx->tile_cost = ctx->tile_order = nullptr;
+        ctx->order_tiles = 0;
+        ctx->order_gen = ~0ull;
+        p.tile_order = nullptr;
+        hipError_t e = hipMalloc(&ctx->tile_cost, tiles * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMalloc(&ctx->tile_order, tiles * sizeof(uint32_t));
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(tile order)");
+        ctx->order_tiles = tiles;
+    }
+    p.tile_cost = ctx->tile_cost;
+    return RT_OK;
+}
+
+// After a launch that recorded tile costs: derive the order for the next launches.
+rt_status finish_tile_order(rt_ctx* ctx, const rtk::TraceParams& p, hipStream_t stream) {
+    if (!p.tile_cost) return RT_OK;
+    const uint32_t tiles_x = (p.width + 7u) >> 3;
+    hipError_t e = rtk::launch_tile_order(p.tile_cost, ctx->tile_order,
+                                          tiles_x * p.local_bands, tiles_x, stream);
+    if (e != hipSuccess) return hip_fail(e, "rt_tile_order_kernel launch");
+    ctx->order_gen = ctx->cand_gen;
+    ctx->order_frames = p.frames;
     return RT_OK;
 }
 
@@ -487,8 +549,11 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         p.reset_first = (f0 == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
         for (uint32_t f = 0; f < nf; ++f) p.seed_b[f] = host_f2u(seeds[f0 + f] * 4294967296.0f);
         plan_hint(ctx, p, src, dst);
-        hipError_t e = rtk::launch_trace(p, trace_kernel_for(ctx, p), stream);
+        const int kernel = trace_kernel_for(ctx, p);
+        if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
+        hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
+        if (rt_status s = finish_tile_order(ctx, p, stream)) return s;
         src = dst;  // later launches continue the accumulation in place
     }
     return RT_OK;
@@ -531,6 +596,8 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->d_srgb);
         (void)hipFree(ctx->d_hx);
         (void)hipFree(ctx->d_hy);
+        (void)hipFree(ctx->tile_cost);
+        (void)hipFree(ctx->tile_order);
         free_candidates(ctx);
     }
     delete ctx;
@@ -556,6 +623,14 @@ rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode) {
     if (mode != RT_FRAME_PAIRS_AUTO && mode != RT_FRAME_PAIRS_OFF && mode != RT_FRAME_PAIRS_ON)
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown frame-pair mode");
     ctx->frame_pairs = mode;
+    return RT_OK;
+}
+
+rt_status rt_set_tile_order(rt_ctx* ctx, int mode) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (mode != RT_TILE_ORDER_AUTO && mode != RT_TILE_ORDER_OFF)
+        return fail(RT_ERR_INVALID_ARGUMENT, "unknown tile-order mode");
+    ctx->tile_order_mode = mode;
     return RT_OK;
 }
 
@@ -662,8 +737,10 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         const bool pairable = kernel == rtk::kTraceList && p.store_each && known &&
                               p.hint_frames == nf;
         if (pairable && ctx->frame_pairs != RT_FRAME_PAIRS_OFF) kernel = rtk::kTraceListPair;
+        if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
+        if (rt_status s = finish_tile_order(ctx, p, stream)) return s;
         // frame f of the launch wrote img[(cur + 1 + f) % 2]
         const int newest = (nf & 1u) ? 1 - cur : cur;
         if (known) {

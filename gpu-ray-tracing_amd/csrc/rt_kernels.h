@@ -63,6 +63,12 @@ struct TraceParams {
     // values and a scalar camera seed; the accumulator load is then only awaited after
     // the sample is traced, and any pixel whose loaded count differs is traced again with
     // its own count — so the hint never changes a bit of the result.
+    // Tile order (camera-ray-only instances, one tile per workgroup): workgroup i of the
+    // launch traces tile tile_order[i] = (local band << 16) | column instead of tile i;
+    // null = natural order.  tile_cost (non-null): each tile's wave 0 stores its
+    // s_memtime duration there, for launch_tile_order.
+    const uint32_t* tile_order;
+    uint32_t* tile_cost;
     uint32_t hint_frames;  // 0 = no hint
     uint32_t hint_n[kHintFrames];
     float4 hint_rs[kHintEntries];
@@ -92,6 +98,10 @@ hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t wid
 hipError_t launch_present(const float4* in, uchar4* out, uint64_t texels,
                           const float* srgb_t, hipStream_t stream);
 const char* trace_kernel_name();
+// tile_order for launch_trace: the local tiles by decreasing recorded cost (quantised
+// log2 of tile_cost), so the slowest tiles start first and the cheap ones fill the tail.
+hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, uint32_t tiles,
+                             uint32_t tiles_x, hipStream_t stream);
 // Exact fast-path self-test (rt_selftest_fastmath): cnt[5] device counters, zeroed.
 hipError_t launch_selftest(unsigned long long* cnt, uint64_t n_rand, hipStream_t stream);
 

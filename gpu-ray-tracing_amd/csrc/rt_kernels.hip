@@ -17,13 +17,16 @@
 #include "rt_device.h"
 #include "rt_kernels.h"
 
+#include <cstring>
+
 namespace rtk {
 
 using namespace rtd;
 
 // Knock-out builds for cost attribution only (tools; never the product): RT_KO bit 1 skips
 // the sphere scan, 2 the shading, 4 the random camera ray, 8 the accumulator load, 16 the
-// store, 32 the accumulator load (keeping the hinted count).
+// store, 32 the accumulator load (keeping the hinted count), 64 the accumulator's divisions
+// of the frame-group path (c = col), 128 the sky's normalisation (uy = d.y).
 #ifndef RT_KO
 #define RT_KO 0
 #endif
@@ -56,6 +59,31 @@ __device__ __forceinline__ void stamp(int k) {
 #define STAMP(k) stamp(k)
 #else
 #define STAMP(k) ((void)0)
+#endif
+
+// ---- diagnostic wave trace (RT_WAVE_TRACE=1 builds only; never in the product) -------
+// Per wave of the camera-ray-only instances: start and end s_memrealtime, HW_ID, XCC_ID,
+// indexed by workgroup * 4 + wave (tools/wave_trace.py reads them via rt_diag_wave_trace).
+#ifndef RT_WAVE_TRACE
+#define RT_WAVE_TRACE 0
+#endif
+#if RT_WAVE_TRACE
+constexpr uint32_t kTraceWaves = 1u << 18;
+__device__ unsigned long long g_wave_t[kTraceWaves][2];
+__device__ unsigned g_wave_id[kTraceWaves][2];
+__device__ __forceinline__ void wave_trace(int end) {
+    const uint32_t gw = (blockIdx.y * gridDim.x + blockIdx.x) * 4u + (threadIdx.x >> 6);
+    if ((threadIdx.x & 63u) == 0 && gw < kTraceWaves) {
+        g_wave_t[gw][end] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
+        if (end) {
+            g_wave_id[gw][0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+            g_wave_id[gw][1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
+        }
+    }
+}
+#define WAVE_TRACE(e) wave_trace(e)
+#else
+#define WAVE_TRACE(e) ((void)0)
 #endif
 
 struct Hit {
@@ -576,6 +604,9 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
     // with either quotient.
     const float dd = dot(d, d);
     float uy;
+#if RT_KO & 128
+    uy = d.y * (dd > -1.0f ? 1.0f : 0.5f);
+#else
     if (fast_core<kScan>(4) &&
         __ballot(__float_as_uint(dd) - kBits2m20 >= kBits2p40 - kBits2m20) == 0ull) {
         const float len = sqrt_core(dd);
@@ -583,6 +614,7 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
     } else {
         uy = d.y / sqrtf(dd);
     }
+#endif
     const float a = 0.5f * (uy + 1.0f);
     const float om = 1.0f - a;
     return mul(cf, mk(fmaf(a, 0.5f, om), fmaf(a, 0x1.666666p-1f, om), fmaf(a, 1.0f, om)));
@@ -636,7 +668,9 @@ __device__ __forceinline__ v3 sample(const TraceParams& p, const Cam& cam, uint3
 // acc: the pixel's loaded accumulator (unused when frame 0 resets it).  Without a hint the
 // count is taken from acc before the first sample; with a hint the first frame is traced
 // with the hinted count while the load is in flight and verified afterwards.
-template <int kScan>
+// kHint = false ignores the hint (counts from acc, full per-pixel random numbers): the
+// frame-group instance's fallback, kept small so that the instance stays within 64 VGPRs.
+template <int kScan, bool kHint = true>
 __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& cam,
                                               uint32_t tile, uint32_t ncand,
                                               const TileCoord& tc, uint32_t hxy, float4 acc) {
@@ -644,7 +678,7 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
     v3 c = mk(0.0f, 0.0f, 0.0f);
     uint32_t n = 0u;
     bool known = p.reset_first != 0u;                             // wgsl:345-350
-    if (!known && p.hint_frames == 0u) {
+    if (!known && (!kHint || p.hint_frames == 0u)) {
         c = mk(acc.x, acc.y, acc.z);                              // wgsl:339-341
         n = f2u(acc.w);
         known = true;
@@ -655,7 +689,7 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
             c = mk(0.0f, 0.0f, 0.0f);
             n = 0u;
         }
-        const bool hinted = f < p.hint_frames;
+        const bool hinted = kHint && f < p.hint_frames;
         uint32_t ng = known ? n : p.hint_n[0];   // count to trace with (unknown: f == 0)
         bool pending = tc.valid;
         for (;;) {
@@ -699,68 +733,75 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 // accumulates the group's frames in order and stores every frame's image (wgsl:352-363) —
 // bit-identical to one wave doing every frame.  More waves, each with a shorter sequential
 // chain: 22.2 vs 24.0 µs per K3 frame on one GPU, 3.3 vs 4.3 µs for an 8-rank share.
-// Returns false (nothing done) when some pixel's loaded count differs from the hint.
+// Called only when every valid pixel's loaded count is the hinted one (rt_trace_kernel).
 #ifndef RT_FRAME_GROUP
 #define RT_FRAME_GROUP 2   // 2 / 4: K3 19.7 / 20.5 us per frame, 8-rank share 3.36 / 3.45
 #endif
 constexpr uint32_t kFrameGroup = RT_FRAME_GROUP;
 template <int kScan>
-__device__ __forceinline__ bool trace_pair(const TraceParams& p, const Cam& cam, uint32_t tile,
+__device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam, uint32_t tile,
                                            uint32_t ncand, const TileCoord& tc, uint32_t hxy,
                                            float4 acc, uint32_t w) {
     const uint32_t spp = p.spp;                                   // wgsl:343
     v3 c = mk(0.0f, 0.0f, 0.0f);
-    uint32_t n = 0u;
-    if (!p.reset_first) {                                         // wgsl:339-341
-        c = mk(acc.x, acc.y, acc.z);
-        n = f2u(acc.w);
-        // every wave sees the same pixels, hence the same decision
-        if (__ballot(tc.valid && n != p.hint_n[0]) != 0ull) return false;
-    }
+    if (!p.reset_first) c = mk(acc.x, acc.y, acc.z);              // wgsl:339-341
+    // From here every valid pixel holds hint_n[f] before frame f (the host's count
+    // bookkeeping, rt_abi.cpp fill_hint): the count arithmetic of wgsl:341-362 is scalar.
     const uint32_t lane = threadIdx.x & 63u;
     for (uint32_t f = 0; f < p.frames; f += kFrameGroup) {
         const uint32_t fw = f + w;
         v3 col = mk(0.0f, 0.0f, 0.0f);
         if (fw < p.frames) {
             const uint32_t ng = p.hint_n[fw];   // every pixel's count before frame fw
-            const bool live = tc.valid && ng < spp;               // wgsl:352
-            if (__ballot(live) != 0ull)
-                col = sample<kScan>(p, cam, tile, ncand, tc, hxy, ng, p.seed_b[fw], fw, live,
-                                    fw < p.hint_frames);
+            if (ng < spp && __ballot(tc.valid) != 0ull)           // wgsl:352
+                col = sample<kScan>(p, cam, tile, ncand, tc, hxy, ng, p.seed_b[fw], fw,
+                                    tc.valid, fw < p.hint_frames);
         }
         if (w != 0u) lds_recs[(w - 1u) * 64u + lane] = make_float4(col.x, col.y, col.z, 0.0f);
         __syncthreads();
         if (w == 0u) {
 #pragma unroll
             for (uint32_t j = 0; j < kFrameGroup; ++j) {
-                if (f + j >= p.frames) break;
+                const uint32_t fj = f + j;
+                if (fj >= p.frames) break;
                 if (j != 0) {
                     const float4 cj = lds_recs[(j - 1u) * 64u + lane];
                     col = mk(cj.x, cj.y, cj.z);
                 }
-                if (tc.valid && n < spp) {
-                    const float k = (float)(n + 1u);              // wgsl:356
+                const uint32_t nb = p.hint_n[fj];                 // count before frame fj
+                uint32_t na = nb;
+                if (nb < spp) {                                   // wgsl:352-358
+#if RT_KO & 64
+                    c = col;
+#else
+                    const float k = (float)(nb + 1u);             // wgsl:356
                     c = mk(c.x + (col.x - c.x) / k, c.y + (col.y - c.y) / k,
                            c.z + (col.z - c.z) / k);
-                    n += 1u;
+#endif
+                    na = nb + 1u;
                 }
                 if (tc.valid)                                     // wgsl:362-363
-                    (((f + j) & 1u) ? p.out2 : p.out)[tc.idx] =
-                        make_float4(c.x, c.y, c.z, (float)n);
-                n = f2u((float)n);
+                    ((fj & 1u) ? p.out2 : p.out)[tc.idx] = make_float4(c.x, c.y, c.z, (float)na);
             }
         }
         __syncthreads();
     }
-    return true;
 }
 
 // One workgroup = 4 waves = 4 consecutive tiles.  (A persistent grid that walks tiles
 // with the next tile's accumulator prefetched — into VGPRs, or into LDS with
 // global_load_lds — measured 15-50 % slower: the loop pushes the kernel past 64 VGPRs /
 // into scratch, and the hardware dispatcher already overlaps the waves' HBM phases.)
+// Minimum waves per SIMD the compiler plans registers for.  7 rather than 8: at 8 it caps
+// SGPRs near 80 and spills ~25 of them into VGPR lanes (v_writelane / v_readlane in the
+// frame loop); at 7 the instances use 94 SGPRs and, at <= 64 VGPRs, still run 8 waves per
+// SIMD (the frame-group instance needs 66 VGPRs: 7 waves).  K3: 29.0 vs 30.3 us per
+// single-frame update, 18.2 vs 18.4 us per fused frame.
 #ifndef RT_TRACE_MIN_WAVES
-#define RT_TRACE_MIN_WAVES 8
+#define RT_TRACE_MIN_WAVES 7
+#endif
+#ifndef RT_TRACE_ATTR
+#define RT_TRACE_ATTR
 #endif
 // Waves (tiles) per workgroup: the culled instance shares the LDS copy of the records
 // among 4 waves; the others use one-wave workgroups, so a finished tile frees its slot
@@ -774,20 +815,55 @@ constexpr uint32_t wg_waves() {
 }
 
 
+// Cost-ordered tiles (TraceParams::tile_order / tile_cost) in the camera-ray-only
+// instances, whose workgroups are one tile each.
+#ifndef RT_TILE_PRIO
+#define RT_TILE_PRIO 0
+#endif
 template <int kScan>
-__global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt_trace_kernel(
+constexpr bool kOrdered =
+    is_list_kernel(kScan) && (kScan == kTraceListPair || wg_waves<kScan>() == 1u);
+// (the start time is parked in tile_cost itself: no register stays live for it)
+template <int kScan>
+__device__ __forceinline__ void cost_start(const TraceParams& p, uint32_t tile, uint32_t wave,
+                                           uint32_t lane) {
+    if (kOrdered<kScan> && p.tile_cost && wave == 0u && lane == 0u)
+        p.tile_cost[tile] = (uint32_t)__builtin_amdgcn_s_memtime();
+}
+template <int kScan>
+__device__ __forceinline__ void record_cost(const TraceParams& p, uint32_t tile, uint32_t wave,
+                                            uint32_t lane) {
+    if (kOrdered<kScan> && p.tile_cost && wave == 0u && lane == 0u)
+        p.tile_cost[tile] = (uint32_t)__builtin_amdgcn_s_memtime() - p.tile_cost[tile];
+}
+
+template <int kScan>
+__global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) RT_TRACE_ATTR void rt_trace_kernel(
     const TraceParams p) {
     STAMP(-2);
+    WAVE_TRACE(0);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     // The wave index is uniform, but the compiler's divergence analysis does not know it;
     // readfirstlane makes the tile (and the candidate-list pointers and counts derived from
     // it) scalar, so list records are read with s_load into SGPRs.
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // (frame pairs: both waves of the workgroup own the same tile)
-    const uint32_t tx =
-        kScan == kTraceListPair ? blockIdx.x : blockIdx.x * wg_waves<kScan>() + wave;
-    const uint32_t lband = blockIdx.y;
+    // (frame groups: all waves of the workgroup own the same tile)
+    uint32_t tx = kScan == kTraceListPair ? blockIdx.x : blockIdx.x * wg_waves<kScan>() + wave;
+    uint32_t lband = blockIdx.y;
+    if (kOrdered<kScan> && p.tile_order) {            // costliest tiles first
+        const uint32_t slot = blockIdx.y * gridDim.x + blockIdx.x;
+        const uint32_t t = p.tile_order[slot];
+        tx = t & 0xFFFFu;
+        lband = t >> 16;
+#if RT_TILE_PRIO
+        // the costliest quarter of the tiles issues first on a shared SIMD
+        const uint32_t q = slot * 4u / (gridDim.x * gridDim.y);
+        if (q == 0u) __builtin_amdgcn_s_setprio(3);
+        else if (q == 1u) __builtin_amdgcn_s_setprio(2);
+        else if (q == 2u) __builtin_amdgcn_s_setprio(1);
+#endif
+    }
     const bool wave_in = tx < tiles_x;
     const TileCoord tc = tile_coord(p, tx, lband, lane);
     // Culled scan: the workgroup stages the scan records (count padded to 64) in LDS once;
@@ -803,6 +879,7 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     }
     if (!wave_in) return;                                         // whole wave exits
     const uint32_t tile = lband * tiles_x + tx;
+    cost_start<kScan>(p, tile, wave, lane);
     // the tile's candidate count (kCandNone: no list)
     const uint32_t ncand =
         (kScan != kTraceExhaustive && p.cand_k) ? p.cand_cnt[tile] : kCandNone;
@@ -829,17 +906,69 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     cam.defocus_angle = p.defocus_angle;
 
     if (kScan == kTraceListPair) {
-        // every frame's image is stored inside; on a count mismatch wave 0 runs the
-        // single-wave loop (with its per-pixel retrace) and wave 1 has nothing to do
-        if (trace_pair<kScan>(p, cam, tile, ncand, tc, hxy, acc, wave) || wave != 0u) return;
+        // every frame's image is stored inside; on a count mismatch (every wave sees the
+        // same pixels, hence takes the same decision) wave 0 runs the single-wave loop and
+        // the others have nothing to do
+        if (p.reset_first || __ballot(tc.valid && f2u(acc.w) != p.hint_n[0]) == 0ull) {
+            trace_pair<kScan>(p, cam, tile, ncand, tc, hxy, acc, wave);
+            record_cost<kScan>(p, tile, wave, lane);
+            WAVE_TRACE(1);
+            return;
+        }
+        if (wave != 0u) return;
     }
-    const float4 res = trace_pixel<kScan>(p, cam, tile, ncand, tc, hxy, acc);
+    const float4 res = trace_pixel<kScan, kScan != kTraceListPair>(p, cam, tile, ncand, tc,
+                                                                   hxy, acc);
 #if RT_KO & 16
     if (res.x == 12345.678f) p.out[tc.idx] = res;
 #else
     if (tc.valid && !(kStoreEach<kScan> && p.store_each)) p.out[tc.idx] = res;  // wgsl:363
 #endif
+    record_cost<kScan>(p, tile, wave, lane);
+    WAVE_TRACE(1);
     STAMP(5);
+}
+
+// launch_tile_order: one 1024-thread workgroup; bucket = quantised log2 of the cost (four
+// buckets per octave), counted in LDS, then each tile is placed at its bucket's next slot,
+// costliest bucket first (order inside a bucket is arbitrary: tiles are independent).
+__global__ __launch_bounds__(1024) void rt_tile_order_kernel(const uint32_t* __restrict__ cost,
+                                                             uint32_t* __restrict__ order,
+                                                             uint32_t tiles, uint32_t tiles_x) {
+    constexpr uint32_t kBuckets = 128;
+    __shared__ uint32_t next[kBuckets];
+    auto bucket = [](uint32_t c) -> uint32_t {
+        if (c == 0u) return kBuckets - 1u;
+        const uint32_t lz = (uint32_t)__builtin_clz(c);
+        const uint32_t e = 31u - lz;
+        const uint32_t m = e >= 2u ? (c >> (e - 2u)) & 3u : (c << (2u - e)) & 3u;
+        return kBuckets - 1u - (e * 4u + m);          // descending cost
+    };
+    for (uint32_t b = threadIdx.x; b < kBuckets; b += blockDim.x) next[b] = 0u;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < tiles; t += blockDim.x) atomicAdd(&next[bucket(cost[t])], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t sum = 0;
+        for (uint32_t b = 0; b < kBuckets; ++b) {
+            const uint32_t c = next[b];
+            next[b] = sum;
+            sum += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < tiles; t += blockDim.x) {
+        const uint32_t pos = atomicAdd(&next[bucket(cost[t])], 1u);
+        order[pos] = ((t / tiles_x) << 16) | (t % tiles_x);
+    }
+}
+
+hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, uint32_t tiles,
+                             uint32_t tiles_x, hipStream_t stream) {
+    if (tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(rt_tile_order_kernel, dim3(1), dim3(1024), 0, stream, tile_cost,
+                       tile_order, tiles, tiles_x);
+    return hipGetLastError();
 }
 
 // One wave per tile: list the spheres the tile's camera rays can hit (see tile_cone).
@@ -1134,6 +1263,25 @@ extern "C" __attribute__((visibility("default"))) int rt_diag_stamps(unsigned lo
 }
 #endif
 
-namespace rtk {
-
-}  // namespace rtk
+#if RT_WAVE_TRACE
+// Diagnostic builds: copies (start, end, hw_id, xcc_id) of the first n waves of the last
+// traced launch to out[4 n] and clears them.
+extern "C" __attribute__((visibility("default"))) int rt_diag_wave_trace(unsigned long long* out,
+                                                                         unsigned n) {
+    if (n > rtk::kTraceWaves) n = rtk::kTraceWaves;
+    static unsigned long long t[rtk::kTraceWaves][2];
+    static unsigned id[rtk::kTraceWaves][2];
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    if (hipMemcpyFromSymbol(t, HIP_SYMBOL(rtk::g_wave_t), sizeof(t)) != hipSuccess) return 1;
+    if (hipMemcpyFromSymbol(id, HIP_SYMBOL(rtk::g_wave_id), sizeof(id)) != hipSuccess) return 1;
+    for (unsigned i = 0; i < n; ++i) {
+        out[4 * i] = t[i][0];
+        out[4 * i + 1] = t[i][1];
+        out[4 * i + 2] = id[i][0];
+        out[4 * i + 3] = id[i][1];
+    }
+    std::memset(t, 0, sizeof(t));
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rtk::g_wave_t), t, sizeof(t)) != hipSuccess) return 1;
+    return 0;
+}
+#endif

@@ -116,6 +116,7 @@ _SIGS = {
     "rt_set_frames_per_launch": (ctypes.c_int, [P, U32]),
     "rt_get_frames_per_launch": (ctypes.c_int, [P, P, ctypes.POINTER(U32)]),
     "rt_set_frame_pairs": (ctypes.c_int, [P, ctypes.c_int]),
+    "rt_set_tile_order": (ctypes.c_int, [P, ctypes.c_int]),
 }
 
 _lib = None

@@ -72,6 +72,11 @@ class ComputeShaderPipeline:
         """rt_set_frame_pairs: 'auto' | 'off' | 'on' (two waves per tile, alternate frames)."""
         _lib.call("rt_set_frame_pairs", self._ctx, {"auto": 0, "off": 1, "on": 2}[mode])
 
+    def set_tile_order(self, mode: str) -> None:
+        """rt_set_tile_order: "auto" (costliest tiles first, from the first launch's
+        per-tile durations) or "off" (raster order)."""
+        _lib.call("rt_set_tile_order", self._ctx, {"auto": 0, "off": 1}[mode])
+
     def frames_per_launch(self, camera) -> int:
         """rt_get_frames_per_launch: frames update_frames fuses per launch for `camera`."""
         out = _lib.U32(0)

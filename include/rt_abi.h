@@ -190,6 +190,15 @@ RT_API rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launc
 #define RT_FRAME_PAIRS_OFF 1
 #define RT_FRAME_PAIRS_ON 2
 RT_API rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode);
+/* Tile scheduling of the fused multi-frame launches of the camera-ray-only kernels
+ * (max_depth <= 1, culled scan mode).  AUTO (default): the first such launch for a camera
+ * geometry / image / stripe map / scene records each 8x8 tile's duration on the device,
+ * and later launches hand the costliest tiles to the first workgroups so that cheap tiles
+ * fill the tail (strong scaling: a rank's share is only a few workgroups per SIMD).  OFF,
+ * and single-frame launches: tiles in raster order.  Pixel results are identical. */
+#define RT_TILE_ORDER_AUTO 0
+#define RT_TILE_ORDER_OFF 1
+RT_API rt_status rt_set_tile_order(rt_ctx* ctx, int mode);
 /* The frames per launch rt_update_frames would use for `camera` (its max_depth) now. */
 RT_API rt_status rt_get_frames_per_launch(const rt_ctx* ctx, const rt_scene_camera* camera,
                                           uint32_t* out_frames);

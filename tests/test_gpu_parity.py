@@ -397,14 +397,17 @@ def test_candidate_list_overflow_falls_back(rt, depth):
 @pytest.mark.parametrize("nranks", [1, 3])
 @pytest.mark.parametrize("frames,depth,spp,per", [(5, 2, 500, 0), (20, 1, 500, 0), (3, 8, 500, 0),
                                                   (7, 1, 4, 0), (4, 1, 500, 1), (6, 3, 500, 4),
-                                                  (5, 8, 500, 4), (9, 2, 3, 3)])
+                                                  (5, 8, 500, 4), (9, 2, 3, 3), (14, 1, 500, 4),
+                                                  (11, 1, 6, 3)])
 @pytest.mark.parametrize("pairs", ["off", "on"])
 def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, spp, per, pairs):
     """rt_update_frames (frames fused per launch, every frame's image stored to the
     ping-pong buffers; or one dispatch per frame) leaves BOTH buffers exactly as chained
     rt_update calls do: the newest frame and the one before, for the whole image and for
     stripe ranks (compact local buffers), across launch boundaries and the spp cap, with
-    and without frame pairs (two waves per tile on alternate frames)."""
+    and without frame groups (several waves per tile on alternate frames); the depth-1
+    cases with several fused launches also run the cost-ordered tile schedule (the first
+    launch records tile costs, the later ones trace the costliest tiles first)."""
     w, h = 56, 40
     sc = rt.synthetic_scene(120)
     seeds = rt.frame_seeds(21, frames)

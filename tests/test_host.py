@@ -21,7 +21,7 @@ def header_functions():
 
 def test_library_exports_every_declared_symbol(rt):
     declared = header_functions()
-    assert len(declared) == 28
+    assert len(declared) == 29
     nm = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True,
                         text=True, check=True).stdout
     exported = set(re.findall(r" T (rt_\w+)$", nm, flags=re.M))
@@ -144,6 +144,7 @@ def test_argument_errors_without_device(rt):
     assert L.rt_present_rgba8(None, None, None, 8, 8, 0, None) == 6
     assert L.rt_set_frames_per_launch(None, 4) == 6
     assert L.rt_set_frame_pairs(None, 0) == 6
+    assert L.rt_set_tile_order(None, 0) == 6
     assert L.rt_get_frames_per_launch(None, None, None) == 6
     assert L.rt_selftest_fastmath(None, 0, None) == 6
 

@@ -1,7 +1,7 @@
 """Per-rank frame time of the stripe partition on ONE GPU (diagnostic, not the bench): times
 rank 0's share of a W x H progressive render for world sizes 1, 2, 4, 8, i.e. what each rank
 of `bench.py --gpus N` computes per step, to predict strong-scaling efficiency without an
-8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] python tools/rank_sim.py [K3|K2|K5] [steps]"""
+8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] python tools/rank_sim.py [K3|K2|K5] [steps]"""
 import json
 import sys
 from pathlib import Path
@@ -20,22 +20,25 @@ CONF = {"K2": (1920, 1080, rt.SCENE_THREE, 3, 1), "K3": (1920, 1080, rt.SCENE_N,
 def main(cfg="K3", steps=50):
     w, h, kind, n, depth = CONF[cfg]
     sc = rt.SphereCollection.generate(kind, n, 1)
-    seeds = rt.frame_seeds(0x5EED, steps + 5)
+    seeds = rt.frame_seeds(0x5EED, steps + 69)
     settings = rt.CameraSettings(max_depth=depth, samples_per_pixel=1000)
     cam = rt.SceneCamera.from_settings(settings, w, h, float(seeds[0]))
     pipe = rt.ComputeShaderPipeline(0)
     pipe.set_spheres(sc)
     import os
     pipe.set_frame_pairs(os.environ.get("RT_FRAME_PAIRS", "auto"))
+    if hasattr(rt._lib.lib(), "rt_set_tile_order"):
+        pipe.set_tile_order(os.environ.get("RT_TILE_ORDER", "auto"))
     base = None
     for world in (1, 2, 4, 8):
         r = StripeRenderer(pipe, w, h, 0, world)
         r.frames(cam, sc, seeds[:5])                       # reset frame + warmup
         cam_t = cam.with_fields(camera_has_moved=0.0)
+        r.frames(cam_t, sc, seeds[5:69])                   # (tile costs of a long launch)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        r.frames(cam_t, sc, seeds[5:5 + steps])
+        r.frames(cam_t, sc, seeds[69:69 + steps])
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / steps

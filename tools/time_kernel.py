@@ -14,6 +14,8 @@ def main(cfg="k3", iters=40):
     pipe = rt.ComputeShaderPipeline(0)
     import os
     pipe.set_scan_mode(os.environ.get('RT_SCAN_MODE', 'culled'))
+    if hasattr(pipe, "set_tile_order") and hasattr(rt._lib.lib(), "rt_set_tile_order"):
+        pipe.set_tile_order(os.environ.get("RT_TILE_ORDER", "auto"))
     a, b = pipe.new_image(w, h), pipe.new_image(w, h)
     pipe.update(a, b, w, h, cam, sc); torch.cuda.synchronize()
     ok = hashlib.sha256(b.cpu().numpy().tobytes()).hexdigest() == str(g["sha256"]) if "sha256" in g else None
