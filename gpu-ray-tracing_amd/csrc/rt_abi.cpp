@@ -444,6 +444,7 @@ uint32_t fill_hint(rtk::TraceParams& p, uint32_t n_in) {
     for (uint32_t f = 0; f < p.frames; ++f) {
         if (f < hf) {
             p.hint_n[f] = n;
+            p.hint_rcp[f] = 1.0 / ((double)n + 1.0);
             const uint32_t B = p.seed_b[f];
             for (uint32_t i = 0; i < depth; ++i) {
                 // wgsl:268 with seed + 1 = n + B + 2 (wgsl:353, 358)

@@ -71,6 +71,9 @@ struct TraceParams {
     uint32_t* tile_cost;
     uint32_t hint_frames;  // 0 = no hint
     uint32_t hint_n[kHintFrames];
+    // RN64(1 / (hint_n[f] + 1)): the accumulator's division by f32(n + 1) as one f64
+    // multiply (rt_kernels.hip, trace_pair; exact for n + 1 <= 2^24)
+    double hint_rcp[kHintFrames];
     float4 hint_rs[kHintEntries];
     uint32_t seed_b[kMaxFramesPerLaunch];
 };

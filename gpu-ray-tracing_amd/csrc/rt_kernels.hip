@@ -200,6 +200,31 @@ constexpr bool kStoreEach = is_list_kernel(kScan);
 #ifndef RT_FAST_CORES
 #define RT_FAST_CORES 15
 #endif
+// The accumulator's division by f32(n + 1) as RN32(num * RN64(1 / (n + 1))) in the frame
+// groups, where every pixel holds the hinted count n (trace_pair: K3 16.5 against 17.3 us
+// per fused frame; the same in the one-wave loop measured +1.4 us per single-frame update,
+// from its register pressure, and is not used).
+#ifndef RT_ACC_F64
+#define RT_ACC_F64 1
+#endif
+// Exactness of acc_f64: for an integer k <= 2^24 and a quotient q = num / k in the normal
+// f32 range, q never falls on an f32 rounding midpoint (a midpoint has 25 significant bits
+// with an odd last one, so num = midpoint * k would need 25) and lies at least 2^-49
+// (relative) from every one; RN64(1 / k) and the f64 product are within 2^-52 of exact, so
+// the f64 result rounds to the same f32 as the exact quotient.  num = +-0, inf and NaN
+// pass through as in the division.  Subnormal quotients can sit exactly on a midpoint
+// (k even), so numerators in (0, 2^-102) — the only ones that give them for k <= 2^24 —
+// take the IEEE division (acc_f64_ok).  rt_selftest_fastmath replays it on random cases.
+constexpr uint32_t kBits2m102 = 0x0C800000u;   // 2^-102
+__device__ __forceinline__ bool acc_f64_ok(v3 num) {
+    // |x| >= 2^-102 or x == +-0 (NaN, inf pass): one unsigned compare per channel
+    return min(min(abs_bits(num.x) - 1u, abs_bits(num.y) - 1u), abs_bits(num.z) - 1u) >=
+           kBits2m102 - 1u;
+}
+__device__ __forceinline__ v3 acc_f64(v3 c, v3 num, double y) {
+    return mk(c.x + (float)((double)num.x * y), c.y + (float)((double)num.y * y),
+              c.z + (float)((double)num.z * y));
+}
 template <int kScan>
 constexpr bool fast_core(int bit) { return is_list_kernel(kScan) && (RT_FAST_CORES & bit) != 0; }
 
@@ -774,9 +799,15 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
 #if RT_KO & 64
                     c = col;
 #else
-                    const float k = (float)(nb + 1u);             // wgsl:356
-                    c = mk(c.x + (col.x - c.x) / k, c.y + (col.y - c.y) / k,
-                           c.z + (col.z - c.z) / k);
+                    const v3 num = sub(col, c);
+                    // num / f32(nb + 1) (wgsl:356) as RN32(num * RN64(1 / k)) (acc_f64)
+                    if (RT_ACC_F64 && nb < (1u << 24) &&
+                        __ballot(tc.valid && !acc_f64_ok(num)) == 0ull) {
+                        c = acc_f64(c, num, p.hint_rcp[fj]);
+                    } else {
+                        const float k = (float)(nb + 1u);         // wgsl:356
+                        c = mk(c.x + num.x / k, c.y + num.y / k, c.z + num.z / k);
+                    }
 #endif
                     na = nb + 1u;
                 }
@@ -1072,7 +1103,9 @@ __global__ __launch_bounds__(256) void rt_present_kernel(const float4* __restric
 // cnt[0]: defocus normalisation, all 2^32 values of hash(seed + 1): fast vs IEEE bits.
 // cnt[1]: div_core_signed vs a / b on random a, b over div_core's domain (rt_device.h:
 //         |b| in [2^-20, 2^33), |a| in [2^-100, 2^91), exponent gap in [-120, 88]; a also
-//         +-0, b also the accumulator's n + 1 up to 2^32) and over [2^-40, 2^40]^2.
+//         +-0, b also the accumulator's n + 1 up to 2^32) and over [2^-40, 2^40]^2; and
+//         acc_f64 vs the division for numerators acc_f64_ok accepts (any f32 bits, many
+//         near the subnormal range) and k in [1, 2^24].
 // cnt[2]: sqrt_core vs sqrtf on every finite x >= 2^-96 (exhaustive).
 // cnt[3]: consider_fast vs consider (root selection, tmax and index) on random rays and
 //         spheres of the camera-ray domain (|d|^2 in [2^-11, 2^20], |O|, |C| + |R| <= 2^39),
@@ -1158,7 +1191,19 @@ __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cn
         if ((r2 & 0x380000u) == 0)                    // n + 1 counts, n < 2^32 - 1
             b = (float)((r2 & 0x400000u) ? 1u + (r1 & 0xFFFFFFu) : max(r1, 1u));
         bad1 += !same_bits(div_core_signed(a, b, rcp_refined(b)), a / b);
-        bad3 += !root_case(i);
+        // the accumulator's f64-reciprocal division: any f32 numerator (r0's bits: zeros,
+        // subnormals, inf, NaN included), k = f32(n + 1) for n + 1 in [1, 2^24]
+        const uint32_t kk = (r2 & 0x800000u) ? 1u + (r1 & 0xFFFFFFu)
+                                             : 1u + (r1 % 4096u);   // small counts too
+        const v3 num = mk(__uint_as_float(r0), __uint_as_float(r0 ^ r1),
+                          __uint_as_float(r2 & 0x83FFFFFFu));       // (many tiny ones)
+        if (acc_f64_ok(num)) {
+            const float kf = (float)kk;
+            const v3 c0 = mk(0.0f, 0.0f, 0.0f);
+            const v3 q = acc_f64(c0, num, 1.0 / (double)kk);
+            bad1 += !same_bits(q.x, 0.0f + num.x / kf) || !same_bits(q.y, 0.0f + num.y / kf) ||
+                    !same_bits(q.z, 0.0f + num.z / kf);
+        }
         ++runs;
     }
     atomicAdd(&cnt[0], bad0);
