@@ -86,6 +86,14 @@ __device__ __forceinline__ void wave_trace(int end) {
 #define WAVE_TRACE(e) ((void)0)
 #endif
 
+// Constant address space (read-only for the whole launch; eligible for scalar loads).
+// (The host pass of hipcc also parses device code; there the qualifier is dropped.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define kconst __attribute__((address_space(4)))
+#else
+#define kconst
+#endif
+
 struct Hit {
     int idx;     // winning sphere, -1 = miss
     float t;     // its root
@@ -228,8 +236,19 @@ __device__ __forceinline__ v3 acc_f64(v3 c, v3 num, double y) {
 template <int kScan>
 constexpr bool fast_core(int bit) { return is_list_kernel(kScan) && (RT_FAST_CORES & bit) != 0; }
 
-// kFast: camera rays in the host-proven domain (consider_fast).
-template <int K, bool kFast = false>
+// Scan records are read through the constant address space: they do not change during a
+// launch, and only then may the compiler use scalar loads (s_load_dwordx8/16 into SGPRs)
+// in kernels that store images inside the frame loop.  (The single-frame list instance
+// keeps vector loads: its SGPRs are short, scalar records measured +0.6 us per update.)
+template <bool kScalar>
+__device__ __forceinline__ float4 load_rec(const float4* __restrict__ geom, uint32_t i) {
+    if (kScalar) return ((const kconst float4*)geom)[i];
+    return geom[i];
+}
+
+// kFast: camera rays in the host-proven domain (consider_fast).  kScalar: read the records
+// through the constant address space (below).
+template <int K, bool kFast = false, bool kScalar = true>
 __device__ __forceinline__ Hit scan_exhaustive(const float4* __restrict__ geom, uint32_t count,
                                                v3 o, v3 d) {
     float tmax = 0x1.05ed2ep+118f;             // 3.4e35 (wgsl:266)
@@ -242,11 +261,11 @@ __device__ __forceinline__ Hit scan_exhaustive(const float4* __restrict__ geom, 
     // never accepted (consider() is only called for indices < count).
     float4 cur[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) cur[k] = geom[k];
+    for (int k = 0; k < K; ++k) cur[k] = load_rec<kScalar>(geom, k);
     for (uint32_t i = 0; i < count; i += K) {
         float4 nxt[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) nxt[k] = geom[i + K + k];
+        for (int k = 0; k < K; ++k) nxt[k] = load_rec<kScalar>(geom, i + K + k);
         float hh[K], dd[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) dd[k] = discriminant(cur[k], o, d, a, hh[k]);
@@ -538,7 +557,7 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
         // (one inlined walk for both pointers: two copies measured slower)
         const Hit hit =
             (kScan != kTraceCulled || listed)
-                ? scan_exhaustive<scan_chunk<kScan>(), fast_core<kScan>(1)>(
+                ? scan_exhaustive<scan_chunk<kScan>(), fast_core<kScan>(1), kScan != kTraceList>(
                       listed ? p.cand_rec + lbase : p.geom, listed ? ncand : p.count, o, d)
             : p.lds_records ? scan_culled<true>(p.geom, p.count, o, d, live)
                             : scan_culled<false>(p.geom, p.count, o, d, live);
@@ -884,7 +903,9 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) RT_TRAC
     uint32_t lband = blockIdx.y;
     if (kOrdered<kScan> && p.tile_order) {            // costliest tiles first
         const uint32_t slot = blockIdx.y * gridDim.x + blockIdx.x;
-        const uint32_t t = p.tile_order[slot];
+        // (readfirstlane: the loaded value is uniform, but only the scalar form keeps the
+        // list pointer and records in SGPRs — s_load chunks instead of vector loads)
+        const uint32_t t = __builtin_amdgcn_readfirstlane(p.tile_order[slot]);
         tx = t & 0xFFFFu;
         lband = t >> 16;
 #if RT_TILE_PRIO
