@@ -21,14 +21,17 @@ def padded_rows(height: int, world: int) -> int:
 
 
 def gather_stripes(local: torch.Tensor, world: int, rank: int, dst: int = 0,
-                   group=None) -> torch.Tensor | None:
-    """Gather equal-shaped (rows0, W, 4) tiles to `dst` as one (world*rows0, W, 4) tensor.
+                   group=None, out: torch.Tensor | None = None) -> torch.Tensor | None:
+    """Gather equal-shaped (rows0, W, 4) tiles to `dst` as one (world*rows0, W, 4) tensor
+    (into `out`, shaped (world, rows0, W, 4), when given).
 
     One collective (dist.gather; RCCL on GPU, gloo on CPU)."""
     if world == 1:
         return local
     if rank == dst:
-        out = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        if out is None:
+            out = torch.empty((world,) + tuple(local.shape), dtype=local.dtype,
+                              device=local.device)
         dist.gather(local, gather_list=list(out.unbind(0)), dst=dst, group=group)
         return out.reshape((world * local.shape[0],) + tuple(local.shape[1:]))
     dist.gather(local, gather_list=None, dst=dst, group=group)
@@ -47,6 +50,14 @@ class StripeRenderer:
         # ping-pong local accumulators, padded to rows0 so the gather is uniform
         self.buf = [pipeline.new_image(width, self.rows0), pipeline.new_image(width, self.rows0)]
         self.cur = 0
+        # the root's gather and output buffers, allocated up front (finish() then runs only
+        # the collective and the de-interleave kernel)
+        self._gathered = self._image = None
+        if world > 1 and rank == 0:
+            dev = self.buf[0].device
+            self._gathered = torch.empty((world, self.rows0, width, 4), dtype=torch.float32,
+                                         device=dev)
+            self._image = torch.empty((height, width, 4), dtype=torch.float32, device=dev)
 
     def frame(self, camera, spheres, seeds) -> None:
         """One progressive `update` (or len(seeds) fused frames) over this rank's bands."""
@@ -79,9 +90,13 @@ class StripeRenderer:
         """Gather the finished tiles; returns the full image on `dst`, None elsewhere."""
         if self.world == 1:
             return self.local[: self.height]
-        gathered = gather_stripes(self.local, self.world, self.rank, dst, group)
+        pre = dst == 0 and self._gathered is not None
+        gathered = gather_stripes(self.local, self.world, self.rank, dst, group,
+                                  out=self._gathered if pre else None)
         if gathered is None:
             return None
-        out = self.pipe.new_image(self.width, self.height)
+        # (the de-interleave writes every pixel: no zero fill needed)
+        out = self._image if pre else torch.empty((self.height, self.width, 4),
+                                                  dtype=torch.float32, device=gathered.device)
         self.pipe.deinterleave(gathered, out, self.width, self.height, self.world)
         return out
