@@ -621,7 +621,8 @@ rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launch) {
 
 rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
-    if (mode != RT_FRAME_PAIRS_AUTO && mode != RT_FRAME_PAIRS_OFF && mode != RT_FRAME_PAIRS_ON)
+    if (mode != RT_FRAME_PAIRS_AUTO && mode != RT_FRAME_PAIRS_OFF && mode != RT_FRAME_PAIRS_ON &&
+        mode != RT_FRAME_PAIRS_QUAD)
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown frame-pair mode");
     ctx->frame_pairs = mode;
     return RT_OK;
@@ -737,7 +738,13 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         int kernel = trace_kernel_for(ctx, p);
         const bool pairable = kernel == rtk::kTraceList && p.store_each && known &&
                               p.hint_frames == nf;
-        if (pairable && ctx->frame_pairs != RT_FRAME_PAIRS_OFF) kernel = rtk::kTraceListPair;
+        if (pairable && ctx->frame_pairs != RT_FRAME_PAIRS_OFF) {
+            // AUTO: four waves per tile when the share is small (a few tiles per SIMD)
+            const uint64_t tiles = (uint64_t)((w + 7u) >> 3) * p.local_bands;
+            const bool quad = ctx->frame_pairs == RT_FRAME_PAIRS_QUAD ||
+                              (ctx->frame_pairs == RT_FRAME_PAIRS_AUTO && tiles <= rtk::kQuadMaxTiles);
+            kernel = quad ? rtk::kTraceListQuad : rtk::kTraceListPair;
+        }
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");

@@ -87,7 +87,13 @@ constexpr int kTraceList = 2;
 // Camera-ray-only, two waves per tile tracing alternate frames (rt_update_frames on small
 // per-rank images; see rt_kernels.hip, trace_pair).
 constexpr int kTraceListPair = 3;
-constexpr bool is_list_kernel(int k) { return k == kTraceList || k == kTraceListPair; }
+// The same with four waves per tile: for small per-rank shares (few tiles per SIMD), where
+// shorter per-wave frame chains keep more waves resident (rt_abi.cpp picks it).
+constexpr int kTraceListQuad = 4;
+constexpr bool is_group_kernel(int k) { return k == kTraceListPair || k == kTraceListQuad; }
+constexpr bool is_list_kernel(int k) { return k == kTraceList || is_group_kernel(k); }
+// Tiles per launch at or below which frame groups of four are used.
+constexpr uint64_t kQuadMaxTiles = 6144;
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream);
 hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream);
 // Builds the per-tile candidate lists for p's camera/scene/stripes (p.cand_k slots each).

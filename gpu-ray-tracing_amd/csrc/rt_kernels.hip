@@ -778,10 +778,10 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 // bit-identical to one wave doing every frame.  More waves, each with a shorter sequential
 // chain: 22.2 vs 24.0 µs per K3 frame on one GPU, 3.3 vs 4.3 µs for an 8-rank share.
 // Called only when every valid pixel's loaded count is the hinted one (rt_trace_kernel).
-#ifndef RT_FRAME_GROUP
-#define RT_FRAME_GROUP 2   // 2 / 4: K3 19.7 / 20.5 us per frame, 8-rank share 3.36 / 3.45
-#endif
-constexpr uint32_t kFrameGroup = RT_FRAME_GROUP;
+// Waves per tile: 2 (kTraceListPair) or 4 (kTraceListQuad).  K3 per frame, whole image on
+// one GPU: 16.8 / 18.8 us; 8-rank share: 3.13 / 2.95 us (`profiles/r01_rank_sim_groups_k3.txt`).
+template <int kScan>
+constexpr uint32_t frame_group() { return kScan == kTraceListQuad ? 4u : 2u; }
 template <int kScan>
 __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam, uint32_t tile,
                                            uint32_t ncand, const TileCoord& tc, uint32_t hxy,
@@ -792,6 +792,7 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
     // From here every valid pixel holds hint_n[f] before frame f (the host's count
     // bookkeeping, rt_abi.cpp fill_hint): the count arithmetic of wgsl:341-362 is scalar.
     const uint32_t lane = threadIdx.x & 63u;
+    constexpr uint32_t kFrameGroup = frame_group<kScan>();
     for (uint32_t f = 0; f < p.frames; f += kFrameGroup) {
         const uint32_t fw = f + w;
         v3 col = mk(0.0f, 0.0f, 0.0f);
@@ -861,7 +862,7 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
 #endif
 template <int kScan>
 constexpr uint32_t wg_waves() {
-    return kScan == kTraceCulled ? 4u : kScan == kTraceListPair ? kFrameGroup : RT_WG_WAVES;
+    return kScan == kTraceCulled ? 4u : is_group_kernel(kScan) ? frame_group<kScan>() : RT_WG_WAVES;
 }
 
 
@@ -872,7 +873,7 @@ constexpr uint32_t wg_waves() {
 #endif
 template <int kScan>
 constexpr bool kOrdered =
-    is_list_kernel(kScan) && (kScan == kTraceListPair || wg_waves<kScan>() == 1u);
+    is_list_kernel(kScan) && (is_group_kernel(kScan) || wg_waves<kScan>() == 1u);
 // (the start time is parked in tile_cost itself: no register stays live for it)
 template <int kScan>
 __device__ __forceinline__ void cost_start(const TraceParams& p, uint32_t tile, uint32_t wave,
@@ -899,7 +900,7 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) RT_TRAC
     // it) scalar, so list records are read with s_load into SGPRs.
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // (frame groups: all waves of the workgroup own the same tile)
-    uint32_t tx = kScan == kTraceListPair ? blockIdx.x : blockIdx.x * wg_waves<kScan>() + wave;
+    uint32_t tx = is_group_kernel(kScan) ? blockIdx.x : blockIdx.x * wg_waves<kScan>() + wave;
     uint32_t lband = blockIdx.y;
     if (kOrdered<kScan> && p.tile_order) {            // costliest tiles first
         const uint32_t slot = blockIdx.y * gridDim.x + blockIdx.x;
@@ -957,7 +958,7 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) RT_TRAC
     cam.ddv = mk(p.ddv[0], p.ddv[1], p.ddv[2]);
     cam.defocus_angle = p.defocus_angle;
 
-    if (kScan == kTraceListPair) {
+    if (is_group_kernel(kScan)) {
         // every frame's image is stored inside; on a count mismatch (every wave sees the
         // same pixels, hence takes the same decision) wave 0 runs the single-wave loop and
         // the others have nothing to do
@@ -969,7 +970,7 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) RT_TRAC
         }
         if (wave != 0u) return;
     }
-    const float4 res = trace_pixel<kScan, kScan != kTraceListPair>(p, cam, tile, ncand, tc,
+    const float4 res = trace_pixel<kScan, !is_group_kernel(kScan)>(p, cam, tile, ncand, tc,
                                                                    hxy, acc);
 #if RT_KO & 16
     if (res.x == 12345.678f) p.out[tc.idx] = res;
@@ -1248,7 +1249,7 @@ static dim3 tile_grid(const TraceParams& p, uint32_t waves = 4) {
 template <int kScan>
 static void launch_trace_as(const TraceParams& p, size_t lds, hipStream_t stream) {
     constexpr uint32_t w = wg_waves<kScan>();
-    const dim3 grid = tile_grid(p, kScan == kTraceListPair ? 1u : w);
+    const dim3 grid = tile_grid(p, is_group_kernel(kScan) ? 1u : w);
     if (grid.x == 0 || grid.y == 0) return;
     hipLaunchKernelGGL(rt_trace_kernel<kScan>, grid, dim3(64 * w), lds, stream, p);
 }
@@ -1259,7 +1260,11 @@ hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
     else if (kernel == kTraceList)
         launch_trace_as<kTraceList>(p, 0, stream);
     else if (kernel == kTraceListPair)
-        launch_trace_as<kTraceListPair>(p, (kFrameGroup - 1) * 64 * sizeof(float4), stream);
+        launch_trace_as<kTraceListPair>(p, (frame_group<kTraceListPair>() - 1) * 64 *
+                                               sizeof(float4), stream);
+    else if (kernel == kTraceListQuad)
+        launch_trace_as<kTraceListQuad>(p, (frame_group<kTraceListQuad>() - 1) * 64 *
+                                               sizeof(float4), stream);
     else
         launch_trace_as<kTraceExhaustive>(p, 0, stream);
     return hipGetLastError();

@@ -69,8 +69,10 @@ class ComputeShaderPipeline:
         _lib.call("rt_set_frames_per_launch", self._ctx, int(n))
 
     def set_frame_pairs(self, mode: str) -> None:
-        """rt_set_frame_pairs: 'auto' | 'off' | 'on' (two waves per tile, alternate frames)."""
-        _lib.call("rt_set_frame_pairs", self._ctx, {"auto": 0, "off": 1, "on": 2}[mode])
+        """rt_set_frame_pairs: 'auto' | 'off' | 'on' (two waves per tile, alternate frames)
+        | 'quad' (four waves per tile)."""
+        _lib.call("rt_set_frame_pairs", self._ctx,
+                  {"auto": 0, "off": 1, "on": 2, "quad": 3}[mode])
 
     def set_tile_order(self, mode: str) -> None:
         """rt_set_tile_order: "auto" (costliest tiles first, from the first launch's

@@ -183,12 +183,14 @@ RT_API rt_status rt_render(rt_ctx* ctx, const float* in_rgba, float* out_rgba, u
 RT_API rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launch);
 /* rt_update_frames at max_depth <= 1 traces with several waves per 8x8 tile, each taking
  * a different frame of each group of frames (the others hand their colours to wave 0,
- * which accumulates and stores every frame in order: the same bits).  AUTO (default) and
- * ON do so whenever every pixel holds the sample count the context expects (otherwise the
- * launch falls back to one wave per tile); OFF always uses one wave per tile. */
+ * which accumulates and stores every frame in order: the same bits), whenever every pixel
+ * holds the sample count the context expects (otherwise the launch falls back to one wave
+ * per tile).  AUTO (default): 2 waves per tile, 4 for launches of at most 6144 tiles (small
+ * per-rank shares); ON: 2; QUAD: 4; OFF: one wave per tile. */
 #define RT_FRAME_PAIRS_AUTO 0
 #define RT_FRAME_PAIRS_OFF 1
 #define RT_FRAME_PAIRS_ON 2
+#define RT_FRAME_PAIRS_QUAD 3
 RT_API rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode);
 /* Tile scheduling of the fused multi-frame launches of the camera-ray-only kernels
  * (max_depth <= 1, culled scan mode).  AUTO (default): the first such launch for a camera

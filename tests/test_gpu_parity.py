@@ -399,7 +399,7 @@ def test_candidate_list_overflow_falls_back(rt, depth):
                                                   (7, 1, 4, 0), (4, 1, 500, 1), (6, 3, 500, 4),
                                                   (5, 8, 500, 4), (9, 2, 3, 3), (14, 1, 500, 4),
                                                   (11, 1, 6, 3)])
-@pytest.mark.parametrize("pairs", ["off", "on"])
+@pytest.mark.parametrize("pairs", ["off", "on", "quad"])
 def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, spp, per, pairs):
     """rt_update_frames (frames fused per launch, every frame's image stored to the
     ping-pong buffers; or one dispatch per frame) leaves BOTH buffers exactly as chained
@@ -550,7 +550,7 @@ def test_hinted_chain_matches_oracle(rt, oracle, pipe, depth, spp):
         assert_same(host(cur), ref)
 
 
-@pytest.mark.parametrize("pairs", ["off", "on"])
+@pytest.mark.parametrize("pairs", ["off", "on", "quad"])
 def test_update_frames_with_foreign_counts(rt, oracle, pipe, pairs):
     """rt_update_frames on an image whose counts the library did not write (mixed per-pixel
     counts behind its back, after init_image): the hinted / frame-pair launch falls back to
