@@ -868,9 +868,7 @@ constexpr uint32_t wg_waves() {
 
 // Cost-ordered tiles (TraceParams::tile_order / tile_cost) in the camera-ray-only
 // instances, whose workgroups are one tile each.
-#ifndef RT_TILE_PRIO
-#define RT_TILE_PRIO 0
-#endif
+
 template <int kScan>
 constexpr bool kOrdered =
     is_list_kernel(kScan) && (is_group_kernel(kScan) || wg_waves<kScan>() == 1u);
@@ -909,13 +907,6 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) RT_TRAC
         const uint32_t t = __builtin_amdgcn_readfirstlane(p.tile_order[slot]);
         tx = t & 0xFFFFu;
         lband = t >> 16;
-#if RT_TILE_PRIO
-        // the costliest quarter of the tiles issues first on a shared SIMD
-        const uint32_t q = slot * 4u / (gridDim.x * gridDim.y);
-        if (q == 0u) __builtin_amdgcn_s_setprio(3);
-        else if (q == 1u) __builtin_amdgcn_s_setprio(2);
-        else if (q == 2u) __builtin_amdgcn_s_setprio(1);
-#endif
     }
     const bool wave_in = tx < tiles_x;
     const TileCoord tc = tile_coord(p, tx, lband, lane);
