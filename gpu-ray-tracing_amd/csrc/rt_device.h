@@ -75,7 +75,8 @@ RT_HD void sincos_c(float x, float& s, float& c) {
 // wgsl:234-243; rf_seed = rf(seed)
 RT_HD v3 random_unit_vector(float rf_seed, uint32_t seed) {
     const float z = fmaf(2.0f, rf_seed, -1.0f);
-    const float a = rf(seed + 1u) * 0x1.921fb6p+2f;  // 6.283185307 as f32
+    // rf(seed + 1) * 6.283185307f in one rounding (the 2^-32 scale of rf is exact)
+    const float a = (float)hash(seed + 1u) * 0x1.921fb6p-30f;
     const float r = sqrtf(fmaf(-z, z, 1.0f));
     float sa, ca;
     sincos_c(a, sa, ca);

@@ -483,13 +483,16 @@ struct Cam {
 __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, uint32_t hxy,
                                         uint32_t su, v3& o, v3& d) {
     const uint32_t seed = hash(hxy ^ su);
-    const float offx = rf(seed) - 0.5f;                 // sample_square wgsl:299-303
-    const float offy = rf(seed * seed) - 0.5f;
+    // rf(v) = f32(hash(v)) * 2^-32 is exact (a power-of-two scale of a value >= 1 or 0), so
+    // the next rounding is the only one: rf - 0.5 is one fma, 2pi * rf one multiply by
+    // 2pi * 2^-32 — the same bits as the two-step forms.
+    const float offx = fmaf((float)hash(seed), 0x1p-32f, -0.5f);         // sample_square
+    const float offy = fmaf((float)hash(seed * seed), 0x1p-32f, -0.5f);  // wgsl:299-303
     const float sx = ((float)x + 0.5f) + offx;
     const float sy = ((float)y + 0.5f) + offy;
     const v3 pc = fmas(sy, cam.pdv, fmas(sx, cam.pdu, cam.vul));
     if (cam.defocus_angle > 0.0f) {                     // defocus_disk_sample wgsl:327-331
-        const float ang = 0x1.921fb4p+2f * rf(seed + 1u);  // 2.0*3.1415926 as f32
+        const float ang = (float)hash(seed + 1u) * 0x1.921fb4p-30f;  // 2*3.1415926 * rf
         float sa, ca;
         sincos_c(ang, sa, ca);
         // normalize((ca, sa)): over all 2^32 values of hash(seed + 1), len2 lies in
