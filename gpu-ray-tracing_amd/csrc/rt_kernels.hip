@@ -202,11 +202,11 @@ constexpr bool kStoreEach = is_list_kernel(kScan);
 // rt_abi.cpp selects only for cameras and scenes inside the proven domain
 // (camera_rays_bounded): bit 1 the roots of the scan, 2 the normal, 4 the sky, 8 the
 // metal / dielectric normalisations (the last three behind a wave-wide check of their
-// operands).  K3 per frame (fused): 21.7 us without, 20.9 / 20.1 / 20.1 us with bits
+// operands), 16 the defocus disk's reciprocal table (disk_unit).  K3 per frame (fused): 21.7 us without, 20.9 / 20.1 / 20.1 us with bits
 // 1 / 1-2 / 1-4; the accumulator's three divisions by f32(n + 1) the same way (checked
 // numerators in [2^-88, 2^88)) measured +0.75 us and are left to the compiler.
 #ifndef RT_FAST_CORES
-#define RT_FAST_CORES 15
+#define RT_FAST_CORES 31
 #endif
 // The accumulator's division by f32(n + 1) as RN32(num * RN64(1 / (n + 1))) in the frame
 // groups, where every pixel holds the hinted count n (trace_pair: K3 16.5 against 17.3 us
@@ -477,9 +477,38 @@ struct Cam {
     float defocus_angle;
 };
 
+// The defocus disk's normalize((cos, sin)) (wgsl:327-331).  Over all 2^32 values of
+// hash(seed + 1), len2 = sa^2 + ca^2 takes only the eight f32 values of
+// [1 - 6*2^-24, 1 + 2^-23], |sa| >= 2^-30 or sa == +0 and |ca| >= 2^-27 (checked
+// exhaustively by rt_selftest_fastmath).  kTable: 1 / sqrtf(len2) has eight values;
+// s_disk_rcp holds them as RN64(1 / len) (each workgroup fills it, init_disk_rcp), and
+// ca / len = RN32(ca * RN64(1 / len)) — the f64-reciprocal division of acc_f64, exact for
+// normal quotients and zeros.  Otherwise sqrt_core / div_core, also exact on this domain.
+__shared__ double s_disk_rcp[8];
+constexpr uint32_t kDiskLen2Lo = 0x3F7FFFFAu;   // 1 - 6 * 2^-24
+__device__ __forceinline__ void init_disk_rcp() {
+    if (threadIdx.x < 8u)
+        s_disk_rcp[threadIdx.x] = 1.0 / (double)sqrtf(__uint_as_float(kDiskLen2Lo + threadIdx.x));
+}
+template <bool kTable>
+__device__ __forceinline__ void disk_unit(float sa, float ca, float& ux, float& uy) {
+    const float len2 = fmaf(sa, sa, ca * ca);
+    if (kTable) {
+        const double y = s_disk_rcp[__float_as_uint(len2) - kDiskLen2Lo];
+        ux = (float)((double)ca * y);
+        uy = (float)((double)sa * y);
+    } else {
+        const float len = sqrt_core(len2);
+        const float y = rcp_refined(len);
+        ux = div_core(ca, len, y);
+        uy = div_core(sa, len, y);
+    }
+}
+
 // get_ray (wgsl:305-325) with the pixel-invariant hash(hash(x*73) ^ hash(y*51)) part
 // precomputed per pixel: seed = hash(hxy ^ su), su = sample_index*25 + B (wave-uniform
 // when every pixel of the wave holds the same sample count).
+template <bool kTable>
 __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, uint32_t hxy,
                                         uint32_t su, v3& o, v3& d) {
     const uint32_t seed = hash(hxy ^ su);
@@ -493,20 +522,10 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
     const v3 pc = fmas(sy, cam.pdv, fmas(sx, cam.pdu, cam.vul));
     if (cam.defocus_angle > 0.0f) {                     // defocus_disk_sample wgsl:327-331
         const float ang = (float)hash(seed + 1u) * 0x1.921fb4p-30f;  // 2*3.1415926 * rf
-        float sa, ca;
+        float sa, ca, ux, uy;
         sincos_c(ang, sa, ca);
-        // normalize((ca, sa)): over all 2^32 values of hash(seed + 1), len2 lies in
-        // [1 - 6*2^-24, 1 + 2^-23], |sa| >= 2^-30 or sa == +0, |ca| >= 2^-27 (checked
-        // exhaustively, tests/test_gpu_parity.py::test_fastmath_selftest), inside the exact
-        // domain of sqrt_core / div_core: the same bits as sqrtf and the two IEEE divides.
-#ifdef RT_DEFOCUS_IEEE
-        const float len = sqrtf(fmaf(sa, sa, ca * ca));
-        o = fmas(sa / len, cam.ddv, fmas(ca / len, cam.ddu, cam.center));
-#else
-        const float len = sqrt_core(fmaf(sa, sa, ca * ca));
-        const float y = rcp_refined(len);
-        o = fmas(div_core(sa, len, y), cam.ddv, fmas(div_core(ca, len, y), cam.ddu, cam.center));
-#endif
+        disk_unit<kTable>(sa, ca, ux, uy);
+        o = fmas(uy, cam.ddv, fmas(ux, cam.ddu, cam.center));
     } else {
         o = cam.center;
     }
@@ -704,7 +723,7 @@ __device__ __forceinline__ v3 sample(const TraceParams& p, const Cam& cam, uint3
     o = cam.center;
     d = sub(fmas((float)tc.y, cam.pdv, fmas((float)tc.x, cam.pdu, cam.vul)), o);
 #else
-    get_ray(cam, tc.x, tc.y, hxy, seed * 25u + B, o, d);          // wgsl:311
+    get_ray<fast_core<kScan>(16)>(cam, tc.x, tc.y, hxy, seed * 25u + B, o, d);   // wgsl:311
 #endif
     STAMP(1);
     const v3 col = ray_color<kScan>(p, tile, ncand, depth, o, d, seed + 1u, live, uni, f);
@@ -924,6 +943,10 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) RT_TRAC
         }
         __syncthreads();
     }
+    if (fast_core<kScan>(16)) {                                   // (disk_unit)
+        init_disk_rcp();
+        __syncthreads();
+    }
     if (!wave_in) return;                                         // whole wave exits
     const uint32_t tile = lband * tiles_x + tx;
     cost_start<kScan>(p, tile, wave, lane);
@@ -1116,7 +1139,8 @@ __global__ __launch_bounds__(256) void rt_present_kernel(const float4* __restric
 }
 
 // ---- Self-test of the exact fast paths (rt_selftest_fastmath) ------------------------
-// cnt[0]: defocus normalisation, all 2^32 values of hash(seed + 1): fast vs IEEE bits.
+// cnt[0]: defocus normalisation, all 2^32 values of hash(seed + 1): both disk_unit forms vs
+//         sqrtf and the IEEE divisions (also the eight-value range of len2 the table needs).
 // cnt[1]: div_core_signed vs a / b on random a, b over div_core's domain (rt_device.h:
 //         |b| in [2^-20, 2^33), |a| in [2^-100, 2^91), exponent gap in [-120, 88]; a also
 //         +-0, b also the accumulator's n + 1 up to 2^32) and over [2^-40, 2^40]^2; and
@@ -1173,6 +1197,8 @@ __device__ __forceinline__ bool root_case(uint64_t i) {
     return same_bits(t1, t2) && i1 == i2;
 }
 __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cnt, uint64_t n_rand) {
+    init_disk_rcp();
+    __syncthreads();
     unsigned long long bad0 = 0, bad1 = 0, bad2 = 0, bad3 = 0, runs = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32);
@@ -1181,10 +1207,14 @@ __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cn
         float sa, ca;
         sincos_c(ang, sa, ca);
         const float len_ref = sqrtf(fmaf(sa, sa, ca * ca));
-        const float len = sqrt_core(fmaf(sa, sa, ca * ca));
-        const float y = rcp_refined(len);
-        bad0 += (__float_as_uint(div_core(sa, len, y)) != __float_as_uint(sa / len_ref)) ||
-                (__float_as_uint(div_core(ca, len, y)) != __float_as_uint(ca / len_ref));
+        const float ux_ref = ca / len_ref, uy_ref = sa / len_ref;
+        float ux, uy, tx, ty;
+        disk_unit<false>(sa, ca, ux, uy);
+        disk_unit<true>(sa, ca, tx, ty);
+        bad0 += (__float_as_uint(ux) != __float_as_uint(ux_ref)) ||
+                (__float_as_uint(uy) != __float_as_uint(uy_ref)) ||
+                (__float_as_uint(tx) != __float_as_uint(ux_ref)) ||
+                (__float_as_uint(ty) != __float_as_uint(uy_ref));
         const float x = __uint_as_float((uint32_t)i);
         if ((uint32_t)i >= 0x0F800000u && (uint32_t)i < 0x7F800000u)   // [2^-96, +inf)
             bad2 += __float_as_uint(sqrt_core(x)) != __float_as_uint(sqrtf(x));
