@@ -30,9 +30,10 @@ constexpr uint32_t kHintEntries = RT_HINT_FRAMES;
 struct TraceParams {
     const float4* in;    // local image (compact stripes), row pitch = width
     float4* out;
-    // store_each (rt_update_frames): every frame f of the launch stores its image, to out
-    // for even f and to out2 (the input buffer) for odd f — the ping-pong of chained
-    // `update` dispatches (lib.rs:366-374), with the accumulator kept in registers.
+    // store_each (rt_update_frames): frame f of the launch stores its image to out for
+    // even f and to out2 (the input buffer) for odd f — the ping-pong of chained `update`
+    // dispatches (lib.rs:366-374), with the accumulator kept in registers.  Only the last
+    // two frames' images survive the launch, so only they are written.
     float4* out2;
     uint32_t store_each;
     const float4* geom;  // per sphere: (cx, cy, cz, r*r) — the scan's 16-B record

@@ -784,8 +784,10 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
         }
         // Chained updates: frame f's image (wgsl:362-363) lands in the other ping-pong
         // buffer; the next frame would read it back (u32(f32(n)), wgsl:341) — here the
-        // registers already hold it.
-        if (kStoreEach<kScan> && p.store_each && tc.valid)
+        // registers already hold it.  Only the last two frames' images survive the launch
+        // (each buffer keeps the last frame written to it, and nothing reads a tile's
+        // pixels during the launch but its own wave), so only they are stored.
+        if (kStoreEach<kScan> && p.store_each && f + 2u >= p.frames && tc.valid)
             ((f & 1u) ? p.out2 : p.out)[tc.idx] = make_float4(c.x, c.y, c.z, (float)n);
         n = f2u((float)n);
     }
@@ -796,9 +798,9 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 // kFrameGroup waves own the same tile; wave w traces frames f + w of each group of
 // kFrameGroup frames (the samples are independent — the count each one uses is the hinted
 // n + f, verified up front), waves 1.. hand their colours to wave 0 through LDS, and wave 0
-// accumulates the group's frames in order and stores every frame's image (wgsl:352-363) —
-// bit-identical to one wave doing every frame.  More waves, each with a shorter sequential
-// chain: 22.2 vs 24.0 µs per K3 frame on one GPU, 3.3 vs 4.3 µs for an 8-rank share.
+// accumulates the group's frames in order and stores the surviving images (wgsl:352-363)
+// — bit-identical to one wave doing every frame.  More waves, each with a shorter
+// sequential chain.
 // Called only when every valid pixel's loaded count is the hinted one (rt_trace_kernel).
 // Waves per tile: 2 (kTraceListPair) or 4 (kTraceListQuad).  K3 per frame, whole image on
 // one GPU: 16.8 / 18.8 us; 8-rank share: 3.13 / 2.95 us (`profiles/r01_rank_sim_groups_k3.txt`).
@@ -853,8 +855,9 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
 #endif
                     na = nb + 1u;
                 }
-                if (tc.valid)                                     // wgsl:362-363
-                    ((fj & 1u) ? p.out2 : p.out)[tc.idx] = make_float4(c.x, c.y, c.z, (float)na);
+                if (fj + 2u >= p.frames && tc.valid)              // wgsl:362-363 (the
+                    ((fj & 1u) ? p.out2 : p.out)[tc.idx] =        // images that survive)
+                        make_float4(c.x, c.y, c.z, (float)na);
             }
         }
         __syncthreads();

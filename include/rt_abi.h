@@ -176,14 +176,15 @@ RT_API rt_status rt_render(rt_ctx* ctx, const float* in_rgba, float* out_rgba, u
  * (the newest frame and the one before).  Frames run in launches of
  * rt_set_frames_per_launch frames (default: 64 at max_depth <= 1, else 1); within a
  * launch each wave carries its pixels' accumulator in registers from frame to frame and
- * stores every frame's image.  No per-frame host round trip. */
+ * writes the images of the launch's last two frames (the earlier ones would be overwritten
+ * unread).  No per-frame host round trip. */
 /* Frames rt_update_frames runs per launch at max_depth <= 1: 0 = automatic (up to 64),
  * 1 = one `update` dispatch per frame, exactly the reference's dispatch structure, n = up
  * to n (at most 128).  Launches with bounce rays always run one frame each. */
 RT_API rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launch);
 /* rt_update_frames at max_depth <= 1 traces with several waves per 8x8 tile, each taking
  * a different frame of each group of frames (the others hand their colours to wave 0,
- * which accumulates and stores every frame in order: the same bits), whenever every pixel
+ * which accumulates every frame in order: the same bits), whenever every pixel
  * holds the sample count the context expects (otherwise the launch falls back to one wave
  * per tile).  AUTO (default): 2 waves per tile, 4 for launches of at most 6144 tiles (small
  * per-rank shares); ON: 2; QUAD: 4; OFF: one wave per tile. */
