@@ -46,8 +46,10 @@ struct rt_ctx {
     uint32_t* tile_cost = nullptr;
     uint32_t* tile_order = nullptr;
     uint64_t order_tiles = 0;       // allocated tiles
-    uint64_t order_gen = ~0ull;     // cand_gen the order was measured for
-    uint32_t order_frames = 0;      // frames of the launch that measured it
+    uint64_t cost_gen = ~0ull;      // cand_gen tile_cost was measured for
+    uint32_t cost_frames = 0;       // frames of the launch that measured it
+    uint64_t order_gen = ~0ull;     // cand_gen tile_order was derived for
+    uint32_t order_frames = 0;      // frames of the measurement it came from
     int tile_order_mode = RT_TILE_ORDER_AUTO;
     float* d_srgb = nullptr;  // rt_srgb_thresholds table on the device (256 floats)
     // hash(x*73) for x < hx_len and hash(y*51) for y < hy_len (wgsl:309-310)
@@ -320,11 +322,13 @@ rt_status ensure_candidates(rt_ctx* ctx, rtk::TraceParams& p, hipStream_t stream
     return RT_OK;
 }
 
-// Cost-ordered tiles for the camera-ray-only instances: the first such launch of a
-// candidate-list generation (same camera geometry, image, stripes and scene) records each
-// tile's duration; rtk::launch_tile_order then sorts the tiles by it on the stream, and
-// later launches of the generation start the costliest tiles first so that the cheap ones
-// fill the tail.  Only the workgroup -> tile assignment changes, never a pixel's result.
+// Cost-ordered tiles for the camera-ray-only instances: a fused launch of a candidate-list
+// generation (same camera geometry, image, stripes and scene) records each tile's
+// duration; the next launch of the generation first sorts the tiles by it
+// (rtk::launch_tile_order, on the stream) and then starts the costliest tiles first so
+// that the cheap ones fill the tail.  The sort runs only when a generation is reused, so a
+// camera that moves every call never pays for it.  Only the workgroup -> tile assignment
+// changes, never a pixel's result.
 rt_status plan_tile_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t stream) {
     p.tile_order = nullptr;
     p.tile_cost = nullptr;
@@ -333,13 +337,9 @@ rt_status plan_tile_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
     if (!rtk::is_list_kernel(kernel) || ctx->tile_order_mode == RT_TILE_ORDER_OFF ||
         p.cand_k == 0 || p.frames < 2)
         return RT_OK;
-    // A launch of a few frames measures mostly start-up and placement noise: launches keep
-    // re-measuring (in the current order) until one of kOrderFrames frames or more has.
-    constexpr uint32_t kOrderFrames = 16;
-    const bool have = ctx->order_gen == ctx->cand_gen;
-    if (have) p.tile_order = ctx->tile_order;
-    if (have && ctx->order_frames >= std::min(kOrderFrames, p.frames)) return RT_OK;
-    const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
+    const uint64_t gen = ctx->cand_gen;
+    const uint32_t tiles_x = (p.width + 7u) >> 3;
+    const uint64_t tiles = (uint64_t)tiles_x * p.local_bands;
     if (tiles > ctx->order_tiles) {
         if (ctx->order_tiles) {
             hipError_t e = hipStreamSynchronize(stream);   // old order may be in use
@@ -349,27 +349,35 @@ rt_status plan_tile_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
         (void)hipFree(ctx->tile_order);
         ctx->tile_cost = ctx->tile_order = nullptr;
         ctx->order_tiles = 0;
-        ctx->order_gen = ~0ull;
-        p.tile_order = nullptr;
+        ctx->cost_gen = ctx->order_gen = ~0ull;
         hipError_t e = hipMalloc(&ctx->tile_cost, tiles * sizeof(uint32_t));
         if (e == hipSuccess) e = hipMalloc(&ctx->tile_order, tiles * sizeof(uint32_t));
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(tile order)");
         ctx->order_tiles = tiles;
     }
+    // the order from the newest measurement of this generation
+    if (ctx->cost_gen == gen && (ctx->order_gen != gen || ctx->order_frames < ctx->cost_frames)) {
+        hipError_t e = rtk::launch_tile_order(ctx->tile_cost, ctx->tile_order,
+                                              (uint32_t)tiles, tiles_x, stream);
+        if (e != hipSuccess) return hip_fail(e, "rt_tile_order_kernel launch");
+        ctx->order_gen = gen;
+        ctx->order_frames = ctx->cost_frames;
+    }
+    const bool have = ctx->order_gen == gen;
+    if (have) p.tile_order = ctx->tile_order;
+    // A launch of a few frames measures mostly start-up and placement noise: launches keep
+    // re-measuring (in the current order) until one of kOrderFrames frames or more has.
+    constexpr uint32_t kOrderFrames = 16;
+    if (have && ctx->order_frames >= std::min(kOrderFrames, p.frames)) return RT_OK;
     p.tile_cost = ctx->tile_cost;
     return RT_OK;
 }
 
-// After a launch that recorded tile costs: derive the order for the next launches.
-rt_status finish_tile_order(rt_ctx* ctx, const rtk::TraceParams& p, hipStream_t stream) {
-    if (!p.tile_cost) return RT_OK;
-    const uint32_t tiles_x = (p.width + 7u) >> 3;
-    hipError_t e = rtk::launch_tile_order(p.tile_cost, ctx->tile_order,
-                                          tiles_x * p.local_bands, tiles_x, stream);
-    if (e != hipSuccess) return hip_fail(e, "rt_tile_order_kernel launch");
-    ctx->order_gen = ctx->cand_gen;
-    ctx->order_frames = p.frames;
-    return RT_OK;
+// After a launch that recorded tile costs.
+void finish_tile_order(rt_ctx* ctx, const rtk::TraceParams& p) {
+    if (!p.tile_cost) return;
+    ctx->cost_gen = ctx->cand_gen;
+    ctx->cost_frames = p.frames;
 }
 
 // Per-column / per-row halves of the pixel-invariant seed hash (wgsl:309-310), built on
@@ -554,7 +562,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
-        if (rt_status s = finish_tile_order(ctx, p, stream)) return s;
+        finish_tile_order(ctx, p);
         src = dst;  // later launches continue the accumulation in place
     }
     return RT_OK;
@@ -748,7 +756,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
-        if (rt_status s = finish_tile_order(ctx, p, stream)) return s;
+        finish_tile_order(ctx, p);
         // frame f of the launch wrote img[(cur + 1 + f) % 2]
         const int newest = (nf & 1u) ? 1 - cur : cur;
         if (known) {

@@ -1003,13 +1003,16 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) RT_TRAC
 }
 
 // launch_tile_order: one 1024-thread workgroup; bucket = quantised log2 of the cost (four
-// buckets per octave), counted in LDS, then each tile is placed at its bucket's next slot,
-// costliest bucket first (order inside a bucket is arbitrary: tiles are independent).
+// buckets per octave).  Each wave counts its tiles into its own LDS histogram (atomics only
+// contend inside a wave), one block-wide scan over the [bucket][wave] counts turns them
+// into offsets, costliest bucket first, and each tile is placed at its wave's next slot of
+// its bucket (order inside a bucket is arbitrary: tiles are independent).
 __global__ __launch_bounds__(1024) void rt_tile_order_kernel(const uint32_t* __restrict__ cost,
                                                              uint32_t* __restrict__ order,
                                                              uint32_t tiles, uint32_t tiles_x) {
-    constexpr uint32_t kBuckets = 128;
-    __shared__ uint32_t next[kBuckets];
+    constexpr uint32_t kBuckets = 128, kWaves = 16, kSlots = kBuckets * kWaves;
+    __shared__ uint32_t hist[kSlots];          // [bucket][wave]
+    __shared__ uint32_t scan[1024];
     auto bucket = [](uint32_t c) -> uint32_t {
         if (c == 0u) return kBuckets - 1u;
         const uint32_t lz = (uint32_t)__builtin_clz(c);
@@ -1017,22 +1020,55 @@ __global__ __launch_bounds__(1024) void rt_tile_order_kernel(const uint32_t* __r
         const uint32_t m = e >= 2u ? (c >> (e - 2u)) & 3u : (c << (2u - e)) & 3u;
         return kBuckets - 1u - (e * 4u + m);          // descending cost
     };
-    for (uint32_t b = threadIdx.x; b < kBuckets; b += blockDim.x) next[b] = 0u;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6;
+    hist[2 * tid] = 0u;
+    hist[2 * tid + 1] = 0u;
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < tiles; t += blockDim.x) atomicAdd(&next[bucket(cost[t])], 1u);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t sum = 0;
-        for (uint32_t b = 0; b < kBuckets; ++b) {
-            const uint32_t c = next[b];
-            next[b] = sum;
-            sum += c;
+    // (loads in batches of 8 per thread: one memory latency per batch, not per tile)
+    constexpr uint32_t kBatch = 8;
+    for (uint32_t t0 = tid; t0 < tiles; t0 += 1024u * kBatch) {
+        uint32_t c[kBatch];
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k) {
+            const uint32_t t = t0 + k * 1024u;
+            c[k] = t < tiles ? cost[t] : 0u;
         }
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k)
+            if (t0 + k * 1024u < tiles) atomicAdd(&hist[bucket(c[k]) * kWaves + wave], 1u);
     }
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < tiles; t += blockDim.x) {
-        const uint32_t pos = atomicAdd(&next[bucket(cost[t])], 1u);
-        order[pos] = ((t / tiles_x) << 16) | (t % tiles_x);
+    // exclusive scan of the 2048 counts: pairs per thread, Hillis-Steele over the threads
+    const uint32_t a0 = hist[2 * tid], a1 = hist[2 * tid + 1];
+    uint32_t v = a0 + a1;
+    scan[tid] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024u; d <<= 1) {
+        const uint32_t add = tid >= d ? scan[tid - d] : 0u;
+        __syncthreads();
+        v += add;
+        scan[tid] = v;
+        __syncthreads();
+    }
+    const uint32_t before = v - a0 - a1;               // exclusive prefix of the pair
+    hist[2 * tid] = before;
+    hist[2 * tid + 1] = before + a0;
+    __syncthreads();
+    for (uint32_t t0 = tid; t0 < tiles; t0 += 1024u * kBatch) {
+        uint32_t c[kBatch];
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k) {
+            const uint32_t t = t0 + k * 1024u;
+            c[k] = t < tiles ? cost[t] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k) {
+            const uint32_t t = t0 + k * 1024u;
+            if (t < tiles) {
+                const uint32_t pos = atomicAdd(&hist[bucket(c[k]) * kWaves + wave], 1u);
+                order[pos] = ((t / tiles_x) << 16) | (t % tiles_x);
+            }
+        }
     }
 }
 
