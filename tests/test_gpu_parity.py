@@ -577,3 +577,32 @@ def test_update_frames_with_foreign_counts(rt, oracle, pipe, pairs):
     assert newest == 1
     assert_same(host(b), ref)
     assert_same(host(a), prev)
+
+
+def test_tile_order_does_not_change_pixels(rt, pipe):
+    """Cost-ordered tiles (rt_set_tile_order AUTO: the first fused launch of a camera
+    measures, the next ones sort and reorder the workgroups) leave both ping-pong buffers
+    bit-identical to raster order, for the whole image and a stripe rank."""
+    w, h = 72, 48
+    sc = rt.synthetic_scene(300)
+    seeds = rt.frame_seeds(31, 24)
+    cam = camera(rt, w, h, depth=1, spp=500)
+    out = {}
+    pipe.set_frames_per_launch(6)
+    try:
+        for mode in ("off", "auto"):
+            pipe.set_tile_order(mode)
+            for r, n in ((0, 1), (1, 2)):
+                rows = rt.stripe_local_rows(h, r, n) if n > 1 else h
+                a, b = pipe.new_image(w, rows), pipe.new_image(w, rows)
+                newest = pipe.update_frames(a, b, w, h, cam, sc, seeds, r, n)
+                out[mode, r, n] = (newest, host(a), host(b))
+    finally:
+        pipe.set_frames_per_launch(0)
+        pipe.set_tile_order("auto")
+    for key in ((0, 1), (1, 2)):
+        na, a0, b0 = out[("off",) + key]
+        nb, a1, b1 = out[("auto",) + key]
+        assert na == nb
+        assert_same(a1, a0)
+        assert_same(b1, b0)
