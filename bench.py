@@ -190,15 +190,20 @@ def main():
     r.frames(cam_t, spheres, seeds[args.warmup:frames])
     ev1.record(stream)
     image = r.finish()
+    ev2 = torch.cuda.Event(enable_timing=True)
+    ev2.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    # breakdown (HIP events on this rank's stream): the K frames, then the gather +
+    # de-interleave; both stay inside dt
+    render_s, gather_s = ev0.elapsed_time(ev1) / 1e3, ev1.elapsed_time(ev2) / 1e3
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt, render_s, gather_s], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt, render_s, gather_s = (float(x) for x in t.tolist())
 
     # every pixel of the gathered image must hold exactly warmup + steps samples
     sample_ok = image is not None and bool(torch.all(image[..., 3] == frames).item())
@@ -308,6 +313,9 @@ def main():
             "present_rgba8": present,
             "per_frame_dispatch": per_frame,
             "accumulated_spp_ok": sample_ok,
+            # max over ranks; value's time includes both (and the barriers)
+            "timed_breakdown_ms": {"frames": round(render_s * 1e3, 4),
+                                   "gather_and_deinterleave": round(gather_s * 1e3, 4)},
         }
         if world == 1 and args.cpu_seconds > 0:
             line["cpu_baseline"] = cpu_baseline(cams[0], spheres, w, h, args.cpu_seconds)
