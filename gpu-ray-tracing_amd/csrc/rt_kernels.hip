@@ -826,7 +826,10 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
                 col = sample<kScan>(p, cam, tile, ncand, tc, hxy, ng, p.seed_b[fw], fw,
                                     tc.valid, fw < p.hint_frames);
         }
-        if (w != 0u) lds_recs[(w - 1u) * 64u + lane] = make_float4(col.x, col.y, col.z, 0.0f);
+        // two LDS slots alternating by group: wave 0 reads group g's slot before it reaches
+        // the barrier of group g + 1, so one barrier per group suffices
+        float4* slot = lds_recs + ((f / kFrameGroup) & 1u) * (kFrameGroup - 1u) * 64u;
+        if (w != 0u) slot[(w - 1u) * 64u + lane] = make_float4(col.x, col.y, col.z, 0.0f);
         __syncthreads();
         if (w == 0u) {
 #pragma unroll
@@ -834,7 +837,7 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
                 const uint32_t fj = f + j;
                 if (fj >= p.frames) break;
                 if (j != 0) {
-                    const float4 cj = lds_recs[(j - 1u) * 64u + lane];
+                    const float4 cj = slot[(j - 1u) * 64u + lane];
                     col = mk(cj.x, cj.y, cj.z);
                 }
                 const uint32_t nb = p.hint_n[fj];                 // count before frame fj
@@ -860,7 +863,6 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
                         make_float4(c.x, c.y, c.z, (float)na);
             }
         }
-        __syncthreads();
     }
 }
 
@@ -1323,10 +1325,10 @@ hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
     else if (kernel == kTraceList)
         launch_trace_as<kTraceList>(p, 0, stream);
     else if (kernel == kTraceListPair)
-        launch_trace_as<kTraceListPair>(p, (frame_group<kTraceListPair>() - 1) * 64 *
+        launch_trace_as<kTraceListPair>(p, 2 * (frame_group<kTraceListPair>() - 1) * 64 *
                                                sizeof(float4), stream);
     else if (kernel == kTraceListQuad)
-        launch_trace_as<kTraceListQuad>(p, (frame_group<kTraceListQuad>() - 1) * 64 *
+        launch_trace_as<kTraceListQuad>(p, 2 * (frame_group<kTraceListQuad>() - 1) * 64 *
                                                sizeof(float4), stream);
     else
         launch_trace_as<kTraceExhaustive>(p, 0, stream);
