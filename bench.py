@@ -1,6 +1,6 @@
 """Benchmark of the per-pixel ray-tracing hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config K3]   (K=128, W=128)
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config K3]   (K=512, W=128)
 
 Workload (default K3 = BASELINE.json configs[2], the config the north-star target is
 quoted on): 1920x1080, seeded 500-sphere scene, max_depth 1.  A "step" is one
@@ -64,8 +64,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # defaults: whole 64-frame launches; the first warmup launch measures the tile costs
-    # the timed launches are scheduled by and the second sorts them (rt_set_tile_order)
-    ap.add_argument("--steps", type=int, default=128)
+    # the timed launches are scheduled by and the second sorts them (rt_set_tile_order);
+    # 512 timed frames (8 ms on one GPU) amortise the job's single gather at N > 1
+    ap.add_argument("--steps", type=int, default=512)
     ap.add_argument("--warmup", type=int, default=128)
     ap.add_argument("--config", default="K3", choices=sorted(CONFIGS))
     ap.add_argument("--scan", default="culled", choices=["culled", "exhaustive"],
