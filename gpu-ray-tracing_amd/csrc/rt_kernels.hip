@@ -878,9 +878,6 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
 #ifndef RT_TRACE_MIN_WAVES
 #define RT_TRACE_MIN_WAVES 7
 #endif
-#ifndef RT_TRACE_ATTR
-#define RT_TRACE_ATTR
-#endif
 // Waves (tiles) per workgroup: the culled instance shares the LDS copy of the records
 // among 4 waves; the others use one-wave workgroups, so a finished tile frees its slot
 // without waiting for slower neighbours.
@@ -914,7 +911,7 @@ __device__ __forceinline__ void record_cost(const TraceParams& p, uint32_t tile,
 }
 
 template <int kScan>
-__global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) RT_TRACE_ATTR void rt_trace_kernel(
+__global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt_trace_kernel(
     const TraceParams p) {
     STAMP(-2);
     WAVE_TRACE(0);
