@@ -16,10 +16,11 @@ timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo benc
 cat $O/bench.json
 timeout -k 10 300 python bench.py --config K2 --cpu-seconds 0 > $O/bench_k2.json 2>> $O/bench.err || exit 1
 timeout -k 10 300 python bench.py --config K5 --steps 5 --warmup 2 --cpu-seconds 0 > $O/bench_k5.json 2>> $O/bench.err || exit 1
-# profiled command: whole 64-frame launches only (warmup 128 + 128 timed), so rocprofv3's
-# per-launch average and the line's kernel_avg_us describe the same launches
+# profiled command: the default bench (whole 64-frame launches: 128 warmup + 512 timed) without
+# the side measurements, so rocprofv3's per-launch average and the line's kernel_avg_us
+# describe the same kind of launches
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench \
-  -- python3 bench.py --cpu-seconds 0 --exhaustive-steps 0 --per-frame-steps 0 --warmup 128 --steps 128 \
+  -- python3 bench.py --cpu-seconds 0 --exhaustive-steps 0 --per-frame-steps 0 \
   > $O/prof.log 2>&1 || { echo prof failed; tail $O/prof.log; exit 1; }
 grep '^{' $O/prof.log > $O/bench_profiled.json; cat $O/bench_profiled.json
 head -4 $O/prof/bench_kernel_stats.csv
@@ -31,3 +32,5 @@ done
 FRAMES_PER_LAUNCH=64 python3 tools/pmc_summary.py $O/pmc_K3_culled.json trace_kernel $O/pmc/culled_FETCH_SIZE_counter_collection.csv $O/pmc/culled_WRITE_SIZE_counter_collection.csv | tail -8
 timeout -k 10 300 python tools/rank_sim.py K3 50 > $O/rank_k3.jsonl 2>&1 || exit 1
 cat $O/rank_k3.jsonl
+timeout -k 10 300 python tools/rank_sim.py K5 10 > $O/rank_k5.jsonl 2>&1 || exit 1
+grep '^{' $O/rank_k5.jsonl
