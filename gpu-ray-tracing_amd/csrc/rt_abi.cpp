@@ -34,6 +34,13 @@ struct rt_ctx {
     // |R| lies in [2^-20, 2^20]: the scene half of camera_rays_bounded
     double scene_bound = 0.0;
     bool radii_ok = true;
+    // XZ grid of the small spheres for wide-cone bounce rays (build_grid; TraceParams
+    // grid_*): device CSR arrays and the parameters copied into every launch.
+    uint32_t* d_grid = nullptr;     // [cells + 1] starts, then items, then the big list
+    struct Grid {
+        uint32_t nx = 0, nz = 0, nbig = 0, items = 0;
+        float x0, z0, s, inv_s, ylo, yhi, cx, cy, cz, reach, m, e;
+    } grid;
     // Per-tile candidate lists of camera rays (culled scan), valid for cand_key.
     uint32_t* cand_cnt = nullptr;
     float4* cand_rec = nullptr;
@@ -108,6 +115,7 @@ uint32_t host_f2u(float f) {
 double norm3(const float* v) {
     return std::sqrt((double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2]);
 }
+double norm3d(const double* v) { return std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
 
 // Whether every camera ray of p's camera, image and stripes, against the context's scene,
 // stays inside the domain where the camera-ray-only instances use the exact fast division
@@ -179,6 +187,139 @@ rt_status check_image(uint32_t w, uint32_t h) {
     return RT_OK;
 }
 
+// Uniform XZ grid of the small spheres (rt_kernels.hip scan_grid), built on every scene
+// upload of at least kGridMinSpheres spheres whose |C| + |R| stay within 2^40 (so no f32
+// intermediate of the root test overflows for the rays that may use the grid).  Small:
+// |R| <= 4x the median radius; the others (the ground, the few large spheres) go to the
+// big list that every ray tests.  Cells are about two small spheres' worth of the centres'
+// bounding area, at most kGridMaxDim per axis.  A ray may walk the grid when
+// 2.5e-3 (|o - c| + reach) <= m (c, reach: centre and radius of the small spheres' extent),
+// which bounds the f32 discriminant margin of every small sphere by m; each sphere is then
+// registered in every cell within |R| + m + e of its centre, e bounding the f32 error of
+// the walk's cell positions: (steps + 16) x 8 eps x the largest coordinate magnitude it
+// handles, plus 1e-3 of a cell.  Rays further out, with |d|^2 outside [2^-20, 2^20] or
+// non-finite, keep the exhaustive scan.
+constexpr uint32_t kGridMinSpheres = 64;
+constexpr uint32_t kGridMaxDim = 256;
+
+rt_status build_grid(rt_ctx* ctx, const rt_sphere* sp, uint32_t count, hipStream_t stream) {
+    ctx->grid.nx = 0;
+    if (count < kGridMinSpheres || !(ctx->scene_bound <= 0x1p40)) return RT_OK;
+    std::vector<double> radii(count);
+    for (uint32_t i = 0; i < count; ++i) radii[i] = std::fabs((double)sp[i].radius);
+    std::vector<double> sorted = radii;
+    std::nth_element(sorted.begin(), sorted.begin() + count / 2, sorted.end());
+    const double r_small = 4.0 * sorted[count / 2];
+    std::vector<uint32_t> small, big;
+    for (uint32_t i = 0; i < count; ++i) (radii[i] <= r_small ? small : big).push_back(i);
+    if (small.size() < kGridMinSpheres / 2) return RT_OK;
+    // extent of the small spheres: centre c (mid-point of the bounding box) and reach
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    double rmax = 0.0;
+    for (uint32_t i : small) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], (double)sp[i].position[k]);
+            hi[k] = std::max(hi[k], (double)sp[i].position[k]);
+        }
+        rmax = std::max(rmax, radii[i]);
+    }
+    double c[3], g_r = 0.0;
+    for (int k = 0; k < 3; ++k) c[k] = (double)(float)(0.5 * (lo[k] + hi[k]));
+    for (uint32_t i : small) {
+        double v[3];
+        for (int k = 0; k < 3; ++k) v[k] = (double)sp[i].position[k] - c[k];
+        g_r = std::max(g_r, norm3d(v));
+    }
+    const double reach = (g_r + rmax) * 1.001;
+    // rays up to 3 reaches from the centre may use the grid
+    const double m = 2.5e-3 * 4.0 * reach * 1.001 + 1e-30;
+    const double area = std::max(hi[0] - lo[0], 1e-30) * std::max(hi[2] - lo[2], 1e-30);
+    double s = std::sqrt(area * 2.0 / (double)small.size());
+    s = std::max({s, (hi[0] - lo[0]) / (kGridMaxDim - 8), (hi[2] - lo[2]) / (kGridMaxDim - 8),
+                  2.0 * rmax / 8.0, 1e-6});
+    const double L = norm3d(c) + m / 2.5e-3 + 2.0 * reach + 4.0 * s;
+    const double e = (2.0 * kGridMaxDim + 16.0) * 8.0 * 0x1p-24 * L + 1e-3 * s;
+    const double pad = m + e;
+    double x0 = INFINITY, x1 = -INFINITY, z0 = INFINITY, z1 = -INFINITY;
+    double ylo = INFINITY, yhi = -INFINITY;
+    for (uint32_t i : small) {
+        const double w = radii[i] * 1.0001 + pad;
+        x0 = std::min(x0, sp[i].position[0] - w);
+        x1 = std::max(x1, sp[i].position[0] + w);
+        z0 = std::min(z0, sp[i].position[2] - w);
+        z1 = std::max(z1, sp[i].position[2] + w);
+        ylo = std::min(ylo, sp[i].position[1] - w);
+        yhi = std::max(yhi, sp[i].position[1] + w);
+    }
+    x0 = (double)(float)x0 - e;
+    z0 = (double)(float)z0 - e;
+    s = (double)(float)s;
+    const uint32_t nx = (uint32_t)std::ceil((x1 + e - x0) / s);
+    const uint32_t nz = (uint32_t)std::ceil((z1 + e - z0) / s);
+    if (nx < 1 || nz < 1 || nx > kGridMaxDim || nz > kGridMaxDim) return RT_OK;
+    // CSR: count, prefix, fill (small spheres in index order within every cell)
+    const uint32_t cells = nx * nz;
+    std::vector<uint32_t> start(cells + 1, 0u);
+    auto span = [&](uint32_t i, uint32_t& ax, uint32_t& bx, uint32_t& az, uint32_t& bz) {
+        const double w = radii[i] * 1.0001 + pad;
+        auto cell = [&](double v, double o, uint32_t n) {
+            const double f = std::floor((v - o) / s);
+            return (uint32_t)std::min(std::max(f, 0.0), (double)(n - 1));
+        };
+        ax = cell(sp[i].position[0] - w, x0, nx);
+        bx = cell(sp[i].position[0] + w, x0, nx);
+        az = cell(sp[i].position[2] - w, z0, nz);
+        bz = cell(sp[i].position[2] + w, z0, nz);
+    };
+    for (uint32_t i : small) {
+        uint32_t ax, bx, az, bz;
+        span(i, ax, bx, az, bz);
+        for (uint32_t z = az; z <= bz; ++z)
+            for (uint32_t x = ax; x <= bx; ++x) start[z * nx + x + 1]++;
+    }
+    for (uint32_t k = 0; k < cells; ++k) start[k + 1] += start[k];
+    const uint32_t items = start[cells];
+    std::vector<uint32_t> buf(cells + 1 + items + big.size());
+    std::copy(start.begin(), start.end(), buf.begin());
+    std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+    for (uint32_t i : small) {
+        uint32_t ax, bx, az, bz;
+        span(i, ax, bx, az, bz);
+        for (uint32_t z = az; z <= bz; ++z)
+            for (uint32_t x = ax; x <= bx; ++x) buf[cells + 1 + fill[z * nx + x]++] = i;
+    }
+    std::copy(big.begin(), big.end(), buf.begin() + cells + 1 + items);
+    // The previous grid may still be read by queued launches: order on the stream.
+    hipError_t err = hipStreamSynchronize(stream);
+    if (err != hipSuccess) return hip_fail(err, "hipStreamSynchronize");
+    (void)hipFree(ctx->d_grid);
+    ctx->d_grid = nullptr;
+    err = hipMalloc(&ctx->d_grid, buf.size() * sizeof(uint32_t));
+    if (err != hipSuccess) return hip_fail(err, "hipMalloc(sphere grid)");
+    err = hipMemcpyAsync(ctx->d_grid, buf.data(), buf.size() * sizeof(uint32_t),
+                         hipMemcpyHostToDevice, stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(stream);
+    if (err != hipSuccess) return hip_fail(err, "hipMemcpyAsync(sphere grid)");
+    rt_ctx::Grid& g = ctx->grid;
+    g.nx = nx;
+    g.nz = nz;
+    g.nbig = (uint32_t)big.size();
+    g.items = items;
+    g.x0 = (float)x0;
+    g.z0 = (float)z0;
+    g.s = (float)s;
+    g.inv_s = (float)(1.0 / s);
+    g.ylo = (float)(ylo - e);
+    g.yhi = (float)(yhi + e);
+    g.cx = (float)c[0];
+    g.cy = (float)c[1];
+    g.cz = (float)c[2];
+    g.reach = (float)reach;
+    g.m = (float)m;
+    g.e = (float)e;
+    return RT_OK;
+}
+
 rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
                          hipStream_t stream) {
     if (count > kMaxSpheres) return fail(RT_ERR_INVALID_SIZE, "sphere_count too large");
@@ -246,6 +387,7 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
     }
     ctx->scene_bound = bound;
     ctx->radii_ok = radii_ok;
+    if (rt_status s = build_grid(ctx, spheres, count, stream)) return s;
     ctx->cached.assign(spheres, spheres + count);
     ctx->count = count;
     ctx->valid = true;
@@ -529,6 +671,28 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
         const bool bounces = cam->max_depth >= 2.0f;
         p.lds_records = (bounces && padded <= rtk::kLdsMaxRecords) ? padded : 0u;
         if (rt_status s = ensure_candidates(ctx, p, stream)) return s;
+        if (bounces && ctx->grid.nx) {
+            const rt_ctx::Grid& g = ctx->grid;
+            const uint32_t cells = g.nx * g.nz;
+            p.grid_start = ctx->d_grid;
+            p.grid_items = ctx->d_grid + cells + 1;
+            p.grid_big = ctx->d_grid + cells + 1 + g.items;
+            p.grid_nx = g.nx;
+            p.grid_nz = g.nz;
+            p.grid_nbig = g.nbig;
+            p.grid_x0 = g.x0;
+            p.grid_z0 = g.z0;
+            p.grid_s = g.s;
+            p.grid_inv_s = g.inv_s;
+            p.grid_ylo = g.ylo;
+            p.grid_yhi = g.yhi;
+            p.grid_cx = g.cx;
+            p.grid_cy = g.cy;
+            p.grid_cz = g.cz;
+            p.grid_reach = g.reach;
+            p.grid_m = g.m;
+            p.grid_e = g.e;
+        }
     }
     return RT_OK;
 }
@@ -607,6 +771,7 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->d_hy);
         (void)hipFree(ctx->tile_cost);
         (void)hipFree(ctx->tile_order);
+        (void)hipFree(ctx->d_grid);
         free_candidates(ctx);
     }
     delete ctx;

@@ -47,6 +47,20 @@ struct TraceParams {
     const uint32_t* cand_cnt;  // [tile] listed spheres, kCandNone = no list
     const float4* cand_rec;    // [tile][cand_k] their scan records, in index order, padded
     const float4* cand_sph;    // [tile][cand_k][2] their 32-B GpuSphere records
+    // Uniform XZ grid over the small spheres for the bounce rays whose wave cone is too
+    // wide (rt_kernels.hip, scan_grid; built by rt_abi.cpp build_grid): CSR cell lists of
+    // sphere indices, every sphere registered in each cell within grid_pad of its centre;
+    // grid_big lists the other spheres.  grid_nx == 0: no grid.
+    const uint32_t* grid_start;  // [grid_nx * grid_nz + 1]
+    const uint32_t* grid_items;
+    const uint32_t* grid_big;    // ascending sphere indices
+    uint32_t grid_nx, grid_nz, grid_nbig;
+    float grid_x0, grid_z0, grid_s, grid_inv_s;
+    float grid_ylo, grid_yhi;    // slab of the gridded spheres, padded
+    // a ray may use the grid only if 2.5e-3 * (|o - grid_c| + grid_reach) <= grid_m (the
+    // f32 margin of the discriminant stays inside the registration padding)
+    float grid_cx, grid_cy, grid_cz, grid_reach, grid_m;
+    float grid_e;                // bound on the walk's f32 position error (also in the padding)
     const uint32_t* hx;    // [width]  hash(x * 73)  (wgsl:309, pixel-invariant)
     const uint32_t* hy;    // [height] hash(y * 51)  (wgsl:310)
     float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3];

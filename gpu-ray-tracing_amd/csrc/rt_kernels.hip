@@ -387,13 +387,127 @@ extern __shared__ float4 lds_recs[];
 
 // kLds: read the cull records from the workgroup's LDS copy (else from the global array);
 // both hold count records zero-padded to a multiple of 64.
+// ---- Exact grid walk for incoherent bounce rays ---------------------------------------
+//
+// The closest hit of the linear scan (consider() in index order: a later sphere wins only
+// if strictly nearer) is the minimum over spheres of c_i = root1 if root1 > 0.001, else
+// root2 if root2 > 0.001, with ties going to the lower index: a sphere whose first root is
+// valid but not below the running tmax has a second root at least as large (h + q >= h - q,
+// a > 0), and a tie keeps the earlier index.  So the spheres may be tested in any order with
+// consider_any's rule.  A sphere can be accepted only at a root t > 0 whose point lies
+// within R + m of its centre (m the f32 margin of the discriminant, as in the cone test), so
+// the grid walk visits every cell the ray passes through for t >= 0 inside the gridded
+// spheres' slab, and each sphere is registered in every cell within R + grid_m + grid_e of
+// its centre (rt_abi.cpp): no sphere that could be accepted is skipped.
+__device__ __forceinline__ void consider_any(float disc, float h, float a, uint32_t i,
+                                             float& tmax, int& idx) {
+    if (!(disc < 0.0f)) {                                               // wgsl:189
+        const float q = sqrtf(disc);
+        float root = (h - q) / a;
+        if (root <= 0x1.0624dep-10f) {                                  // wgsl:196
+            root = (h + q) / a;
+            if (root <= 0x1.0624dep-10f) return;                        // wgsl:198
+        }
+        if (root < tmax || (root == tmax && (int)i < idx)) {
+            tmax = root;
+            idx = (int)i;
+        }
+    }
+}
+__device__ __forceinline__ Hit scan_grid(const TraceParams& p, v3 o, v3 d, bool live) {
+    const float a = dot(d, d);
+    float tmax = 0x1.05ed2ep+118f;             // 3.4e35 (wgsl:266)
+    int idx = -1;
+    // spheres outside the grid (the ground, large ones): every live lane tests them
+    for (uint32_t b = 0; b < p.grid_nbig; ++b) {
+        const uint32_t i = p.grid_big[b];
+        const float4 g = p.geom[i];
+        float h;
+        const float disc = discriminant(g, o, d, a, h);
+        if (live) consider_any(disc, h, a, i, tmax, idx);
+    }
+    if (!live) return Hit{idx, tmax};
+    // t range of the ray inside the slab and the grid box (t >= 0)
+    float t0 = 0.0f, t1 = 0x1.05ed2ep+118f;
+    auto clip = [&](float oc, float dc, float lo, float hi) {
+        if (dc != 0.0f) {
+            const float ta = (lo - oc) / dc, tb = (hi - oc) / dc;
+            t0 = fmaxf(t0, fminf(ta, tb));
+            t1 = fminf(t1, fmaxf(ta, tb));
+        } else if (oc < lo || oc > hi) {
+            t1 = -1.0f;
+        }
+    };
+    const float xhi = p.grid_x0 + p.grid_s * (float)p.grid_nx;
+    const float zhi = p.grid_z0 + p.grid_s * (float)p.grid_nz;
+    clip(o.y, d.y, p.grid_ylo, p.grid_yhi);
+    clip(o.x, d.x, p.grid_x0, xhi);
+    clip(o.z, d.z, p.grid_z0, zhi);
+    if (!(t0 <= t1)) return Hit{idx, tmax};
+    // 2-D DDA over the cells from P(t0) to P(t1)
+    const int nx = (int)p.grid_nx, nz = (int)p.grid_nz;
+    int ix = (int)floorf((fmaf(t0, d.x, o.x) - p.grid_x0) * p.grid_inv_s);
+    int iz = (int)floorf((fmaf(t0, d.z, o.z) - p.grid_z0) * p.grid_inv_s);
+    ix = min(max(ix, 0), nx - 1);
+    iz = min(max(iz, 0), nz - 1);
+    const int sx = d.x > 0.0f ? 1 : -1, sz = d.z > 0.0f ? 1 : -1;
+    const float inf = 0x1.05ed2ep+118f;
+    float tx = d.x != 0.0f
+                   ? (p.grid_x0 + p.grid_s * (float)(ix + (sx > 0)) - o.x) / d.x : inf;
+    float tz = d.z != 0.0f
+                   ? (p.grid_z0 + p.grid_s * (float)(iz + (sz > 0)) - o.z) / d.z : inf;
+    const float dtx = d.x != 0.0f ? p.grid_s / fabsf(d.x) : inf;
+    const float dtz = d.z != 0.0f ? p.grid_s / fabsf(d.z) : inf;
+    const float slack = 2.0f * p.grid_e * rsqrtf(a) * 1.01f;
+    for (int step = 0; step < nx + nz + 2; ++step) {
+        const uint32_t c = (uint32_t)(iz * nx + ix);
+        const uint32_t k1 = p.grid_start[c + 1];
+        for (uint32_t k = p.grid_start[c]; k < k1; ++k) {
+            const uint32_t i = p.grid_items[k];
+            float h;
+            const float disc = discriminant(p.geom[i], o, d, a, h);
+            consider_any(disc, h, a, i, tmax, idx);
+        }
+        // A cell entered beyond t1, or beyond the closest hit so far, holds no better hit;
+        // slack: the walk's position error (grid_e, as t) and 1e-4 of t.
+        const float tn = fminf(tx, tz);
+        if (tn > fminf(t1, tmax) * 1.0001f + slack) break;
+        if (tx < tz) {
+            ix += sx;
+            tx += dtx;
+            if (ix < 0 || ix >= nx) break;
+        } else {
+            iz += sz;
+            tz += dtz;
+            if (iz < 0 || iz >= nz) break;
+        }
+    }
+    return Hit{idx, tmax};
+}
+
+// The wave may walk the grid: every live ray finite and within reach of the grid margin.
+__device__ __forceinline__ bool grid_usable(const TraceParams& p, v3 o, v3 d, bool live) {
+    if (p.grid_nx == 0u) return false;
+    const v3 oc = mk(o.x - p.grid_cx, o.y - p.grid_cy, o.z - p.grid_cz);
+    const float dist = __builtin_amdgcn_sqrtf(dot(oc, oc));
+    const float dd = dot(d, d);
+    const bool ok = finite3(o) && finite3(d) && dd >= 0x1p-20f && dd <= 0x1p20f &&
+                    2.5e-3f * 1.01f * (dist + p.grid_reach) <= p.grid_m;
+    return __ballot(live && !ok) == 0ull;
+}
+
 template <bool kLds>
-__device__ __forceinline__ Hit scan_culled(const float4* __restrict__ geom, uint32_t count,
-                                           v3 o, v3 d, bool live) {
+__device__ __forceinline__ Hit scan_culled(const TraceParams& p, const float4* __restrict__ geom,
+                                           uint32_t count, v3 o, v3 d, bool live) {
     const float4* recs = kLds ? lds_recs : geom;
     Cone k;
-    if (count < kCullMinSpheres || !wave_cone(o, d, live, k))
+    if (count < kCullMinSpheres || !wave_cone(o, d, live, k)) {
+#ifndef RT_NO_GRID
+        if (count >= kCullMinSpheres && grid_usable(p, o, d, live))
+            return scan_grid(p, o, d, live);
+#endif
         return scan_exhaustive<RT_SCAN_CHUNK>(geom, count, o, d);
+    }
     STAMP(2);
     const uint32_t lane = threadIdx.x & 63u;
     const float a = dot(d, d);
@@ -581,8 +695,8 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
             (kScan != kTraceCulled || listed)
                 ? scan_exhaustive<scan_chunk<kScan>(), fast_core<kScan>(1), kScan != kTraceList>(
                       listed ? p.cand_rec + lbase : p.geom, listed ? ncand : p.count, o, d)
-            : p.lds_records ? scan_culled<true>(p.geom, p.count, o, d, live)
-                            : scan_culled<false>(p.geom, p.count, o, d, live);
+            : p.lds_records ? scan_culled<true>(p, p.geom, p.count, o, d, live)
+                            : scan_culled<false>(p, p.geom, p.count, o, d, live);
 #endif
         if (kScan != kTraceCulled) STAMP(2);                      // (culled: inside the scan)
         const float4* hs = listed ? p.cand_sph + 2 * lbase : p.sph;

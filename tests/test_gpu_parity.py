@@ -346,6 +346,58 @@ def test_culled_scan_equals_exhaustive(rt, seed):
     assert_same(out["culled"], out["exhaustive"])
 
 
+def _lattice_scene(rng, jitter=0.9, twins=False, y_spread=0.0):
+    """RTIOW-like layout: small spheres on a unit lattice, three large ones, the ground."""
+    rows = []
+    for a in range(-11, 11):
+        for b in range(-11, 11):
+            x = a + jitter * rng.uniform()
+            z = b + jitter * rng.uniform()
+            y = 0.2 + y_spread * rng.uniform()
+            mat = rng.integers(0, 3)
+            fuzz = -2.0 if mat == 0 else (rng.uniform(0, 0.5) if mat == 1 else 2.0)
+            col = [1.5, 1.0, 1.0] if mat == 2 else list(rng.uniform(0, 1, 3))
+            rows.append([x, y, z, 0.2] + col + [fuzz])
+            if twins and rng.uniform() < 0.3:
+                rows.append(rows[-1][:])          # coincident: the lower index must win
+    rows += [[0, 1, 0, 1.0, 1.5, 1, 1, 2.0], [-4, 1, 0, 1.0, 0.4, 0.2, 0.1, -2.0],
+             [4, 1, 0, 1.0, 0.7, 0.6, 0.5, 0.0]]
+    s = np.array([[0, -1000, 0, 1000, 0.5, 0.5, 0.5, -2]] + rows, np.float32)
+    return s
+
+
+@pytest.mark.parametrize("case", ["lattice", "twins", "inside", "down", "tall", "aligned"])
+def test_grid_walk_equals_exhaustive(rt, case):
+    """Bounce rays whose wave cone is too wide walk the XZ grid of the small spheres
+    (rt_kernels.hip scan_grid): bitwise equal to the exhaustive scan, for coincident
+    spheres (index tie-break), a camera inside the cluster, rays straight down (zero x/z
+    direction components), a tall slab and spheres centred on cell boundaries."""
+    rng = np.random.default_rng(["lattice", "twins", "inside", "down", "tall",
+                                 "aligned"].index(case) + 11)
+    spheres = _lattice_scene(rng, jitter=0.0 if case == "aligned" else 0.9,
+                             twins=case == "twins", y_spread=25.0 if case == "tall" else 0.0)
+    sc = rt.SphereCollection(spheres)
+    # (looking straight down: a tiny z offset keeps the camera basis defined)
+    look_from, look_at, fov, lens = {
+        "inside": ((0.3, 0.6, 0.2), (5.0, 0.3, 2.0), 90.0, 0.6),
+        "down": ((0.0, 20.0, 1e-3), (0.0, 0.0, 0.0), 60.0, 0.0)}.get(
+        case, ((13.0, 2.0, 3.0), (0.0, 0.0, 0.0), 20.0, 0.6))
+    settings = rt.CameraSettings(field_of_view=fov, max_depth=8, defocus_angle=lens,
+                                 focus_distance=10.0, look_from=look_from, look_at=look_at)
+    w, h = 192, 128
+    cam = rt.SceneCamera.from_settings(settings, w, h, 0.375)
+    seeds = rt.frame_seeds(5, 3)
+    out = {}
+    for mode in ("culled", "exhaustive"):
+        p = rt.ComputeShaderPipeline(0)
+        p.set_scan_mode(mode)
+        img = p.new_image(w, h)
+        p.render(img, img, w, h, cam, sc, seeds)
+        out[mode] = host(img)
+        p.close()
+    assert_same(out["culled"], out["exhaustive"])
+
+
 @pytest.mark.parametrize("depth", [1, 2])
 def test_candidate_lists_follow_camera_and_scene(rt, oracle, depth):
     """The per-tile camera-ray candidate lists are rebuilt when the camera geometry, the
