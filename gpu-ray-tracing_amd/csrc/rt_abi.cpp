@@ -34,7 +34,7 @@ struct rt_ctx {
     // |R| lies in [2^-20, 2^20]: the scene half of camera_rays_bounded
     double scene_bound = 0.0;
     bool radii_ok = true;
-    // XZ grid of the small spheres for wide-cone bounce rays (build_grid; TraceParams
+    // XZ grid of the small spheres for bounce rays (build_grid; TraceParams
     // grid_*): device CSR arrays and the parameters copied into every launch.
     uint32_t* d_grid = nullptr;     // [cells + 1] starts, then items, then the big list
     struct Grid {
@@ -200,6 +200,12 @@ rt_status check_image(uint32_t w, uint32_t h) {
 // handles, plus 1e-3 of a cell.  Rays further out, with |d|^2 outside [2^-20, 2^20] or
 // non-finite, keep the exhaustive scan.
 constexpr uint32_t kGridMinSpheres = 64;
+#ifndef RT_GRID_PER_CELL
+#define RT_GRID_PER_CELL 2.0
+#endif
+#ifndef RT_GRID_REACHES
+#define RT_GRID_REACHES 4.0
+#endif
 constexpr uint32_t kGridMaxDim = 256;
 
 rt_status build_grid(rt_ctx* ctx, const rt_sphere* sp, uint32_t count, hipStream_t stream) {
@@ -231,10 +237,10 @@ rt_status build_grid(rt_ctx* ctx, const rt_sphere* sp, uint32_t count, hipStream
         g_r = std::max(g_r, norm3d(v));
     }
     const double reach = (g_r + rmax) * 1.001;
-    // rays up to 3 reaches from the centre may use the grid
-    const double m = 2.5e-3 * 4.0 * reach * 1.001 + 1e-30;
+    // rays up to RT_GRID_REACHES - 1 reaches from the centre may use the grid
+    const double m = 2.5e-3 * RT_GRID_REACHES * reach * 1.001 + 1e-30;
     const double area = std::max(hi[0] - lo[0], 1e-30) * std::max(hi[2] - lo[2], 1e-30);
-    double s = std::sqrt(area * 2.0 / (double)small.size());
+    double s = std::sqrt(area * RT_GRID_PER_CELL / (double)small.size());
     s = std::max({s, (hi[0] - lo[0]) / (kGridMaxDim - 8), (hi[2] - lo[2]) / (kGridMaxDim - 8),
                   2.0 * rmax / 8.0, 1e-6});
     const double L = norm3d(c) + m / 2.5e-3 + 2.0 * reach + 4.0 * s;

@@ -47,8 +47,8 @@ struct TraceParams {
     const uint32_t* cand_cnt;  // [tile] listed spheres, kCandNone = no list
     const float4* cand_rec;    // [tile][cand_k] their scan records, in index order, padded
     const float4* cand_sph;    // [tile][cand_k][2] their 32-B GpuSphere records
-    // Uniform XZ grid over the small spheres for the bounce rays whose wave cone is too
-    // wide (rt_kernels.hip, scan_grid; built by rt_abi.cpp build_grid): CSR cell lists of
+    // Uniform XZ grid over the small spheres for bounce rays (rt_kernels.hip scan_grid;
+    // built by rt_abi.cpp build_grid): CSR cell lists of
     // sphere indices, every sphere registered in each cell within grid_pad of its centre;
     // grid_big lists the other spheres.  grid_nx == 0: no grid.
     const uint32_t* grid_start;  // [grid_nx * grid_nz + 1]

@@ -300,9 +300,9 @@ __device__ __forceinline__ Hit scan_exhaustive(const float4* __restrict__ geom, 
 // through the exact per-lane test in list order, so the closest-hit result (including
 // the first-index-wins tie rule) is bit-identical to the exhaustive scan.  One sphere
 // per lane is tested against the cone (64 spheres per VALU instruction); survivors are
-// picked from the ballot mask in increasing index order.  Non-finite or degenerate rays,
-// wide cones (theta >~ 60 deg, e.g. diffuse bounces) and short lists use the exhaustive
-// scan instead.
+// picked from the ballot mask in increasing index order.  Bounce rays walk the sphere grid
+// instead when the scene has one (scan_grid below); non-finite or degenerate rays, wide
+// cones (theta >~ 60 deg) and short lists use the exhaustive scan.
 constexpr uint32_t kCullMinSpheres = 32;
 
 // Wave-wide reductions on the VALU: row_ror DPP inside each 16-lane row, then the four
@@ -498,16 +498,19 @@ __device__ __forceinline__ bool grid_usable(const TraceParams& p, v3 o, v3 d, bo
 
 template <bool kLds>
 __device__ __forceinline__ Hit scan_culled(const TraceParams& p, const float4* __restrict__ geom,
-                                           uint32_t count, v3 o, v3 d, bool live) {
+                                           uint32_t count, v3 o, v3 d, bool live, bool bounce) {
     const float4* recs = kLds ? lds_recs : geom;
-    Cone k;
-    if (count < kCullMinSpheres || !wave_cone(o, d, live, k)) {
+    // Bounce rays walk the grid whenever the wave may (measured faster than the cone
+    // culling even for coherent specular waves); camera rays of tiles without a candidate
+    // list keep the cone, whose rays share a narrow beam.
 #ifndef RT_NO_GRID
-        if (count >= kCullMinSpheres && grid_usable(p, o, d, live))
-            return scan_grid(p, o, d, live);
+    if (bounce && count >= kCullMinSpheres && grid_usable(p, o, d, live))
+        return scan_grid(p, o, d, live);
 #endif
+    (void)bounce;
+    Cone k;
+    if (count < kCullMinSpheres || !wave_cone(o, d, live, k))
         return scan_exhaustive<RT_SCAN_CHUNK>(geom, count, o, d);
-    }
     STAMP(2);
     const uint32_t lane = threadIdx.x & 63u;
     const float a = dot(d, d);
@@ -695,8 +698,8 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
             (kScan != kTraceCulled || listed)
                 ? scan_exhaustive<scan_chunk<kScan>(), fast_core<kScan>(1), kScan != kTraceList>(
                       listed ? p.cand_rec + lbase : p.geom, listed ? ncand : p.count, o, d)
-            : p.lds_records ? scan_culled<true>(p, p.geom, p.count, o, d, live)
-                            : scan_culled<false>(p, p.geom, p.count, o, d, live);
+            : p.lds_records ? scan_culled<true>(p, p.geom, p.count, o, d, live, i > 0)
+                            : scan_culled<false>(p, p.geom, p.count, o, d, live, i > 0);
 #endif
         if (kScan != kTraceCulled) STAMP(2);                      // (culled: inside the scan)
         const float4* hs = listed ? p.cand_sph + 2 * lbase : p.sph;
