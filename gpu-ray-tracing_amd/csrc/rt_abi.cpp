@@ -35,8 +35,8 @@ struct rt_ctx {
     double scene_bound = 0.0;
     bool radii_ok = true;
     // XZ grid of the small spheres for bounce rays (build_grid; TraceParams
-    // grid_*): device CSR arrays and the parameters copied into every launch.
-    uint32_t* d_grid = nullptr;     // [cells + 1] starts, then items, then the big list
+    // grid_*): device arrays and the parameters copied into every launch.
+    void* d_grid = nullptr;  // cell ranges (uint2), item records (float4), item indices, big list
     struct Grid {
         uint32_t nx = 0, nz = 0, nbig = 0, items = 0;
         float x0, z0, s, inv_s, ylo, yhi, cx, cy, cz, reach, m, e;
@@ -285,25 +285,37 @@ rt_status build_grid(rt_ctx* ctx, const rt_sphere* sp, uint32_t count, hipStream
     }
     for (uint32_t k = 0; k < cells; ++k) start[k + 1] += start[k];
     const uint32_t items = start[cells];
-    std::vector<uint32_t> buf(cells + 1 + items + big.size());
-    std::copy(start.begin(), start.end(), buf.begin());
+    // one buffer: cells x uint2, items x float4, items x u32, big x u32
+    const size_t geom_off = ((size_t)cells * 8 + 15) & ~(size_t)15;   // float4-aligned
+    const size_t idx_off = geom_off + (size_t)items * 16;
+    const size_t big_off = idx_off + (size_t)items * 4;
+    std::vector<unsigned char> buf(big_off + big.size() * 4 + 16);
+    uint2* rng = reinterpret_cast<uint2*>(buf.data());
+    float4* gg = reinterpret_cast<float4*>(buf.data() + geom_off);
+    uint32_t* gi = reinterpret_cast<uint32_t*>(buf.data() + idx_off);
+    for (uint32_t k = 0; k < cells; ++k) rng[k] = make_uint2(start[k], start[k + 1]);
     std::vector<uint32_t> fill(start.begin(), start.end() - 1);
     for (uint32_t i : small) {
         uint32_t ax, bx, az, bz;
         span(i, ax, bx, az, bz);
+        const float4 rec = make_float4(sp[i].position[0], sp[i].position[1], sp[i].position[2],
+                                       sp[i].radius * sp[i].radius);   // as upload_spheres
         for (uint32_t z = az; z <= bz; ++z)
-            for (uint32_t x = ax; x <= bx; ++x) buf[cells + 1 + fill[z * nx + x]++] = i;
+            for (uint32_t x = ax; x <= bx; ++x) {
+                const uint32_t k = fill[z * nx + x]++;
+                gg[k] = rec;
+                gi[k] = i;
+            }
     }
-    std::copy(big.begin(), big.end(), buf.begin() + cells + 1 + items);
+    std::memcpy(buf.data() + big_off, big.data(), big.size() * 4);
     // The previous grid may still be read by queued launches: order on the stream.
     hipError_t err = hipStreamSynchronize(stream);
     if (err != hipSuccess) return hip_fail(err, "hipStreamSynchronize");
     (void)hipFree(ctx->d_grid);
     ctx->d_grid = nullptr;
-    err = hipMalloc(&ctx->d_grid, buf.size() * sizeof(uint32_t));
+    err = hipMalloc(&ctx->d_grid, buf.size());
     if (err != hipSuccess) return hip_fail(err, "hipMalloc(sphere grid)");
-    err = hipMemcpyAsync(ctx->d_grid, buf.data(), buf.size() * sizeof(uint32_t),
-                         hipMemcpyHostToDevice, stream);
+    err = hipMemcpyAsync(ctx->d_grid, buf.data(), buf.size(), hipMemcpyHostToDevice, stream);
     if (err == hipSuccess) err = hipStreamSynchronize(stream);
     if (err != hipSuccess) return hip_fail(err, "hipMemcpyAsync(sphere grid)");
     rt_ctx::Grid& g = ctx->grid;
@@ -679,10 +691,13 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
         if (rt_status s = ensure_candidates(ctx, p, stream)) return s;
         if (bounces && ctx->grid.nx) {
             const rt_ctx::Grid& g = ctx->grid;
-            const uint32_t cells = g.nx * g.nz;
-            p.grid_start = ctx->d_grid;
-            p.grid_items = ctx->d_grid + cells + 1;
-            p.grid_big = ctx->d_grid + cells + 1 + g.items;
+            const unsigned char* base = static_cast<const unsigned char*>(ctx->d_grid);
+            const size_t cells = (size_t)g.nx * g.nz;
+            p.grid_cells = reinterpret_cast<const uint2*>(base);
+            const size_t geom_off = (cells * 8 + 15) & ~(size_t)15;     // as build_grid
+            p.grid_geom = reinterpret_cast<const float4*>(base + geom_off);
+            p.grid_items = reinterpret_cast<const uint32_t*>(base + geom_off + g.items * 16ull);
+            p.grid_big = p.grid_items + g.items;
             p.grid_nx = g.nx;
             p.grid_nz = g.nz;
             p.grid_nbig = g.nbig;

@@ -48,12 +48,13 @@ struct TraceParams {
     const float4* cand_rec;    // [tile][cand_k] their scan records, in index order, padded
     const float4* cand_sph;    // [tile][cand_k][2] their 32-B GpuSphere records
     // Uniform XZ grid over the small spheres for bounce rays (rt_kernels.hip scan_grid;
-    // built by rt_abi.cpp build_grid): CSR cell lists of
-    // sphere indices, every sphere registered in each cell within grid_pad of its centre;
-    // grid_big lists the other spheres.  grid_nx == 0: no grid.
-    const uint32_t* grid_start;  // [grid_nx * grid_nz + 1]
-    const uint32_t* grid_items;
-    const uint32_t* grid_big;    // ascending sphere indices
+    // built by rt_abi.cpp build_grid): per cell the range of its items, each item a copy
+    // of the sphere's scan record and its index (every small sphere is registered in the
+    // cells near its centre); grid_big lists the other spheres.  grid_nx == 0: no grid.
+    const uint2* grid_cells;     // [grid_nx * grid_nz] (first item, end)
+    const float4* grid_geom;     // [items] scan records (cx, cy, cz, r*r)
+    const uint32_t* grid_items;  // [items] sphere indices
+    const uint32_t* grid_big;    // sphere indices
     uint32_t grid_nx, grid_nz, grid_nbig;
     float grid_x0, grid_z0, grid_s, grid_inv_s;
     float grid_ylo, grid_yhi;    // slab of the gridded spheres, padded

@@ -460,13 +460,11 @@ __device__ __forceinline__ Hit scan_grid(const TraceParams& p, v3 o, v3 d, bool 
     const float dtz = d.z != 0.0f ? p.grid_s / fabsf(d.z) : inf;
     const float slack = 2.0f * p.grid_e * rsqrtf(a) * 1.01f;
     for (int step = 0; step < nx + nz + 2; ++step) {
-        const uint32_t c = (uint32_t)(iz * nx + ix);
-        const uint32_t k1 = p.grid_start[c + 1];
-        for (uint32_t k = p.grid_start[c]; k < k1; ++k) {
-            const uint32_t i = p.grid_items[k];
+        const uint2 range = p.grid_cells[iz * nx + ix];
+        for (uint32_t k = range.x; k < range.y; ++k) {
             float h;
-            const float disc = discriminant(p.geom[i], o, d, a, h);
-            consider_any(disc, h, a, i, tmax, idx);
+            const float disc = discriminant(p.grid_geom[k], o, d, a, h);
+            consider_any(disc, h, a, p.grid_items[k], tmax, idx);
         }
         // A cell entered beyond t1, or beyond the closest hit so far, holds no better hit;
         // slack: the walk's position error (grid_e, as t) and 1e-4 of t.
