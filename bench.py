@@ -160,7 +160,9 @@ def main():
     w, h, kind, nsph, depth, desc = CONFIGS[args.config]
     spheres = rt.SphereCollection.generate(kind, nsph, 1)
     frames = args.warmup + args.steps
-    extra = max(args.exhaustive_steps, args.per_frame_steps)
+    # the side measurements keep accumulating into the same image after the timed frames:
+    # the exhaustive frames first, then the one-launch-per-frame frames (own seeds each)
+    extra = args.exhaustive_steps + args.per_frame_steps
     seeds = rt.frame_seeds(FRAME_SEED, frames + extra)
     # spp cap above every frame this run traces (so no frame is a no-op)
     settings = rt.CameraSettings(max_depth=depth,
@@ -261,7 +263,8 @@ def main():
         pipe.set_frames_per_launch(1)
         q0, q1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         q0.record(stream)
-        r.frames(cam_t, spheres, seeds[frames:frames + args.per_frame_steps])
+        s0 = frames + args.exhaustive_steps
+        r.frames(cam_t, spheres, seeds[s0:s0 + args.per_frame_steps])
         q1.record(stream)
         torch.cuda.synchronize()
         pipe.set_frames_per_launch(0)
