@@ -346,6 +346,11 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
     if (ctx->valid && count == ctx->count &&
         (count == 0 || std::memcmp(ctx->cached.data(), spheres, count * sizeof(rt_sphere)) == 0))
         return RT_OK;  // unchanged since the last upload
+    // From here the device copy no longer matches `cached`: a failure below leaves the
+    // context invalid (the next call uploads again) and retires every scene-derived cache
+    // (candidate lists, tile costs) by bumping the generation.
+    ctx->valid = false;
+    ctx->scene_gen++;
     if (count > ctx->capacity || ctx->d_geom == nullptr) {
         uint32_t cap = ctx->capacity ? ctx->capacity : 64u;
         while (cap < count) cap *= 2u;
@@ -409,7 +414,6 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
     ctx->cached.assign(spheres, spheres + count);
     ctx->count = count;
     ctx->valid = true;
-    ctx->scene_gen++;
     return RT_OK;
 }
 
@@ -650,6 +654,14 @@ void fill_camera(rtk::TraceParams& p, const rt_scene_camera& c) {
         p.ddv[i] = c.defocus_disk_v[i];
     }
     p.defocus_angle = c.defocus_angle;
+    // the defocus disk's eight reciprocals (rt_kernels.hip init_disk_rcp): IEEE sqrtf and a
+    // correctly rounded f64 division, as the device would compute them
+    for (uint32_t k = 0; k < 8u; ++k) {
+        const uint32_t bits = 0x3F7FFFFAu + k;
+        float len2;
+        std::memcpy(&len2, &bits, 4);
+        p.disk_rcp[k] = 1.0 / (double)std::sqrt(len2);
+    }
     p.depth = host_f2u(c.max_depth);
     p.spp = host_f2u(c.samples_per_pixel);
 }

@@ -85,6 +85,9 @@ struct TraceParams {
     // s_memtime duration there, for launch_tile_order.
     const uint32_t* tile_order;
     uint32_t* tile_cost;
+    // RN64(1 / sqrtf(f32 bits 0x3F7FFFFA + k)), k = 0..7: the defocus disk's reciprocal
+    // table (rt_kernels.hip disk_unit), computed on the host
+    double disk_rcp[8];
     uint32_t hint_frames;  // 0 = no hint
     uint32_t hint_n[kHintFrames];
     // RN64(1 / (hint_n[f] + 1)): the accumulator's division by f32(n + 1) as one f64

@@ -46,11 +46,12 @@ __device__ __forceinline__ void stamp(int k) {
         if (k == -2)
             for (int i = 0; i < 8; ++i) s_acc[w][i] = i == 7 ? t : 0;  // [7] = entry time
         if (k == 0 && s_acc[w][6] == 0) s_acc[w][6] = t - s_acc[w][7];  // entry -> 1st ray
+        else if (k == 0) s_acc[w][0] += t - s_last[w];                  // -> later rays
         if (k > 0) s_acc[w][k] += t - s_last[w];
         if (k == 5) s_acc[w][7] = t - s_acc[w][7];                      // lifetime
         s_last[w] = t;
         if (k == 5) {
-            const unsigned gw = (blockIdx.y * gridDim.x + blockIdx.x) * 4u + w;
+            const unsigned gw = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + w;
             if (gw < kStampWaves)
                 for (int i = 0; i < 8; ++i) g_stamp[gw][i] = s_acc[w][i];
         }
@@ -244,6 +245,12 @@ template <bool kScalar>
 __device__ __forceinline__ float4 load_rec(const float4* __restrict__ geom, uint32_t i) {
     if (kScalar) return ((const kconst float4*)geom)[i];
     return geom[i];
+}
+
+// A tile's candidate count through the constant address space: a scalar load (the lists do
+// not change during a launch), not a vector load + readfirstlane.
+__device__ __forceinline__ uint32_t load_cnt(const TraceParams& p, uint32_t tile) {
+    return ((const kconst uint32_t*)p.cand_cnt)[tile];
 }
 
 // kFast: camera rays in the host-proven domain (consider_fast).  kScalar: read the records
@@ -604,6 +611,22 @@ constexpr uint32_t kDiskLen2Lo = 0x3F7FFFFAu;   // 1 - 6 * 2^-24
 __device__ __forceinline__ void init_disk_rcp() {
     if (threadIdx.x < 8u)
         s_disk_rcp[threadIdx.x] = 1.0 / (double)sqrtf(__uint_as_float(kDiskLen2Lo + threadIdx.x));
+}
+// The same table from the launch parameters (the host computes it with the same IEEE
+// operations, rt_abi.cpp fill_camera): eight selects from SGPRs at every wave start instead
+// of a square root and an f64 division.  (The self-test keeps the device computation, and
+// every parity test compares the two through the image bits.)
+__device__ __forceinline__ void init_disk_rcp(const TraceParams& p) {
+    if (threadIdx.x < 8u) {
+        double v = 0.0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8u; ++k) {
+            double dk = p.disk_rcp[k];
+            asm volatile("" : "+s"(dk));   // a scalar (kernarg) value, not a per-lane load
+            if (threadIdx.x == k) v = dk;
+        }
+        s_disk_rcp[threadIdx.x] = v;
+    }
 }
 template <bool kTable>
 __device__ __forceinline__ void disk_unit(float sa, float ca, float& ux, float& uy) {
@@ -999,6 +1022,40 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
 #ifndef RT_WG_WAVES
 #define RT_WG_WAVES 1
 #endif
+// Kernel-argument prefetch (single-frame list instance, one tile per wave): the launch
+// parameters a wave reads are spread over ~12 cache lines of the 2.6-KB kernarg segment and
+// the compiler loads each just before its use — a chain of dependent scalar-cache misses at
+// every wave start.  One scalar load per line, all in flight together and awaited once,
+// brings them into the scalar cache first (K3 single-frame 30.56 -> 30.28 us, K2 23.72 ->
+// 23.40, profiles/r02_ab_single_frame.log).
+#ifndef RT_KARG_PREFETCH
+#define RT_KARG_PREFETCH 1
+#endif
+__device__ __forceinline__ void karg_prefetch() {
+    const void kconst* kp = (const void kconst*)__builtin_amdgcn_kernarg_segment_ptr();
+    uint32_t d0, d1, d2, d3, d4, d5, d6, d7, d8, d9, d10;
+    asm volatile(
+        "s_load_dword %0, %11, 0x0\n\t"
+        "s_load_dword %1, %11, 0x40\n\t"
+        "s_load_dword %2, %11, 0x80\n\t"
+        "s_load_dword %3, %11, 0xc0\n\t"
+        "s_load_dword %4, %11, 0x100\n\t"
+        "s_load_dword %5, %11, 0x140\n\t"
+        "s_load_dword %6, %11, 0x180\n\t"
+        "s_load_dword %7, %11, %12\n\t"
+        "s_load_dword %8, %11, %13\n\t"
+        "s_load_dword %9, %11, %14\n\t"
+        "s_load_dword %10, %11, %15\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(d0), "=&s"(d1), "=&s"(d2), "=&s"(d3), "=&s"(d4), "=&s"(d5), "=&s"(d6),
+          "=&s"(d7), "=&s"(d8), "=&s"(d9), "=&s"(d10)
+        : "s"(kp), "i"(offsetof(TraceParams, hint_n)), "i"(offsetof(TraceParams, hint_rcp)),
+          "i"(offsetof(TraceParams, hint_rs)), "i"(offsetof(TraceParams, seed_b))
+        : "memory");
+    (void)d0; (void)d1; (void)d2; (void)d3; (void)d4; (void)d5;
+    (void)d6; (void)d7; (void)d8; (void)d9; (void)d10;
+}
+
 template <int kScan>
 constexpr uint32_t wg_waves() {
     return kScan == kTraceCulled ? 4u : is_group_kernel(kScan) ? frame_group<kScan>() : RT_WG_WAVES;
@@ -1030,6 +1087,7 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     const TraceParams p) {
     STAMP(-2);
     WAVE_TRACE(0);
+    if (RT_KARG_PREFETCH && kScan == kTraceList) karg_prefetch();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     // The wave index is uniform, but the compiler's divergence analysis does not know it;
@@ -1061,7 +1119,7 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
         __syncthreads();
     }
     if (fast_core<kScan>(16)) {                                   // (disk_unit)
-        init_disk_rcp();
+        init_disk_rcp(p);
         __syncthreads();
     }
     if (!wave_in) return;                                         // whole wave exits
@@ -1069,7 +1127,7 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     cost_start<kScan>(p, tile, wave, lane);
     // the tile's candidate count (kCandNone: no list)
     const uint32_t ncand =
-        (kScan != kTraceExhaustive && p.cand_k) ? p.cand_cnt[tile] : kCandNone;
+        (kScan != kTraceExhaustive && p.cand_k) ? load_cnt(p, tile) : kCandNone;
 #if RT_KO & 8
     const float4 acc = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
 #elif RT_KO & 32

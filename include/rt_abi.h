@@ -81,6 +81,42 @@ typedef struct rt_sphere {
     float color[4];
 } rt_sphere;
 
+/* Compile-time layout locks: the byte offsets a Rust binder's #[repr(C)] structs have
+ * (SceneCamera camera.rs:256-291, GpuSphere sphere.rs:20-26; WGSL wgsl:7-40, 151-155).
+ * Any reordering or resizing of a field fails the build of every translation unit. */
+#if defined(__cplusplus)
+#define RT_STATIC_ASSERT(cond, msg) static_assert(cond, msg)
+#else
+#define RT_STATIC_ASSERT(cond, msg) _Static_assert(cond, msg)
+#endif
+RT_STATIC_ASSERT(sizeof(rt_scene_camera) == 176, "SceneCamera is 176 bytes (camera.rs:256-291)");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, center) == 0, "center @ 0");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, viewport_height) == 12, "viewport_height @ 12");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, viewport_upper_left) == 16, "viewport_upper_left @ 16");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, viewport_width) == 28, "viewport_width @ 28");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, pixel_delta_u) == 32, "pixel_delta_u @ 32");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, defocus_angle) == 44, "defocus_angle @ 44");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, pixel_delta_v) == 48, "pixel_delta_v @ 48");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, aspect_ratio) == 60, "aspect_ratio @ 60");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, defocus_disk_u) == 64, "defocus_disk_u @ 64");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, _padding0) == 76, "_padding0 @ 76");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, viewport_u) == 80, "viewport_u @ 80");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, _padding1) == 92, "_padding1 @ 92");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, defocus_disk_v) == 96, "defocus_disk_v @ 96");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, max_depth) == 108, "max_depth @ 108");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, look_from) == 112, "look_from @ 112");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, samples_per_pixel) == 124, "samples_per_pixel @ 124");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, look_at) == 128, "look_at @ 128");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, camera_has_moved) == 140, "camera_has_moved @ 140");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, vup) == 144, "vup @ 144");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, random_seed) == 156, "random_seed @ 156");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, viewport_v) == 160, "viewport_v @ 160");
+RT_STATIC_ASSERT(offsetof(rt_scene_camera, defocus_radius) == 172, "defocus_radius @ 172");
+RT_STATIC_ASSERT(sizeof(rt_sphere) == 32, "GpuSphere is 32 bytes (sphere.rs:20-26)");
+RT_STATIC_ASSERT(offsetof(rt_sphere, position) == 0, "position @ 0");
+RT_STATIC_ASSERT(offsetof(rt_sphere, radius) == 12, "radius @ 12");
+RT_STATIC_ASSERT(offsetof(rt_sphere, color) == 16, "material.color @ 16");
+
 /* CameraSettings — camera.rs:9-28 (main-world settings the camera builder consumes). */
 typedef struct rt_camera_settings {
     float field_of_view;          /* degrees (camera.rs:37: 20) */
@@ -113,7 +149,11 @@ typedef enum rt_status {
     RT_ERR_INVALID_CONTEXT = 6
 } rt_status;
 
-typedef struct rt_ctx rt_ctx; /* one per device; calls on one ctx are externally serialized */
+/* One context per device; calls on one ctx are externally serialized.  A context keeps
+ * device state that its launches read (sphere records, candidate lists, tile costs): use
+ * ONE stream per context, or synchronize before switching streams — a scene change or a
+ * list rebuild is ordered only on the stream of the call that makes it. */
+typedef struct rt_ctx rt_ctx;
 
 /* Version / introspection ------------------------------------------------------------ */
 RT_API uint32_t rt_abi_version(void); /* RT_ABI_VERSION */

@@ -162,3 +162,28 @@ def test_srgb_thresholds_match_restatement(rt):
     v = t[1:].astype(np.float64)
     enc = np.where(v <= 0.0031308, v * 12.92, 1.055 * v ** (1 / 2.4) - 0.055) * 255
     assert np.all(enc >= np.arange(1, 256) - 0.5 - 1e-9)
+
+
+def test_header_layout_locks_compile_in_c(tmp_path):
+    """include/rt_abi.h carries _Static_assert layout locks (camera.rs:256-291,
+    sphere.rs:20-26): a C translation unit compiles against it with gcc, and one that
+    breaks a lock (a field inserted in a copy of the header) does not."""
+    src = tmp_path / "abi_check.c"
+    src.write_text('#include "rt_abi.h"\nint main(void) { return (int)sizeof(rt_scene_camera) - 176; }\n')
+    ok = subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", str(HEADER.parent), "-c",
+                         str(src), "-o", str(tmp_path / "a.o")], capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stderr
+    broken = tmp_path / "broken"
+    broken.mkdir()
+    text = HEADER.read_text().replace("    float viewport_height;", "    float inserted;\n    float viewport_height;", 1)
+    assert "float inserted;" in text
+    (broken / "rt_abi.h").write_text(text)
+    bad = subprocess.run(["gcc", "-std=c11", "-I", str(broken), "-c", str(src), "-o",
+                          str(tmp_path / "b.o")], capture_output=True, text=True)
+    assert bad.returncode != 0 and "static assert" in bad.stderr.lower()
+    # C++ (the library's own translation units) sees the same locks
+    cpp = tmp_path / "abi_check.cpp"
+    cpp.write_text('#include "rt_abi.h"\nint main() { return 0; }\n')
+    ok = subprocess.run(["g++", "-std=c++17", "-I", str(HEADER.parent), "-c", str(cpp), "-o",
+                         str(tmp_path / "c.o")], capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stderr
