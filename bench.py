@@ -1,35 +1,40 @@
 """Benchmark of the per-pixel ray-tracing hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config K3]   (K=512, W=128)
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config K3]
 
-Workload (default K3 = BASELINE.json configs[2], the config the north-star target is
-quoted on): 1920x1080, seeded 500-sphere scene, max_depth 1.  A "step" is one
-progressive `update` (wgsl:333-364): one camera sample per pixel of this rank's stripe
-bands, read-modify-write of the RGBA32F accumulator in HBM.  With N GPUs (one process per
-GPU, launched by torch.distributed.run) the image is split into 8-row bands dealt
-round-robin, and after the K timed steps the finished tiles are gathered to rank 0 with
-ONE RCCL gather + the de-interleave kernel — both inside the timed region.
+Configs (BASELINE.json `configs`):
+  K2, K3 (default)  1920x1080, 3 / 500 spheres, max_depth 1.  A step is ONE progressive
+                    `update` dispatch (wgsl:333-364) — one launch per frame, the reference's
+                    dispatch structure (lib.rs:408-417): one camera sample per pixel of this
+                    rank's stripe bands, read-modify-write of the RGBA32F accumulator.
+  K4                1920x1080, 500 spheres, 64 spp anti-aliased accumulate, max_depth 1.  A
+                    step is one 64-spp render from a reset accumulator: 64 chained updates
+                    issued by one rt_update_frames call (fused launches of up to 64 frames).
+  K5                3840x2160, 500 spheres, 64 spp, 8 bounces — the multi-GPU config.  A step
+                    is one 64-spp render (bounce instance, one launch per frame).
+With N GPUs (one process per GPU, torch.distributed.run) the image is split into 8-row bands
+dealt round-robin; after the K timed steps the finished tiles are gathered to rank 0 with ONE
+RCCL gather + the de-interleave kernel, both inside the timed region.
 
-The K steps are issued by one rt_update_frames call per rank: at max_depth <= 1 it runs up
-to 64 frames per launch, each wave carrying its pixels' accumulator in registers from frame
-to frame and storing every frame's image to the ping-pong buffers — both buffers end exactly
-as K chained `update` dispatches leave them (tests/test_gpu_parity.py); per_frame_dispatch
-times the same frames with one launch per frame (the reference's dispatch structure).
-
-value = W*H*K camera rays / max-over-ranks wall time (Mrays/s, whole job).
-roofline (trace kernel, average launch time from HIP events): for the default culled scan
-the algorithmic HBM bytes of the reference's progressive update (32 B/pixel/frame, SURVEY
-§8d) against 8 TB/s — the fused launches move 16 B/pixel/frame + 16 B/pixel/launch
-(moved_bytes_per_launch; PMC traffic beside it); for --scan exhaustive the
-algorithmic FP32 work (23 FLOP per ray-sphere test) against the 157.3 TFLOP/s
-FP32 vector peak.  The exhaustive kernel is also timed on the same frames
-(fp32_exhaustive_scan) so both rooflines appear in one line.
-cpu_baseline: the scalar C oracle on one host core over a bounded sample (rank 0, N=1).
+value = W*H*spp_per_step*K camera rays / max-over-ranks wall time (Mrays/s, whole job).
+image_ok: the timed image against committed fixtures (K2/K3: 4096 sampled pixels after W+K
+frames, tests/golden/bench_k*.npz; K4: the full-image SHA-256 of tests/golden/k4.npz; K5:
+the 512 sampled pixels of k5.npz) — null when no fixture covers the run's frame count.
+roofline (the timed trace-kernel launches, HIP events on the stream they run on): the
+algorithmic bytes of the reference's progressive update, 32 B per pixel per launch (16 B
+load + 16 B store of the accumulator), against 8 TB/s; `traffic` = the PMC
+bytes of the same kernel at the same frames per launch (profiles/pmc_r02_<config>.json,
+FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM); `valu` = the binding resource: VALU
+wave-instructions per launch (same PMC file) x 2 cycles (a wave64 VALU op on a SIMD-32) over
+the cycles 1024 SIMDs offer at 2.4 GHz during the measured launch time.
+cpu_baseline: the scalar C oracle on the box's host cores over a bounded sample (rank 0, N=1).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
+import math
 import os
 import sys
 import time
@@ -46,39 +51,50 @@ import gpu_ray_tracing as rt  # noqa: E402
 from gpu_ray_tracing.distributed import StripeRenderer  # noqa: E402
 
 BASELINE = json.loads((ROOT / "BASELINE.json").read_text())
+GOLDEN = ROOT / "tests" / "golden"
 PEAK_FP32_TFLOPS = 157.3      # MI355X FP32 vector peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0         # MI355X HBM3E peak
+CLOCK_GHZ = 2.4               # MI355X max engine clock
+SIMDS = 1024                  # 256 CUs x 4 SIMDs
+VALU_ISSUE_CYCLES = 2         # one wave64 VALU instruction on a SIMD-32
 FLOP_PER_TEST = 23            # oc 3, a 5, h 5, c 7, D 3 (wgsl:183-187)
-BYTES_PER_PIXEL_STEP = 32     # 16 B load + 16 B store (wgsl:339, 363)
+BYTES_PER_PIXEL_LAUNCH = 32   # 16 B load + 16 B store of the accumulator (wgsl:339, 363)
 FRAME_SEED = 0x5EED
+BENCH_SPP = 65536             # the dispatch configs' spp cap (never reached; fixtures agree)
 
 CONFIGS = {
-    # name: (width, height, scene kind, n_spheres, max_depth, description)
-    "K2": (1920, 1080, rt.SCENE_THREE, 3, 1, "configs[1]: 1920x1080, 3 spheres, 1 spp/step"),
-    "K3": (1920, 1080, rt.SCENE_N, 500, 1, "configs[2]: 1920x1080, 500 spheres, 1 spp/step"),
-    "K5": (3840, 2160, rt.SCENE_N, 500, 8, "configs[4]: 3840x2160, 500 spheres, 1 spp/step, 8 bounces"),
+    # name: width, height, scene kind, spheres, max_depth, frames per step, description
+    "K2": (1920, 1080, rt.SCENE_THREE, 3, 1, 1,
+           "configs[1]: 1920x1080, 3 spheres, 1 spp, one update dispatch per step"),
+    "K3": (1920, 1080, rt.SCENE_N, 500, 1, 1,
+           "configs[2]: 1920x1080, 500 spheres, 1 spp, one update dispatch per step"),
+    "K4": (1920, 1080, rt.SCENE_N, 500, 1, 64,
+           "configs[3]: 1920x1080, 500 spheres, 64 spp accumulate per step (fused launches)"),
+    "K5": (3840, 2160, rt.SCENE_N, 500, 8, 64,
+           "configs[4]: 3840x2160, 500 spheres, 64 spp, 8 bounces per step"),
 }
+DEFAULT_STEPS = {"K2": (200, 20), "K3": (200, 20), "K4": (8, 2), "K5": (2, 1)}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults: whole 64-frame launches; the first warmup launch measures the tile costs
-    # the timed launches are scheduled by and the second sorts them (rt_set_tile_order);
-    # 512 timed frames (8 ms on one GPU) amortise the job's single gather at N > 1
-    ap.add_argument("--steps", type=int, default=512)
-    ap.add_argument("--warmup", type=int, default=128)
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--config", default="K3", choices=sorted(CONFIGS))
     ap.add_argument("--scan", default="culled", choices=["culled", "exhaustive"],
-                    help="sphere-list scan: exact wave-level culling (default) or the "
-                         "reference's exhaustive linear walk; images are bit-identical")
-    ap.add_argument("--exhaustive-steps", type=int, default=20,
-                    help="also time the exhaustive-scan kernel for its FP32 roofline")
-    ap.add_argument("--per-frame-steps", type=int, default=20,
-                    help="also time frames with one launch each (the reference's structure)")
+                    help="sphere-list scan: exact culling (default) or the reference's "
+                         "exhaustive linear walk; images are bit-identical")
+    ap.add_argument("--side", type=int, default=20,
+                    help="frames for each side measurement (exhaustive scan, fused frames, "
+                         "moving camera; 0 = none)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="CPU baseline budget in seconds (0 = skip)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    d_steps, d_warm = DEFAULT_STEPS[a.config]
+    a.steps = d_steps if a.steps is None else a.steps
+    a.warmup = d_warm if a.warmup is None else a.warmup
+    return a
 
 
 def host_threads():
@@ -102,13 +118,13 @@ def cpu_model():
 
 
 def cpu_baseline(cam, spheres, w, h, seconds):
-    """The scalar C oracle on the same frame: (i) one thread on a row band
-    sized to ~seconds/3, (ii) host_threads() threads over 8-row bands of whole frames
-    for ~2*seconds/3.  The threaded run is the reported value."""
+    """The scalar C oracle on one update of the same camera and scene: (i) one
+    thread on a row band sized to ~seconds/3, (ii) host_threads() threads over 8-row bands
+    of whole frames for ~2*seconds/3 (at least one frame).  The threaded run is the
+    reported value."""
     from oracle import oracle as O
     img = np.zeros((h, w, 4), np.float32)
     O.lib()
-    # single thread: calibrate on 8 rows through the middle of the image, then size the band
     mid = (h // 2) & ~7
     t0 = time.perf_counter()
     O.update(img, cam.blob, spheres.spheres, rows=(mid, mid + 8))
@@ -118,7 +134,6 @@ def cpu_baseline(cam, spheres, w, h, seconds):
     t0 = time.perf_counter()
     O.update(img, cam.blob, spheres.spheres, rows=(y0, y0 + rows1))
     single = rows1 * w / (time.perf_counter() - t0) / 1e6
-    # threaded: whole frames
     T = host_threads()
     frames = max(1, int(round(2 * seconds / 3 / (w * h / (single * 1e6 * T)))))
     t0 = time.perf_counter()
@@ -128,21 +143,59 @@ def cpu_baseline(cam, spheres, w, h, seconds):
     return {"value": round(w * h * frames / dt / 1e6, 3), "unit": "Mrays/s", "cores": T,
             "kind": "port",
             "sample": f"{frames} full {w}x{h} update(s) on {T} threads (8-row bands from a "
-                      f"queue), {dt:.1f} s; scalar C oracle (oracle/rt_oracle.c, gcc -O3)",
+                      f"queue), {dt:.1f} s; scalar C oracle (oracle/rt_oracle.c, gcc -O3), "
+                      f"max_depth {int(cam.max_depth)}",
             "single_thread": {"value": round(single, 3), "cores": 1,
                               "sample": f"{w}x{rows1} rows of one update"},
             "cpu_model": cpu_model()}
 
 
-def load_pmc(config, frames_per_launch=1):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC passes, if present and taken
-    at the same frames per launch."""
-    p = ROOT / "profiles" / f"pmc_{config}.json"
-    if p.exists():
-        d = json.loads(p.read_text())
-        if d.get("frames_per_launch", 1) == frames_per_launch:
-            return d.get("hbm_bytes_per_launch")
-    return None
+def load_pmc(config, kernel, frames_per_launch):
+    """The committed rocprofv3 PMC summary of the timed kernel (tools/pmc_bench.sh), if it
+    was taken for the same kernel instance at the same frames per launch."""
+    p = ROOT / "profiles" / f"pmc_r02_{config}.json"
+    if not p.exists():
+        return None
+    d = json.loads(p.read_text())
+    if d.get("kernel") != kernel or d.get("frames_per_launch") != frames_per_launch:
+        return None
+    return d
+
+
+def image_check(config, image, frames, cam, w, h):
+    """The timed image against the committed fixtures (see the module docstring)."""
+    if image is None:
+        return None, "not the gathering rank"
+    img = image.detach().cpu().numpy()
+    if config in ("K2", "K3"):
+        g = dict(np.load(GOLDEN / f"bench_{config.lower()}.npz"))
+        if not np.array_equal(g["camera"].view(np.uint32), cam.blob.view(np.uint32)):
+            return False, "camera blob differs from the fixture's"
+        counts = [int(c) for c in g["frame_counts"]]
+        if frames not in counts:
+            return None, f"no fixture for {frames} frames (have {counts})"
+        want = g["pixels"][counts.index(frames)]
+        got = img[g["py"], g["px"]]
+        same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+        return bool(same.all()), f"{want.shape[0]} sampled pixels after {frames} frames"
+    g = dict(np.load(GOLDEN / f"{config.lower()}.npz"))
+    if "sha256" in g:
+        ok = hashlib.sha256(np.ascontiguousarray(img, np.float32).tobytes()).hexdigest() == \
+            str(g["sha256"])
+        return ok, "full-image SHA-256 of the 64-spp render"
+    got = img[g["py"], g["px"]]
+    want = g["pixels"]
+    same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+    return bool(same.all()), f"{want.shape[0]} sampled pixels of the 64-spp render"
+
+
+def timed(stream, fn):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3
 
 
 def main():
@@ -157,172 +210,193 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    w, h, kind, nsph, depth, desc = CONFIGS[args.config]
-    spheres = rt.SphereCollection.generate(kind, nsph, 1)
-    frames = args.warmup + args.steps
-    # the side measurements keep accumulating into the same image after the timed frames:
-    # the exhaustive frames first, then the one-launch-per-frame frames (own seeds each)
-    extra = args.exhaustive_steps + args.per_frame_steps
-    seeds = rt.frame_seeds(FRAME_SEED, frames + extra)
-    # spp cap above every frame this run traces (so no frame is a no-op)
-    settings = rt.CameraSettings(max_depth=depth,
-                                 samples_per_pixel=max(500, frames + extra))
-    cam0 = rt.SceneCamera.from_settings(settings, w, h, float(seeds[0]))
-    cams = [cam0.with_fields(camera_has_moved=1.0 if f == 0 else 0.0) for f in range(2)]
+    cfg = args.config
+    w, h, kind, nsph, depth, spf, desc = CONFIGS[cfg]
+    dispatch = spf == 1
+    if dispatch:
+        # progressive frames: frame 0 resets, one seed per frame
+        spheres = rt.SphereCollection.generate(kind, nsph, 1)
+        seeds = rt.frame_seeds(FRAME_SEED, args.warmup + args.steps + 3 * args.side)
+        settings = rt.CameraSettings(max_depth=depth, samples_per_pixel=BENCH_SPP)
+        cam0 = rt.SceneCamera.from_settings(settings, w, h, float(seeds[0]))
+        cam_t = cam0.with_fields(camera_has_moved=0.0)
+    else:
+        # every step renders the golden 64-spp image from a reset accumulator
+        g = dict(np.load(GOLDEN / f"{cfg.lower()}.npz"))
+        spheres = rt.SphereCollection(g["spheres"])
+        seeds = g["seeds"]
+        cam0 = cam_t = rt.SceneCamera(g["camera"])
+        assert cam0.camera_has_moved > 0.5 and len(seeds) == spf
 
     pipe = rt.ComputeShaderPipeline(local_rank)
     pipe.set_scan_mode(args.scan)
     pipe.set_spheres(spheres)
+    if dispatch:
+        pipe.set_frames_per_launch(1)          # one `update` launch per frame
     r = StripeRenderer(pipe, w, h, rank, world)
     stream = torch.cuda.current_stream()
+    local_px = w * min(r.rows, h)
 
-    # warmup (untimed) — frame 0 resets the accumulator (camera_has_moved = 1)
+    def step_block(n, first):
+        if dispatch:
+            off = 0 if first else args.warmup
+            r.frames(cam0 if first else cam_t, spheres, seeds[off:off + n])
+        else:
+            for _ in range(n):
+                r.frames(cam0, spheres, seeds)
+
+    # warmup (untimed); the dispatch configs' frame 0 resets the accumulator
     if args.warmup:
-        r.frames(cams[0], spheres, seeds[:args.warmup])
+        step_block(args.warmup, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
 
-    # timed: `steps` progressive frames = `steps` update dispatches issued by one C call
-    # (rt_update_frames), then the single gather of the finished tiles.
-    cam_t = cams[min(1, frames - 1)]          # camera_has_moved = 0 from here on
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # timed: K steps issued by rt_update_frames, then the single gather of the tiles
     t0 = time.perf_counter()
+    ev0, ev1, ev2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
     ev0.record(stream)
-    r.frames(cam_t, spheres, seeds[args.warmup:frames])
+    step_block(args.steps, args.warmup == 0)
     ev1.record(stream)
     image = r.finish()
-    ev2 = torch.cuda.Event(enable_timing=True)
     ev2.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    # breakdown (HIP events on this rank's stream): the K frames, then the gather +
-    # de-interleave; both stay inside dt
+    info = pipe.last_launch_info()             # the last timed rt_update_frames call
     render_s, gather_s = ev0.elapsed_time(ev1) / 1e3, ev1.elapsed_time(ev2) / 1e3
     if world > 1:
         t = torch.tensor([dt, render_s, gather_s], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, render_s, gather_s = (float(x) for x in t.tolist())
+    frames_total = (args.warmup + args.steps) if dispatch else spf
+    image_ok, image_what = image_check(cfg, image, frames_total, cam0, w, h)
 
-    # every pixel of the gathered image must hold exactly warmup + steps samples
-    sample_ok = image is not None and bool(torch.all(image[..., 3] == frames).item())
-    # HIP events around the timed dispatches: per step and per launch, gaps included
-    fpl = r.frames_per_launch(cam_t)
-    launches = -(-args.steps // fpl)
-    step_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
-    launch_s = ev0.elapsed_time(ev1) / 1e3 / launches
-    local_px = w * min(r.rows, h)
-    # SURVEY §8d algorithmic units: the reference's exhaustive scan does N tests of 23 FLOP
-    # per segment; at max_depth 1 every sample is exactly one segment.
-    flops = local_px * nsph * FLOP_PER_TEST if depth == 1 else None
-    hbm_bytes = local_px * BYTES_PER_PIXEL_STEP
-    value = w * h * args.steps / dt / 1e6
+    # dispatch configs: the timed steps are ONE rt_update_frames call (one launch per
+    # frame); 64-spp configs: one call per step, all alike
+    total_launches = info["launches"] * (1 if dispatch else args.steps)
+    launches_per_step = total_launches / args.steps
+    launch_s = ev0.elapsed_time(ev1) / 1e3 / max(1, total_launches)
+    value = w * h * spf * args.steps / dt / 1e6
 
-    # The exhaustive (reference-algorithm) kernel on the same frames, for its FP32 roofline.
-    exh = None
-    if args.scan == "culled" and flops and args.exhaustive_steps > 0:
-        pipe.set_scan_mode("exhaustive")
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        r.frames(cam_t, spheres, seeds[frames:frames + args.exhaustive_steps])
-        e1.record(stream)
-        torch.cuda.synchronize()
-        pipe.set_scan_mode(args.scan)
-        t_exh = e0.elapsed_time(e1) / 1e3 / args.exhaustive_steps
-        exh = {"kernel_avg_us": round(t_exh * 1e6, 2),
-               "achieved": round(flops / t_exh / 1e12, 3), "peak": PEAK_FP32_TFLOPS,
-               "unit": "TFLOP/s", "frac": round(flops / t_exh / 1e12 / PEAK_FP32_TFLOPS, 4),
-               "flop_per_launch": flops,
-               "speedup_of_culled": round(t_exh / step_s, 2)}
+    # roofline of the timed trace kernel
+    kernel = info["kernel_name"]
+    fpl = info["max_frames_per_launch"]
+    bytes_launch = local_px * BYTES_PER_PIXEL_LAUNCH
+    pmc = load_pmc(cfg, kernel, fpl) if world == 1 else None
+    roof = {"bound": "hbm", "achieved": round(bytes_launch / launch_s / 1e9, 1),
+            "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(bytes_launch / launch_s / 1e9 / PEAK_HBM_GBS, 4),
+            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+            "kernel": kernel, "kernel_avg_us": round(launch_s * 1e6, 2),
+            "frames_per_launch": fpl, "launches_per_step": launches_per_step,
+            "algorithmic_bytes_per_launch": bytes_launch,
+            "binding": "valu"}
+    if pmc and pmc.get("valu_insts_per_launch"):
+        insts = pmc["valu_insts_per_launch"]
+        avail = SIMDS * CLOCK_GHZ * 1e9 * launch_s
+        roof["valu"] = {"insts_per_launch": insts,
+                        "issue_cycles": insts * VALU_ISSUE_CYCLES,
+                        "available_cycles": round(avail),
+                        "frac": round(insts * VALU_ISSUE_CYCLES / avail, 4),
+                        "pmc": f"profiles/pmc_r02_{cfg}.json",
+                        "rule": "VALU wave-instructions x 2 cycles / (1024 SIMDs x 2.4 GHz x "
+                                "kernel_avg_us)"}
 
-    # Presentation kernel on the gathered image: 16 B read + 4 B written per
-    # pixel, HBM-bound.
-    present = None
-    if image is not None:
-        out8 = torch.empty((h, w, 4), dtype=torch.uint8, device=image.device)
-        pipe.present(image, w, h, "srgb", out8)
-        p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        p0.record(stream)
-        for _ in range(20):
+    line = {
+        "metric": BASELINE["metric"],
+        "value": round(value, 2),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded scene + per-frame seeds; SURVEY §8d)",
+        "config": {"workload": f"{cfg} {desc}, max_depth {depth}",
+                   "width": w, "height": h, "spheres": nsph, "spp_per_step": spf,
+                   "max_depth": depth, "parallelism": f"stripes{world}",
+                   "scan": args.scan, "kernel": kernel},
+        "roofline": roof,
+        "image_ok": image_ok,
+        "image_check": image_what,
+        # max over ranks; value's time includes both (and the barriers)
+        "timed_breakdown_ms": {"steps": round(render_s * 1e3, 4),
+                               "gather_and_deinterleave": round(gather_s * 1e3, 4)},
+    }
+
+    # ---- side measurements (after the timed region and its image check) -------------
+    side = {}
+    if args.side > 0 and world == 1:
+        base = args.warmup + args.steps
+        if dispatch and depth == 1:
+            # the reference algorithm (exhaustive scan) on further frames: its FP32 roofline
+            pipe.set_scan_mode("exhaustive")
+            t_exh = timed(stream, lambda: r.frames(cam_t, spheres, seeds[base:base + args.side]))
+            t_exh /= args.side
+            pipe.set_scan_mode(args.scan)
+            flops = local_px * nsph * FLOP_PER_TEST
+            side["fp32_exhaustive_scan"] = {
+                "kernel": pipe.last_launch_info()["kernel_name"],
+                "us_per_frame": round(t_exh * 1e6, 2),
+                "achieved": round(flops / t_exh / 1e12, 3), "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(flops / t_exh / 1e12 / PEAK_FP32_TFLOPS, 4),
+                "flop_per_frame": flops}
+            # the same frames fused (up to 64 per launch; K4's launches)
+            pipe.set_frames_per_launch(0)
+            s1 = base + args.side
+            t_f = timed(stream, lambda: r.frames(cam_t, spheres, seeds[s1:s1 + args.side]))
+            fi = pipe.last_launch_info()
+            pipe.set_frames_per_launch(1)
+            side["fused_frames"] = {"kernel": fi["kernel_name"],
+                                    "frames_per_launch": fi["max_frames_per_launch"],
+                                    "us_per_frame": round(t_f / args.side * 1e6, 2),
+                                    "Mrays_per_s": round(local_px * args.side / t_f / 1e6, 1)}
+            # moving camera: every frame a new camera (the reference's WASD movement resets
+            # the accumulator, camera.rs:243-252, wgsl:345-350): candidate lists rebuilt
+            # every frame, one update dispatch each
+            a, b = r.buf[0], r.buf[1]
+            cams = []
+            for f in range(args.side):
+                ang = math.radians(0.05 * (f + 1))
+                st = rt.CameraSettings(max_depth=depth, samples_per_pixel=BENCH_SPP,
+                                       look_from=(13.0 * math.cos(ang) - 3.0 * math.sin(ang),
+                                                  2.0, 13.0 * math.sin(ang) + 3.0 * math.cos(ang)))
+                cams.append(rt.SceneCamera.from_settings(st, w, h, float(seeds[f])))
+
+            def cold():
+                nonlocal a, b
+                for c in cams:
+                    pipe.update(a, b, w, h, c, spheres)
+                    a, b = b, a
+            t_c = timed(stream, cold) / args.side
+            side["cold_camera"] = {"us_per_frame": round(t_c * 1e6, 2),
+                                   "Mrays_per_s": round(local_px / t_c / 1e6, 1),
+                                   "what": "a new camera every frame: candidate-list build "
+                                           "(rt_candidates_kernel) + one update, reset "
+                                           "accumulator; host issue included"}
+        # presentation kernel on the final image: 16 B read + 4 B written/px
+        if image is not None:
+            out8 = torch.empty((h, w, 4), dtype=torch.uint8, device=image.device)
             pipe.present(image, w, h, "srgb", out8)
-        p1.record(stream)
-        torch.cuda.synchronize()
-        t_p = p0.elapsed_time(p1) / 1e3 / 20
-        present = {"kernel": "rt_present_kernel<srgb>", "avg_us": round(t_p * 1e6, 2),
-                   "achieved": round(w * h * 20 / t_p / 1e9, 1), "peak": PEAK_HBM_GBS,
-                   "unit": "GB/s", "frac": round(w * h * 20 / t_p / 1e9 / PEAK_HBM_GBS, 4),
-                   "bytes_per_launch": w * h * 20}
-
-    # The reference's dispatch structure on the same frames: one launch per frame.
-    per_frame = None
-    if fpl > 1 and args.per_frame_steps > 0:
-        pipe.set_frames_per_launch(1)
-        q0, q1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        q0.record(stream)
-        s0 = frames + args.exhaustive_steps
-        r.frames(cam_t, spheres, seeds[s0:s0 + args.per_frame_steps])
-        q1.record(stream)
-        torch.cuda.synchronize()
-        pipe.set_frames_per_launch(0)
-        t_pf = q0.elapsed_time(q1) / 1e3 / args.per_frame_steps
-        per_frame = {"frames_per_launch": 1, "us_per_step": round(t_pf * 1e6, 2),
-                     "Mrays_per_s": round(local_px / t_pf / 1e6, 1),
-                     "hbm_frac": round(hbm_bytes / t_pf / 1e9 / PEAK_HBM_GBS, 4)}
-
-    avg_frames = args.steps / launches
-    if args.scan == "exhaustive" and flops:
-        roof = {"bound": "valu", "achieved": round(flops / step_s / 1e12, 3),
-                "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(flops / step_s / 1e12 / PEAK_FP32_TFLOPS, 4),
-                "traffic": load_pmc(f"{args.config}_exhaustive", fpl),
-                "kernel_avg_us": round(launch_s * 1e6, 2), "frames_per_launch": fpl,
-                "flop_per_launch": round(flops * avg_frames)}
-    else:
-        # Culled scan: the redundant ray-sphere tests are gone (exactly), so
-        # the algorithm-independent unit left is the progressive update's 32 B/pixel.
-        roof = {"bound": "hbm", "achieved": round(hbm_bytes / step_s / 1e9, 1),
-                "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(hbm_bytes / step_s / 1e9 / PEAK_HBM_GBS, 4),
-                "traffic": load_pmc(f"{args.config}_culled", fpl),
-                "kernel_avg_us": round(launch_s * 1e6, 2), "frames_per_launch": fpl,
-                "bytes_per_launch": round(hbm_bytes * avg_frames),
-                "moved_bytes_per_launch": round(local_px * 16 * (avg_frames + 1)),
-                "us_per_step": round(step_s * 1e6, 2)}
+            t_p = timed(stream, lambda: [pipe.present(image, w, h, "srgb", out8)
+                                         for _ in range(20)]) / 20
+            side["present_rgba8"] = {"kernel": "rt_present_kernel<srgb>",
+                                     "avg_us": round(t_p * 1e6, 2),
+                                     "achieved": round(w * h * 20 / t_p / 1e9, 1),
+                                     "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                     "frac": round(w * h * 20 / t_p / 1e9 / PEAK_HBM_GBS, 4)}
+    line.update(side)
 
     if rank == 0:
-        line = {
-            "metric": BASELINE["metric"],
-            "value": round(value, 2),
-            "unit": "Mrays/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 5),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (seeded scene + per-frame seeds; SURVEY §8d)",
-            "config": {"workload": f"{args.config} {desc}, max_depth {depth}",
-                       "width": w, "height": h, "spheres": nsph, "spp_per_step": 1,
-                       "max_depth": depth, "parallelism": f"stripes{world}",
-                       "scan": args.scan,
-                       "kernel": rt._lib.lib().rt_kernel_name(0).decode()},
-            "roofline": roof,
-            "fp32_exhaustive_scan": exh,
-            "present_rgba8": present,
-            "per_frame_dispatch": per_frame,
-            "accumulated_spp_ok": sample_ok,
-            # max over ranks; value's time includes both (and the barriers)
-            "timed_breakdown_ms": {"frames": round(render_s * 1e3, 4),
-                                   "gather_and_deinterleave": round(gather_s * 1e3, 4)},
-        }
         if world == 1 and args.cpu_seconds > 0:
-            line["cpu_baseline"] = cpu_baseline(cams[0], spheres, w, h, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(cam0, spheres, w, h, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -71,6 +71,7 @@ struct rt_ctx {
     };
     std::vector<CountRecord> counts;
     uint32_t frames_per_launch = 0;  // rt_update_frames fusion cap (0 = automatic)
+    rt_launch_info last = {0, 0, 0, -1};  // the last call's launches (rt_last_launch_info)
     int frame_pairs = RT_FRAME_PAIRS_AUTO;
 };
 
@@ -730,6 +731,13 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
     return RT_OK;
 }
 
+void note_launch(rt_ctx* ctx, int kernel, uint32_t frames) {
+    ctx->last.launches++;
+    ctx->last.frames += frames;
+    ctx->last.max_frames_per_launch = std::max(ctx->last.max_frames_per_launch, frames);
+    ctx->last.kernel = kernel;
+}
+
 // Shared body of rt_update / rt_render / rt_render_stripes: `frames` accumulated in
 // launches of up to kMaxFramesPerLaunch frames each.
 rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h,
@@ -747,6 +755,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         return s;
     const float4* src = reinterpret_cast<const float4*>(in);
     float4* dst = reinterpret_cast<float4*>(out);
+    ctx->last = {0, 0, 0, -1};
     for (uint32_t f0 = 0; f0 < frames; f0 += rtk::kMaxFramesPerLaunch) {
         const uint32_t nf = std::min<uint32_t>(frames - f0, rtk::kMaxFramesPerLaunch);
         p.in = src;
@@ -760,6 +769,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         finish_tile_order(ctx, p);
+        note_launch(ctx, kernel, nf);
         src = dst;  // later launches continue the accumulation in place
     }
     return RT_OK;
@@ -774,8 +784,18 @@ uint32_t rt_abi_version(void) { return RT_ABI_VERSION; }
 const char* rt_last_error(void) { return g_last_error.c_str(); }
 
 const char* rt_kernel_name(int which) {
-    (void)which;
+    static const char* const names[] = {"rt_trace_kernel<0>", "rt_trace_kernel<1>",
+                                        "rt_trace_kernel<2>", "rt_trace_kernel<3>",
+                                        "rt_trace_kernel<4>"};
+    if (which >= 0 && which < (int)(sizeof(names) / sizeof(names[0]))) return names[which];
     return rtk::trace_kernel_name();
+}
+
+rt_status rt_last_launch_info(const rt_ctx* ctx, rt_launch_info* out) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!out) return fail(RT_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = ctx->last;
+    return RT_OK;
 }
 
 rt_status rt_create(int device, rt_ctx** out_ctx) {
@@ -917,6 +937,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
     // camera-ray-only kernel (1 = one dispatch per frame, the reference's structure).
     const uint32_t per = frames_per_launch_for(ctx, p);
     int cur = 0;
+    ctx->last = {0, 0, 0, -1};
     for (uint32_t f0 = 0; f0 < frames; f0 += per) {
         const uint32_t nf = std::min<uint32_t>(per, frames - f0);
         p.in = img[cur];
@@ -955,6 +976,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         finish_tile_order(ctx, p);
+        note_launch(ctx, kernel, nf);
         // frame f of the launch wrote img[(cur + 1 + f) % 2]
         const int newest = (nf & 1u) ? 1 - cur : cur;
         if (known) {

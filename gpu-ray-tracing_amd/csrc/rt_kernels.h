@@ -109,6 +109,10 @@ constexpr int kTraceListPair = 3;
 // The same with four waves per tile: for small per-rank shares (few tiles per SIMD), where
 // shorter per-wave frame chains keep more waves resident (rt_abi.cpp picks it).
 constexpr int kTraceListQuad = 4;
+static_assert(kTraceExhaustive == RT_KERNEL_EXHAUSTIVE && kTraceCulled == RT_KERNEL_CULLED &&
+                  kTraceList == RT_KERNEL_LIST && kTraceListPair == RT_KERNEL_LIST_PAIR &&
+                  kTraceListQuad == RT_KERNEL_LIST_QUAD,
+              "instance ids are the ABI's RT_KERNEL_* values");
 constexpr bool is_group_kernel(int k) { return k == kTraceListPair || k == kTraceListQuad; }
 constexpr bool is_list_kernel(int k) { return k == kTraceList || is_group_kernel(k); }
 // Tiles per launch at or below which frame groups of four are used.

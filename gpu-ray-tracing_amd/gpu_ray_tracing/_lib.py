@@ -117,7 +117,14 @@ _SIGS = {
     "rt_get_frames_per_launch": (ctypes.c_int, [P, P, ctypes.POINTER(U32)]),
     "rt_set_frame_pairs": (ctypes.c_int, [P, ctypes.c_int]),
     "rt_set_tile_order": (ctypes.c_int, [P, ctypes.c_int]),
+    "rt_last_launch_info": (ctypes.c_int, [P, P]),
 }
+
+
+class LaunchInfoC(ctypes.Structure):
+    """rt_launch_info (rt_abi.h)."""
+    _fields_ = [("launches", U32), ("frames", U32), ("max_frames_per_launch", U32),
+                ("kernel", ctypes.c_int32)]
 
 _lib = None
 

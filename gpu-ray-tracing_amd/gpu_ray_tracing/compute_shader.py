@@ -86,6 +86,15 @@ class ComputeShaderPipeline:
         _lib.call("rt_get_frames_per_launch", self._ctx, ctypes.byref(cam), ctypes.byref(out))
         return int(out.value)
 
+    def last_launch_info(self) -> dict:
+        """rt_last_launch_info: what the last trace call launched — launches, frames,
+        max_frames_per_launch, kernel (RT_KERNEL_* id) and its rocprofv3 name."""
+        info = _lib.LaunchInfoC()
+        _lib.call("rt_last_launch_info", self._ctx, ctypes.byref(info))
+        d = {k: int(getattr(info, k)) for k, _ in info._fields_}
+        d["kernel_name"] = _lib.lib().rt_kernel_name(d["kernel"]).decode()
+        return d
+
     def selftest_fastmath(self, n_random: int = 1 << 26) -> list[int]:
         """rt_selftest_fastmath: [defocus, division, sqrt, root-selection mismatches,
         cases run]."""

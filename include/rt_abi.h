@@ -160,8 +160,28 @@ RT_API uint32_t rt_abi_version(void); /* RT_ABI_VERSION */
 #define RT_ABI_VERSION 1u
 /* Text of the last error on this thread (never NULL). */
 RT_API const char* rt_last_error(void);
-/* Kernel variant names for profiling/bench labelling; `which` 0 = update, 1 = render. */
+/* Trace-kernel instances (rt_launch_info.kernel) and their names as rocprofv3 lists them
+ * (rt_kernel_name).  The library picks the instance per launch: the reference's exhaustive
+ * scan, the culled scan (bounce rays), the camera-ray-only instance with candidate lists
+ * (max_depth <= 1; one wave per tile), and its frame groups of two / four waves per tile
+ * (fused multi-frame launches). */
+#define RT_KERNEL_EXHAUSTIVE 0
+#define RT_KERNEL_CULLED 1
+#define RT_KERNEL_LIST 2
+#define RT_KERNEL_LIST_PAIR 3
+#define RT_KERNEL_LIST_QUAD 4
+/* "rt_trace_kernel<k>" for an instance k above, "rt_trace_kernel" otherwise. */
 RT_API const char* rt_kernel_name(int which);
+/* What the last rt_update / rt_render / rt_render_stripes / rt_update_frames call on this
+ * context launched: trace launches, frames traced, the most frames one launch carried and
+ * the instance of its last launch (RT_KERNEL_*, -1 before any launch). */
+typedef struct rt_launch_info {
+    uint32_t launches;
+    uint32_t frames;
+    uint32_t max_frames_per_launch;
+    int32_t kernel;
+} rt_launch_info;
+RT_API rt_status rt_last_launch_info(const rt_ctx* ctx, rt_launch_info* out);
 
 /* Context ---------------------------------------------------------------------------- */
 /* Create a context on HIP device `device`.  Replaces ComputeShaderPipeline::from_world

@@ -121,6 +121,79 @@ def test_golden_k4_fused_64spp(rt, pipe):
     assert hashlib.sha256(img.tobytes()).hexdigest() == str(g["sha256"])
 
 
+@pytest.mark.parametrize("pairs", ["auto", "quad"])
+def test_bench_k4_launches_match_golden(rt, pairs):
+    """The kernel bench.py --config K4 times, at the timed size: rt_update_frames of 64
+    frames from a reset at 1920x1080 / 500 spheres (AUTO: frame pairs, kTraceListPair; the
+    first launch records tile costs, the second runs cost-ordered tiles).  Both launches'
+    newest image hashes to k4.npz's, the other buffer holds frame 63."""
+    g = load_golden("k4.npz")
+    w, h = int(g["width"]), int(g["height"])
+    cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
+    p = rt.ComputeShaderPipeline(0)
+    p.set_frame_pairs(pairs)
+    try:
+        a, b = p.new_image(w, h), p.new_image(w, h)
+        for launch in range(2):
+            newest = p.update_frames(a, b, w, h, cam, sc, g["seeds"])
+            info = p.last_launch_info()
+            assert info["launches"] == 1 and info["max_frames_per_launch"] == 64
+            assert info["kernel_name"] == ("rt_trace_kernel<3>" if pairs == "auto"
+                                           else "rt_trace_kernel<4>")
+            img = host(b if newest == 1 else a)
+            assert hashlib.sha256(img.tobytes()).hexdigest() == str(g["sha256"]), launch
+            other = host(a if newest == 1 else b)
+            assert np.all(other[..., 3] == 63)
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("cfg", ["k2", "k3"])
+def test_bench_dispatch_chain_matches_fixture(rt, cfg):
+    """bench.py --config K2/K3's timed structure: one update launch per frame
+    (rt_set_frames_per_launch(1)), 5 + 20 frames from a reset at 1920x1080 (the driver's
+    --warmup 5 --steps 20), checked against the oracle's sampled pixels
+    (tests/golden/bench_k*.npz)."""
+    g = load_golden(f"bench_{cfg}.npz")
+    w, h = int(g["width"]), int(g["height"])
+    cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
+    p = rt.ComputeShaderPipeline(0)
+    p.set_frames_per_launch(1)
+    try:
+        a, b = p.new_image(w, h), p.new_image(w, h)
+        n0 = p.update_frames(a, b, w, h, cam, sc, g["seeds"][:5])
+        if n0 == 1:
+            a, b = b, a
+        newest = p.update_frames(a, b, w, h, cam.with_fields(camera_has_moved=0.0), sc,
+                                 g["seeds"][5:25])
+        info = p.last_launch_info()
+        assert info["launches"] == 20 and info["max_frames_per_launch"] == 1
+        assert info["kernel_name"] == "rt_trace_kernel<2>"
+        img = host(b if newest == 1 else a)
+        k = list(g["frame_counts"]).index(25)
+        assert_same(img[g["py"], g["px"]], g["pixels"][k])
+    finally:
+        p.close()
+
+
+def test_bench_k5_launches_match_golden(rt):
+    """bench.py --config K5's timed structure on one GPU: rt_update_frames of 64 frames
+    (bounce instance, one launch per frame) at 3840x2160, depth 8, sampled pixels."""
+    g = load_golden("k5.npz")
+    w, h = int(g["width"]), int(g["height"])
+    p = rt.ComputeShaderPipeline(0)
+    try:
+        a, b = p.new_image(w, h), p.new_image(w, h)
+        newest = p.update_frames(a, b, w, h, rt.SceneCamera(g["camera"]),
+                                 rt.SphereCollection(g["spheres"]), g["seeds"])
+        info = p.last_launch_info()
+        assert info["frames"] == 64 and info["kernel_name"] == "rt_trace_kernel<1>"
+        img = host(b if newest == 1 else a)
+        assert_same(img[g["py"], g["px"]], g["pixels"])
+    finally:
+        p.close()
+
+
 def test_golden_k5_sampled(rt, pipe):
     """configs[4] shape on one GPU: 3840x2160, 500 spheres, 64 spp, depth 8 (sampled)."""
     g = load_golden("k5.npz")

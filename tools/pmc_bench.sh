@@ -1,0 +1,26 @@
+#!/bin/bash
+# PMC summaries of the timed trace kernel of `bench.py --config CFG` (the kernel instance and
+# frames per launch the bench line reports): FETCH_SIZE and WRITE_SIZE in separate passes
+# (MI355X_MICROARCH.md §HBM), then one SQ/GRBM group.  Writes gpurun_out/TAG/pmc_r02_CFG.json
+# (copy to profiles/ to have bench.py report `traffic` and `roofline.valu` from it).
+# Usage: bash tools/pmc_bench.sh TAG "K3 K2 K4 K5"
+set -o pipefail
+TAG=$1; CFGS=$2
+cd $GRAFT_REPO_ROOT; O=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $O
+export TMPDIR=/tmp
+for c in $CFGS; do
+  ARGS="--config $c --side 0 --cpu-seconds 0"
+  [ "$c" = "K5" ] && ARGS="$ARGS --steps 1 --warmup 1"
+  timeout -k 10 300 python3 bench.py $ARGS > $O/pmc_bench_$c.json 2> $O/pmc_bench_$c.err \
+    || { echo "bench $c failed"; tail -3 $O/pmc_bench_$c.err; exit 1; }
+  K=$(python3 -c "import json; print(json.loads(open('$O/pmc_bench_$c.json').read())['roofline']['kernel'])")
+  F=$(python3 -c "import json; print(json.loads(open('$O/pmc_bench_$c.json').read())['roofline']['frames_per_launch'])")
+  i=0
+  for CS in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    timeout -k 10 300 rocprofv3 --pmc $CS --output-format csv -d $O/raw -o ${c}_p$i -- python3 bench.py $ARGS \
+      > $O/pmc_${c}_p$i.log 2>&1 || { echo "pmc $c pass $i failed"; tail -5 $O/pmc_${c}_p$i.log; exit 1; }
+  done
+  python3 tools/pmc_bench_summary.py $O/pmc_r02_$c.json "$K" "$F" $O/raw/${c}_p1_counter_collection.csv \
+    $O/raw/${c}_p2_counter_collection.csv $O/raw/${c}_p3_counter_collection.csv || exit 1
+done
