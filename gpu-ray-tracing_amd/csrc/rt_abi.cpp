@@ -57,6 +57,7 @@ struct rt_ctx {
     uint32_t cost_frames = 0;       // frames of the launch that measured it
     uint64_t order_gen = ~0ull;     // cand_gen tile_order was derived for
     uint32_t order_frames = 0;      // frames of the measurement it came from
+    bool cost_groups = false;       // tile_cost/tile_order count bounce workgroups, not tiles
     int tile_order_mode = RT_TILE_ORDER_AUTO;
     float* d_srgb = nullptr;  // rt_srgb_thresholds table on the device (256 floats)
     // hash(x*73) for x < hx_len and hash(y*51) for y < hy_len (wgsl:309-310)
@@ -72,6 +73,7 @@ struct rt_ctx {
     std::vector<CountRecord> counts;
     uint32_t frames_per_launch = 0;  // rt_update_frames fusion cap (0 = automatic)
     rt_launch_info last = {0, 0, 0, -1};  // the last call's launches (rt_last_launch_info)
+    int path_compaction = RT_PATHS_PER_WAVE;
     int frame_pairs = RT_FRAME_PAIRS_AUTO;
 };
 
@@ -169,13 +171,18 @@ int trace_kernel_for(const rt_ctx* ctx, const rtk::TraceParams& p) {
 #ifndef RT_FORCE_CULLED_KERNEL
     if (p.depth <= 1u && camera_rays_bounded(ctx, p)) return rtk::kTraceList;
 #endif
+#ifndef RT_NO_BOUNCE_KERNEL
+    // bounce rays: paths compacted across the workgroup after every bounce
+    if (p.depth >= 2u) return rtk::kTraceBounce;
+#endif
     return rtk::kTraceCulled;
 }
 
 // Frames per rt_update_frames launch (see rt_update_frames).  Only the camera-ray-only
 // instance has the per-frame stores (rt_kernels.hip, kStoreEach).
 uint32_t frames_per_launch_for(const rt_ctx* ctx, const rtk::TraceParams& p) {
-    const bool fusable = trace_kernel_for(ctx, p) == rtk::kTraceList;
+    const int k = trace_kernel_for(ctx, p);
+    const bool fusable = k == rtk::kTraceList || k == rtk::kTraceBounce;
     if (!fusable) return 1u;
     if (ctx->frames_per_launch)
         return std::min<uint32_t>(ctx->frames_per_launch, rtk::kMaxFramesPerLaunch);
@@ -499,11 +506,20 @@ rt_status plan_tile_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
     p.tile_cost = nullptr;
     // (single-frame launches keep raster order: their accumulator traffic is a large part
     // of the frame, and scattered tiles cost more in HBM than the tail they save)
-    if (!rtk::is_list_kernel(kernel) || ctx->tile_order_mode == RT_TILE_ORDER_OFF ||
+    const bool bounce = kernel == rtk::kTraceBounce;
+    if (!(rtk::is_list_kernel(kernel) || bounce) || ctx->tile_order_mode == RT_TILE_ORDER_OFF ||
         p.cand_k == 0 || p.frames < 2)
         return RT_OK;
+    // scheduling units: 8x8 tiles, or the compacting bounce instance's workgroups of
+    // kBounceWaves tiles (costs measured in the other unit are discarded)
+    const uint32_t group = (bounce && p.compact) ? rtk::kBounceWaves : 1u;
+    if (ctx->cost_groups != (group > 1u)) {
+        ctx->cost_gen = ctx->order_gen = ~0ull;
+        ctx->cost_groups = group > 1u;
+    }
     const uint64_t gen = ctx->cand_gen;
-    const uint32_t tiles_x = (p.width + 7u) >> 3;
+    const uint32_t tiles_x0 = (p.width + 7u) >> 3;
+    const uint32_t tiles_x = (tiles_x0 + group - 1u) / group;
     const uint64_t tiles = (uint64_t)tiles_x * p.local_bands;
     if (tiles > ctx->order_tiles) {
         if (ctx->order_tiles) {
@@ -691,6 +707,7 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
     p.band_step = nranks;
     p.local_bands = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
     fill_camera(p, *cam);
+    p.compact = ctx->path_compaction == RT_PATHS_COMPACT ? 1u : 0u;
     if (rt_status s = ensure_hash_tables(ctx, w, h, stream)) return s;
     p.hx = ctx->d_hx;
     p.hy = ctx->d_hy;
@@ -700,7 +717,11 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
         // (tiles without a list then read the records from L2).
         const uint32_t padded = (count + 63u) & ~63u;   // <= count + 63 < count + kScanPad
         const bool bounces = cam->max_depth >= 2.0f;
-        p.lds_records = (bounces && padded <= rtk::kLdsMaxRecords) ? padded : 0u;
+        // (the per-wave bounce instance runs one-wave workgroups: no LDS copy, which each
+        // of them would stage)
+        p.lds_records = (bounces && padded <= rtk::kLdsMaxRecords &&
+                         ctx->path_compaction == RT_PATHS_COMPACT)
+                            ? padded : 0u;
         if (rt_status s = ensure_candidates(ctx, p, stream)) return s;
         if (bounces && ctx->grid.nx) {
             const rt_ctx::Grid& g = ctx->grid;
@@ -731,11 +752,13 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
     return RT_OK;
 }
 
-void note_launch(rt_ctx* ctx, int kernel, uint32_t frames) {
+void note_launch(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t frames) {
     ctx->last.launches++;
     ctx->last.frames += frames;
     ctx->last.max_frames_per_launch = std::max(ctx->last.max_frames_per_launch, frames);
-    ctx->last.kernel = kernel;
+    ctx->last.kernel = kernel != rtk::kTraceBounce ? kernel
+                       : p.compact                ? RT_KERNEL_BOUNCE_COMPACT
+                                                  : RT_KERNEL_BOUNCE;
 }
 
 // Shared body of rt_update / rt_render / rt_render_stripes: `frames` accumulated in
@@ -769,7 +792,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         finish_tile_order(ctx, p);
-        note_launch(ctx, kernel, nf);
+        note_launch(ctx, p, kernel, nf);
         src = dst;  // later launches continue the accumulation in place
     }
     return RT_OK;
@@ -784,9 +807,10 @@ uint32_t rt_abi_version(void) { return RT_ABI_VERSION; }
 const char* rt_last_error(void) { return g_last_error.c_str(); }
 
 const char* rt_kernel_name(int which) {
-    static const char* const names[] = {"rt_trace_kernel<0>", "rt_trace_kernel<1>",
-                                        "rt_trace_kernel<2>", "rt_trace_kernel<3>",
-                                        "rt_trace_kernel<4>"};
+    static const char* const names[] = {"rt_trace_kernel<0>",      "rt_trace_kernel<1>",
+                                        "rt_trace_kernel<2>",      "rt_trace_kernel<3>",
+                                        "rt_trace_kernel<4>",      "rt_bounce_kernel<true>",
+                                        "rt_bounce_kernel<false>"};
     if (which >= 0 && which < (int)(sizeof(names) / sizeof(names[0]))) return names[which];
     return rtk::trace_kernel_name();
 }
@@ -851,6 +875,14 @@ rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode) {
         mode != RT_FRAME_PAIRS_QUAD)
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown frame-pair mode");
     ctx->frame_pairs = mode;
+    return RT_OK;
+}
+
+rt_status rt_set_path_compaction(rt_ctx* ctx, int mode) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (mode != RT_PATHS_PER_WAVE && mode != RT_PATHS_COMPACT)
+        return fail(RT_ERR_INVALID_ARGUMENT, "unknown path-compaction mode");
+    ctx->path_compaction = mode;
     return RT_OK;
 }
 
@@ -976,7 +1008,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         finish_tile_order(ctx, p);
-        note_launch(ctx, kernel, nf);
+        note_launch(ctx, p, kernel, nf);
         // frame f of the launch wrote img[(cur + 1 + f) % 2]
         const int newest = (nf & 1u) ? 1 - cur : cur;
         if (known) {

@@ -88,6 +88,9 @@ struct TraceParams {
     // RN64(1 / sqrtf(f32 bits 0x3F7FFFFA + k)), k = 0..7: the defocus disk's reciprocal
     // table (rt_kernels.hip disk_unit), computed on the host
     double disk_rcp[8];
+    // bounce instance (kTraceBounce): compact live paths across the workgroup's waves
+    // after every bounce (1) or let each wave keep its own paths (0)
+    uint32_t compact;
     uint32_t hint_frames;  // 0 = no hint
     uint32_t hint_n[kHintFrames];
     // RN64(1 / (hint_n[f] + 1)): the accumulator's division by f32(n + 1) as one f64
@@ -113,6 +116,10 @@ static_assert(kTraceExhaustive == RT_KERNEL_EXHAUSTIVE && kTraceCulled == RT_KER
                   kTraceList == RT_KERNEL_LIST && kTraceListPair == RT_KERNEL_LIST_PAIR &&
                   kTraceListQuad == RT_KERNEL_LIST_QUAD,
               "instance ids are the ABI's RT_KERNEL_* values");
+// Bounce rays (max_depth >= 2) over several frames per launch, live paths compacted across
+// the workgroup's waves after every bounce (rt_kernels.hip, rt_bounce_kernel).
+constexpr int kTraceBounce = 5;
+constexpr uint32_t kBounceWaves = 4;   // tiles (waves) per bounce workgroup
 constexpr bool is_group_kernel(int k) { return k == kTraceListPair || k == kTraceListQuad; }
 constexpr bool is_list_kernel(int k) { return k == kTraceList || is_group_kernel(k); }
 // Tiles per launch at or below which frame groups of four are used.

@@ -1174,6 +1174,263 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     STAMP(5);
 }
 
+// ---- Bounce paths with workgroup-wide compaction (kTraceBounce) -----------------------
+//
+// rt_update_frames with bounce rays (max_depth >= 2), several frames per launch.  One
+// workgroup = kBounceWaves waves = kBounceWaves consecutive 8x8 tiles of a stripe band; each
+// lane owns one pixel and keeps its accumulator in registers across the launch's frames.
+// Per frame the camera rays of a wave are its own tile's (candidate list or cone scan, as
+// in the culled instance).  After every bounce the paths still alive in the workgroup are
+// compacted: a ballot per wave, the popcounts combined through LDS into wave offsets, and
+// mbcnt gives each live lane its slot; the path state (origin, direction, throughput, seed,
+// owner) goes to LDS slot `prefix`, and the next bounce is traced by the first
+// ceil(live / 64) waves only — the others wait at the barrier, their SIMD time free for
+// other workgroups.  A path that ends (sky, absorbed, depth exhausted) writes its colour to
+// its owner's LDS result slot; the owner accumulates it after the frame (wgsl:352-363).
+// Every path runs exactly the reference's per-pixel arithmetic (ray_color, wgsl:261-297):
+// only which lane executes it changes.  kBounceWaves = 4: a bounce's live paths of four
+// tiles fill one wave where they filled four (K5: path lengths fall off geometrically, the
+// longest of 64 lanes sets a wave's bounce count without compaction).
+constexpr uint32_t kBounceLanes = 64 * kBounceWaves;
+struct BounceLds {
+    float4 po[kBounceLanes];   // origin, seed + 1 (bits) of the path in slot k
+    float4 pd[kBounceLanes];   // direction, owner lane (bits)
+    float4 pc[kBounceLanes];   // throughput
+    float4 res[kBounceLanes];  // colour of the path owned by lane k
+    uint32_t cnt[kBounceWaves];
+};
+__shared__ BounceLds s_bounce;
+
+// One bounce of a path after its hit (wgsl:205-218 record, wgsl:268-286 scatter): the new
+// direction and attenuation, or false when the metal scatter absorbs it.
+__device__ __forceinline__ bool scatter_path(float4 pr, float4 mat, float t, v3 o, v3 d,
+                                             uint32_t sb, v3& hp, v3& nd, v3& att) {
+    const float r_sb = rf(sb);
+    const v3 ruv = random_unit_vector(r_sb, sb);
+    hp = fmas(t, d, o);
+    const v3 outward = divs(sub(hp, mk(pr.x, pr.y, pr.z)), pr.w);          // wgsl:209
+    const bool front = dot(d, outward) < 0.0f;
+    const v3 n = front ? outward : neg(outward);
+    if (mat.w < -1.0f) {                                      // lambertian wgsl:84-93
+        v3 dir = add(n, ruv);
+        if (dot(dir, dir) < 0x1.0c6f7ap-20f) dir = n;
+        nd = dir;
+        att = mk(mat.x, mat.y, mat.z);
+    } else if (mat.w <= 1.0f) {                               // metal wgsl:95-100
+        const v3 refl = fmas(mat.w, ruv, normalize(reflect(d, n)));
+        if (!(dot(refl, n) > 0.0f)) return false;             // wgsl:277-279
+        nd = normalize(refl);
+        att = mk(mat.x, mat.y, mat.z);
+    } else {                                                  // dielectric wgsl:102-135
+        att = mk(1.0f, 1.0f, 1.0f);
+        const float ratio = front ? 1.0f / mat.x : mat.x;
+        const v3 u = normalize(d);
+        const float cos_t = fminf(dot(neg(u), n), 1.0f);
+        const float sin_t = sqrtf(fmaf(-cos_t, cos_t, 1.0f));
+        const bool cannot = ratio * sin_t > 1.0f;
+        const bool refl = cannot || reflectance(cos_t, ratio) > r_sb;
+        nd = normalize(refl ? reflect(u, n) : refract(u, n, ratio));
+    }
+    return true;
+}
+
+// Sky colour of the final direction times the throughput (wgsl:293-296).
+__device__ __forceinline__ v3 sky(v3 cf, v3 d) {
+    const float uy = d.y / sqrtf(dot(d, d));
+    const float a = 0.5f * (uy + 1.0f);
+    const float om = 1.0f - a;
+    return mul(cf, mk(fmaf(a, 0.5f, om), fmaf(a, 0x1.666666p-1f, om), fmaf(a, 1.0f, om)));
+}
+
+// Workgroup-wide prefix of `live` over the kBounceWaves waves: returns this lane's slot
+// (valid when live) and the total.  Two barriers (counts written, counts read).
+__device__ __forceinline__ uint32_t compact_slot(bool live, uint32_t wave, uint32_t& total) {
+    const unsigned long long m = __ballot(live);
+    if ((threadIdx.x & 63u) == 0u) s_bounce.cnt[wave] = (uint32_t)__builtin_popcountll(m);
+    __syncthreads();
+    uint32_t before = 0, sum = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kBounceWaves; ++w) {
+        const uint32_t c = s_bounce.cnt[w];
+        before += w < wave ? c : 0u;
+        sum += c;
+    }
+    total = sum;
+    return before + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+#ifndef RT_BOUNCE_MIN_WAVES
+#define RT_BOUNCE_MIN_WAVES 6
+#endif
+// kCompact: four-wave workgroups exchanging paths through LDS; otherwise one-wave
+// workgroups (one tile each: the finest unit for the cost-ordered schedule) whose paths stay
+// in their lanes, colours in registers, no barriers.
+template <bool kCompact>
+constexpr uint32_t bounce_waves() { return kCompact ? kBounceWaves : 1u; }
+#ifndef RT_BOUNCE_MIN_WAVES
+#define RT_BOUNCE_MIN_WAVES 6
+#endif
+template <bool kCompact>
+__global__ __launch_bounds__(64 * bounce_waves<kCompact>(), RT_BOUNCE_MIN_WAVES) void
+rt_bounce_kernel(const TraceParams p) {
+    constexpr uint32_t kW = bounce_waves<kCompact>();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = kW == 1u ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t me = threadIdx.x;                    // lane in the workgroup
+    const uint32_t tiles_x = (p.width + 7u) >> 3;
+    uint32_t gx = blockIdx.x, lband = blockIdx.y;       // group of kW tiles
+    if (p.tile_order) {                                 // costliest groups first
+        const uint32_t t = __builtin_amdgcn_readfirstlane(p.tile_order[blockIdx.y * gridDim.x +
+                                                                       blockIdx.x]);
+        gx = t & 0xFFFFu;
+        lband = t >> 16;
+    }
+    const uint32_t tx = gx * kW + wave;
+    const bool wave_in = tx < tiles_x;
+    const TileCoord tc = tile_coord(p, wave_in ? tx : 0u, lband, lane);
+    const bool valid = wave_in && tc.valid;
+    if (p.lds_records) {                                // records for the cone culling
+        for (uint32_t j = threadIdx.x; j < p.lds_records; j += 64u * kW) lds_recs[j] = p.geom[j];
+    }
+    const uint32_t group = lband * ((tiles_x + kW - 1u) / kW) + gx;
+    if (p.tile_cost && threadIdx.x == 0u)
+        p.tile_cost[group] = (uint32_t)__builtin_amdgcn_s_memtime();
+    if (p.lds_records || kCompact) __syncthreads();
+    const uint32_t tile = lband * tiles_x + (wave_in ? tx : 0u);
+    const uint32_t ncand = (p.cand_k && wave_in) ? load_cnt(p, tile) : kCandNone;
+    const size_t lbase = (size_t)tile * p.cand_k;
+    const uint32_t hxy = p.hx[min(tc.x, p.width - 1u)] ^ p.hy[min(tc.y, p.height - 1u)];
+    Cam cam;
+    cam.center = mk(p.center[0], p.center[1], p.center[2]);
+    cam.vul = mk(p.vul[0], p.vul[1], p.vul[2]);
+    cam.pdu = mk(p.pdu[0], p.pdu[1], p.pdu[2]);
+    cam.pdv = mk(p.pdv[0], p.pdv[1], p.pdv[2]);
+    cam.ddu = mk(p.ddu[0], p.ddu[1], p.ddu[2]);
+    cam.ddv = mk(p.ddv[0], p.ddv[1], p.ddv[2]);
+    cam.defocus_angle = p.defocus_angle;
+    const uint32_t spp = p.spp, depth = p.depth;        // wgsl:343, 264
+    // the pixel's accumulator (wgsl:339-341; a frame-0 reset discards it)
+    v3 c = mk(0.0f, 0.0f, 0.0f);
+    uint32_t n = 0u;
+    if (!p.reset_first && valid) {
+        const float4 acc = p.in[tc.idx];
+        c = mk(acc.x, acc.y, acc.z);
+        n = f2u(acc.w);
+    }
+    for (uint32_t f = 0; f < p.frames; ++f) {
+        const uint32_t B = p.seed_b[f];                           // wgsl:311, 353
+        if (f == 0 && p.reset_first) {                            // wgsl:345-350
+            c = mk(0.0f, 0.0f, 0.0f);
+            n = 0u;
+        }
+        const bool sampling = valid && n < spp;                   // wgsl:352
+        const uint32_t seed = 1u + n + B;                         // wgsl:353
+        v3 res = mk(0.0f, 0.0f, 0.0f);                            // this pixel's colour
+        if (kCompact) s_bounce.res[me] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        // bounce 0: this wave's own camera rays (wgsl:305-325), its tile's scan
+        v3 o, d, cf = mk(1.0f, 1.0f, 1.0f);
+        get_ray<false>(cam, tc.x, tc.y, hxy, seed * 25u + B, o, d);
+        uint32_t pseed = seed + 1u;                               // ray_color's seed
+        bool live = sampling;
+        uint32_t owner = me;
+        if (depth == 0u && live) {                                // no bounce: the sky
+            res = sky(cf, d);
+            if (kCompact) s_bounce.res[me] = make_float4(res.x, res.y, res.z, 0.0f);
+        }
+        for (uint32_t i = 0; i < depth; ++i) {
+            // this wave's paths of bounce i (slot = lane for i == 0)
+            Hit hit{-1, 0.0f};
+            const float4* hs = p.sph;
+            if (__ballot(live) != 0ull) {
+                const bool listed = i == 0u && ncand != kCandNone;
+                hit = listed ? scan_exhaustive<RT_SCAN_CHUNK, false, true>(p.cand_rec + lbase,
+                                                                          ncand, o, d)
+                      : p.lds_records ? scan_culled<true>(p, p.geom, p.count, o, d, live, i > 0)
+                                      : scan_culled<false>(p, p.geom, p.count, o, d, live, i > 0);
+                if (listed) hs = p.cand_sph + 2 * lbase;
+            }
+            bool done = false, keep = false;
+            v3 col = mk(0.0f, 0.0f, 0.0f);
+            if (live) {
+                if (hit.idx < 0) {                                // wgsl:288-290: sky
+                    done = true;
+                    col = sky(cf, d);
+                } else {
+                    const float4 pr = hs[2 * hit.idx], mat = hs[2 * hit.idx + 1];
+                    v3 hp, nd, att;
+                    const uint32_t sb = hash(pseed + i * 1000u);  // wgsl:268
+                    if (!scatter_path(pr, mat, hit.t, o, d, sb, hp, nd, att)) {
+                        done = true;                              // absorbed: black
+                    } else {
+                        cf = mul(cf, att);                        // wgsl:285-286
+                        o = hp;
+                        d = nd;
+                        if (i + 1u == depth) {                    // depth exhausted: sky
+                            done = true;
+                            col = sky(cf, d);
+                        } else {
+                            keep = true;
+                        }
+                    }
+                }
+                if (done) {
+                    if (kCompact)
+                        s_bounce.res[owner] = make_float4(col.x, col.y, col.z, 0.0f);
+                    else
+                        res = col;
+                }
+            }
+            if (!kCompact) {                                      // paths stay in their lane
+                live = keep;
+                if (__ballot(keep) == 0ull) break;
+                continue;
+            }
+            // compact the surviving paths into the first slots (uniform trip count)
+            uint32_t total;
+            const uint32_t slot = compact_slot(keep, wave, total);
+            if (keep) {
+                s_bounce.po[slot] = make_float4(o.x, o.y, o.z, __uint_as_float(pseed));
+                s_bounce.pd[slot] = make_float4(d.x, d.y, d.z, __uint_as_float(owner));
+                s_bounce.pc[slot] = make_float4(cf.x, cf.y, cf.z, 0.0f);
+            }
+            __syncthreads();
+            if (total == 0u) break;                               // workgroup-uniform
+            live = me < total;
+            if (live) {
+                const float4 a = s_bounce.po[me], b = s_bounce.pd[me], e = s_bounce.pc[me];
+                o = mk(a.x, a.y, a.z);
+                pseed = __float_as_uint(a.w);
+                d = mk(b.x, b.y, b.z);
+                owner = __float_as_uint(b.w);
+                cf = mk(e.x, e.y, e.z);
+            }
+            __syncthreads();                                      // slots read
+        }
+        if (kCompact) {
+            __syncthreads();                                      // results written
+            const float4 r = s_bounce.res[me];
+            res = mk(r.x, r.y, r.z);
+        }
+        if (sampling) {                                           // wgsl:356-357
+            const float k = (float)(n + 1u);
+            c = mk(c.x + (res.x - c.x) / k, c.y + (res.y - c.y) / k, c.z + (res.z - c.z) / k);
+            n += 1u;
+        }
+        // the images of the launch's last two frames survive (wgsl:362-363): frame f's
+        // image belongs to out for even f, out2 (the input buffer) for odd f (store_each);
+        // otherwise only the last frame's, to out
+        if (valid && (f + 1u == p.frames || (p.store_each && f + 2u == p.frames))) {
+            float4* dst = (p.store_each && (f & 1u)) ? p.out2 : p.out;
+            dst[tc.idx] = make_float4(c.x, c.y, c.z, (float)n);
+        }
+        n = f2u((float)n);
+        if (kCompact) __syncthreads();                            // res reused next frame
+    }
+    if (p.tile_cost && threadIdx.x == 0u)
+        p.tile_cost[group] = (uint32_t)__builtin_amdgcn_s_memtime() - p.tile_cost[group];
+}
+
 // launch_tile_order: one 1024-thread workgroup; bucket = quantised log2 of the cost (four
 // buckets per octave).  Each wave counts its tiles into its own LDS histogram (atomics only
 // contend inside a wave), one block-wide scan over the [bucket][wave] counts turns them
@@ -1489,6 +1746,20 @@ static void launch_trace_as(const TraceParams& p, size_t lds, hipStream_t stream
     hipLaunchKernelGGL(rt_trace_kernel<kScan>, grid, dim3(64 * w), lds, stream, p);
 }
 
+// Workgroups of kBounceWaves tiles along a stripe band: grid (column groups, bands).
+static void launch_bounce(const TraceParams& p, hipStream_t stream) {
+    const uint32_t tiles_x = (p.width + 7u) >> 3;
+    const uint32_t w = p.compact ? kBounceWaves : 1u;
+    const dim3 grid((tiles_x + w - 1u) / w, p.local_bands);
+    if (grid.x == 0 || grid.y == 0) return;
+    if (p.compact)
+        hipLaunchKernelGGL(rt_bounce_kernel<true>, grid, dim3(64 * kBounceWaves),
+                           (size_t)p.lds_records * sizeof(float4), stream, p);
+    else
+        hipLaunchKernelGGL(rt_bounce_kernel<false>, grid, dim3(64),
+                           (size_t)p.lds_records * sizeof(float4), stream, p);
+}
+
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
     if (kernel == kTraceCulled)
         launch_trace_as<kTraceCulled>(p, (size_t)p.lds_records * sizeof(float4), stream);
@@ -1497,6 +1768,8 @@ hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
     else if (kernel == kTraceListPair)
         launch_trace_as<kTraceListPair>(p, 2 * (frame_group<kTraceListPair>() - 1) * 64 *
                                                sizeof(float4), stream);
+    else if (kernel == kTraceBounce)
+        launch_bounce(p, stream);
     else if (kernel == kTraceListQuad)
         launch_trace_as<kTraceListQuad>(p, 2 * (frame_group<kTraceListQuad>() - 1) * 64 *
                                                sizeof(float4), stream);

@@ -170,7 +170,12 @@ RT_API const char* rt_last_error(void);
 #define RT_KERNEL_LIST 2
 #define RT_KERNEL_LIST_PAIR 3
 #define RT_KERNEL_LIST_QUAD 4
-/* "rt_trace_kernel<k>" for an instance k above, "rt_trace_kernel" otherwise. */
+/* bounce rays (max_depth >= 2), several frames per launch, 4-tile workgroups: live paths
+ * compacted across the workgroup's waves after every bounce, or kept by their own wave */
+#define RT_KERNEL_BOUNCE_COMPACT 5
+#define RT_KERNEL_BOUNCE 6
+/* The instance's name as rocprofv3 lists it ("rt_trace_kernel<k>", "rt_bounce_kernel<true>",
+ * "rt_bounce_kernel<false>"), "rt_trace_kernel" for an unknown id. */
 RT_API const char* rt_kernel_name(int which);
 /* What the last rt_update / rt_render / rt_render_stripes / rt_update_frames call on this
  * context launched: trace launches, frames traced, the most frames one launch carried and
@@ -262,6 +267,13 @@ RT_API rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode);
 #define RT_TILE_ORDER_AUTO 0
 #define RT_TILE_ORDER_OFF 1
 RT_API rt_status rt_set_tile_order(rt_ctx* ctx, int mode);
+/* Bounce paths (max_depth >= 2) of multi-frame launches: RT_PATHS_PER_WAVE (default) keeps
+ * every path in the wave of its pixel; RT_PATHS_COMPACT repacks the live paths of a
+ * workgroup's four waves into the fewest waves after every bounce (ballot + mbcnt prefix,
+ * path state through LDS).  Pixel results are identical. */
+#define RT_PATHS_PER_WAVE 0
+#define RT_PATHS_COMPACT 1
+RT_API rt_status rt_set_path_compaction(rt_ctx* ctx, int mode);
 /* The frames per launch rt_update_frames would use for `camera` (its max_depth) now. */
 RT_API rt_status rt_get_frames_per_launch(const rt_ctx* ctx, const rt_scene_camera* camera,
                                           uint32_t* out_frames);

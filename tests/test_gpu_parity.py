@@ -187,7 +187,7 @@ def test_bench_k5_launches_match_golden(rt):
         newest = p.update_frames(a, b, w, h, rt.SceneCamera(g["camera"]),
                                  rt.SphereCollection(g["spheres"]), g["seeds"])
         info = p.last_launch_info()
-        assert info["frames"] == 64 and info["kernel_name"] == "rt_trace_kernel<1>"
+        assert info["frames"] == 64 and info["kernel_name"] == "rt_bounce_kernel<false>"
         img = host(b if newest == 1 else a)
         assert_same(img[g["py"], g["px"]], g["pixels"])
     finally:
@@ -567,6 +567,49 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, s
     assert_same(got_new, want_new)
     if frames >= 2:
         assert_same(got_prev, want_prev)
+
+
+@pytest.mark.parametrize("paths", ["per_wave", "compact"])
+@pytest.mark.parametrize("w,h,depth,frames,scene,nranks", [
+    (56, 40, 2, 5, "n120", 1), (67, 45, 8, 3, "default", 1), (64, 48, 3, 1, "n120", 1),
+    (50, 37, 8, 6, "default", 3), (40, 32, 0, 2, "n120", 1), (72, 48, 5, 4, "three", 2)])
+def test_bounce_launches_match_oracle(rt, oracle, paths, w, h, depth, frames, scene, nranks):
+    """The bounce instance (max_depth >= 2, frames fused per launch, 4-tile workgroups),
+    with live paths compacted across the workgroup after every bounce or kept per wave:
+    both ping-pong buffers equal the oracle's chained updates (the newest frame and the one
+    before), whole image and stripe ranks, ragged edges included."""
+    sc = {"n120": rt.synthetic_scene(120), "default": rt.create_default_spheres(seed=3),
+          "three": rt.three_spheres()}[scene]
+    seeds = rt.frame_seeds(33, frames)
+    cam = camera(rt, w, h, depth=depth, spp=500)
+    yy, xx = np.mgrid[0:h, 0:w]
+    want_new, _ = oracle.render_pixels(np.zeros((h * w, 4), np.float32), xx.ravel(), yy.ravel(),
+                                       cam.blob, sc.spheres, seeds)
+    want_prev, _ = oracle.render_pixels(np.zeros((h * w, 4), np.float32), xx.ravel(),
+                                        yy.ravel(), cam.blob, sc.spheres, seeds[:frames - 1])
+    p = rt.ComputeShaderPipeline(0)
+    p.set_path_compaction(paths)
+    rows0 = rt.stripe_local_rows(h, 0, nranks)
+    got_new = np.zeros((h, w, 4), np.float32)
+    got_prev = np.zeros((h, w, 4), np.float32)
+    try:
+        for r in range(nranks):
+            a, b = p.new_image(w, rows0), p.new_image(w, rows0)
+            newest = p.update_frames(a, b, w, h, cam, sc, seeds, r, nranks)
+            info = p.last_launch_info()
+            if depth >= 2:
+                assert info["kernel_name"] == ("rt_bounce_kernel<true>" if paths == "compact"
+                                               else "rt_bounce_kernel<false>")
+            img_new, img_prev = (host(a), host(b)) if newest == 0 else (host(b), host(a))
+            for lr in range(rt.stripe_local_rows(h, r, nranks)):
+                y = (r + (lr // 8) * nranks) * 8 + lr % 8
+                if y < h:
+                    got_new[y], got_prev[y] = img_new[lr], img_prev[lr]
+    finally:
+        p.close()
+    assert_same(got_new, want_new.reshape(h, w, 4))
+    if frames >= 2:
+        assert_same(got_prev, want_prev.reshape(h, w, 4))
 
 
 def test_accumulator_written_outside_the_library(rt, oracle, pipe):

@@ -21,7 +21,7 @@ def header_functions():
 
 def test_library_exports_every_declared_symbol(rt):
     declared = header_functions()
-    assert len(declared) == 30
+    assert len(declared) == 31
     nm = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True,
                         text=True, check=True).stdout
     exported = set(re.findall(r" T (rt_\w+)$", nm, flags=re.M))
@@ -149,8 +149,10 @@ def test_argument_errors_without_device(rt):
     assert L.rt_selftest_fastmath(None, 0, None) == 6
     assert L.rt_last_launch_info(None, None) == 6
     # instance names are the ones rocprofv3 lists (rt_kernels.h asserts the ids)
-    assert [L.rt_kernel_name(k).decode() for k in range(5)] == [
-        f"rt_trace_kernel<{k}>" for k in range(5)]
+    assert [L.rt_kernel_name(k).decode() for k in range(7)] == [
+        f"rt_trace_kernel<{k}>" for k in range(5)] + ["rt_bounce_kernel<true>",
+                                                    "rt_bounce_kernel<false>"]
+    assert L.rt_set_path_compaction(None, 0) == 6
     assert L.rt_kernel_name(99).decode() == "rt_trace_kernel"
 
 
