@@ -73,7 +73,7 @@ struct rt_ctx {
     std::vector<CountRecord> counts;
     uint32_t frames_per_launch = 0;  // rt_update_frames fusion cap (0 = automatic)
     rt_launch_info last = {0, 0, 0, -1};  // the last call's launches (rt_last_launch_info)
-    int path_compaction = RT_PATHS_PER_WAVE;
+    int path_compaction = RT_PATHS_AUTO;
     int frame_pairs = RT_FRAME_PAIRS_AUTO;
 };
 
@@ -512,7 +512,7 @@ rt_status plan_tile_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
         return RT_OK;
     // scheduling units: 8x8 tiles, or the compacting bounce instance's workgroups of
     // kBounceWaves tiles (costs measured in the other unit are discarded)
-    const uint32_t group = (bounce && p.compact) ? rtk::kBounceWaves : 1u;
+    const uint32_t group = (bounce && p.compact == 1u) ? rtk::kBounceWaves : 1u;
     if (ctx->cost_groups != (group > 1u)) {
         ctx->cost_gen = ctx->order_gen = ~0ull;
         ctx->cost_groups = group > 1u;
@@ -707,7 +707,10 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
     p.band_step = nranks;
     p.local_bands = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
     fill_camera(p, *cam);
-    p.compact = ctx->path_compaction == RT_PATHS_COMPACT ? 1u : 0u;
+    // bounce instance mode (rt_kernels.hip rt_bounce_kernel: 0 per wave, 1 compact, 2 pairs)
+    p.compact = ctx->path_compaction == RT_PATHS_COMPACT ? 1u
+                : ctx->path_compaction == RT_PATHS_PAIR  ? 2u
+                                                         : 0u;
     if (rt_status s = ensure_hash_tables(ctx, w, h, stream)) return s;
     p.hx = ctx->d_hx;
     p.hy = ctx->d_hy;
@@ -721,7 +724,8 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
         // of them would stage)
         p.lds_records = (bounces && padded <= rtk::kLdsMaxRecords &&
                          ctx->path_compaction == RT_PATHS_COMPACT)
-                            ? padded : 0u;
+                            ? padded
+                            : 0u;
         if (rt_status s = ensure_candidates(ctx, p, stream)) return s;
         if (bounces && ctx->grid.nx) {
             const rt_ctx::Grid& g = ctx->grid;
@@ -756,9 +760,7 @@ void note_launch(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t fr
     ctx->last.launches++;
     ctx->last.frames += frames;
     ctx->last.max_frames_per_launch = std::max(ctx->last.max_frames_per_launch, frames);
-    ctx->last.kernel = kernel != rtk::kTraceBounce ? kernel
-                       : p.compact                ? RT_KERNEL_BOUNCE_COMPACT
-                                                  : RT_KERNEL_BOUNCE;
+    ctx->last.kernel = kernel != rtk::kTraceBounce ? kernel : RT_KERNEL_BOUNCE + (int)p.compact;
 }
 
 // Shared body of rt_update / rt_render / rt_render_stripes: `frames` accumulated in
@@ -809,8 +811,8 @@ const char* rt_last_error(void) { return g_last_error.c_str(); }
 const char* rt_kernel_name(int which) {
     static const char* const names[] = {"rt_trace_kernel<0>",      "rt_trace_kernel<1>",
                                         "rt_trace_kernel<2>",      "rt_trace_kernel<3>",
-                                        "rt_trace_kernel<4>",      "rt_bounce_kernel<true>",
-                                        "rt_bounce_kernel<false>"};
+                                        "rt_trace_kernel<4>",      "rt_bounce_kernel<0>",
+                                        "rt_bounce_kernel<1>",     "rt_bounce_kernel<2>"};
     if (which >= 0 && which < (int)(sizeof(names) / sizeof(names[0]))) return names[which];
     return rtk::trace_kernel_name();
 }
@@ -880,7 +882,8 @@ rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode) {
 
 rt_status rt_set_path_compaction(rt_ctx* ctx, int mode) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
-    if (mode != RT_PATHS_PER_WAVE && mode != RT_PATHS_COMPACT)
+    if (mode != RT_PATHS_AUTO && mode != RT_PATHS_PER_WAVE && mode != RT_PATHS_COMPACT &&
+        mode != RT_PATHS_PAIR)
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown path-compaction mode");
     ctx->path_compaction = mode;
     return RT_OK;

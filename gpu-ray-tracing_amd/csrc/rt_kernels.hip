@@ -1263,18 +1263,26 @@ __device__ __forceinline__ uint32_t compact_slot(bool live, uint32_t wave, uint3
 #ifndef RT_BOUNCE_MIN_WAVES
 #define RT_BOUNCE_MIN_WAVES 6
 #endif
-// kCompact: four-wave workgroups exchanging paths through LDS; otherwise one-wave
-// workgroups (one tile each: the finest unit for the cost-ordered schedule) whose paths stay
-// in their lanes, colours in registers, no barriers.
-template <bool kCompact>
-constexpr uint32_t bounce_waves() { return kCompact ? kBounceWaves : 1u; }
+// Modes: kBounceWave — one-wave workgroups (one tile each: the finest unit for the
+// cost-ordered schedule) whose paths stay in their lanes, colours in registers, no
+// barriers; kBounceCompact — four-wave workgroups exchanging paths through LDS (above);
+// kBouncePair — two waves per tile on alternate frames, wave 1 handing its colours to wave
+// 0 through LDS, which accumulates both in order (the frame groups of the camera-ray
+// instance, trace_pair): half as long a chain per wave, for small per-rank shares.
+constexpr int kBounceWave = 0, kBounceCompact = 1, kBouncePair = 2;
+template <int kMode>
+constexpr uint32_t bounce_waves() {
+    return kMode == kBounceCompact ? kBounceWaves : kMode == kBouncePair ? 2u : 1u;
+}
+__shared__ float4 s_pair_col[64];   // kBouncePair: wave 1's colours of the current pair
 #ifndef RT_BOUNCE_MIN_WAVES
 #define RT_BOUNCE_MIN_WAVES 6
 #endif
-template <bool kCompact>
-__global__ __launch_bounds__(64 * bounce_waves<kCompact>(), RT_BOUNCE_MIN_WAVES) void
+template <int kMode>
+__global__ __launch_bounds__(64 * bounce_waves<kMode>(), RT_BOUNCE_MIN_WAVES) void
 rt_bounce_kernel(const TraceParams p) {
-    constexpr uint32_t kW = bounce_waves<kCompact>();
+    constexpr bool kCompact = kMode == kBounceCompact, kPair = kMode == kBouncePair;
+    constexpr uint32_t kW = bounce_waves<kMode>();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = kW == 1u ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t me = threadIdx.x;                    // lane in the workgroup
@@ -1286,17 +1294,18 @@ rt_bounce_kernel(const TraceParams p) {
         gx = t & 0xFFFFu;
         lband = t >> 16;
     }
-    const uint32_t tx = gx * kW + wave;
+    const uint32_t tx = kPair ? gx : gx * kW + wave;   // (pairs: both waves, one tile)
     const bool wave_in = tx < tiles_x;
     const TileCoord tc = tile_coord(p, wave_in ? tx : 0u, lband, lane);
     const bool valid = wave_in && tc.valid;
     if (p.lds_records) {                                // records for the cone culling
         for (uint32_t j = threadIdx.x; j < p.lds_records; j += 64u * kW) lds_recs[j] = p.geom[j];
     }
-    const uint32_t group = lband * ((tiles_x + kW - 1u) / kW) + gx;
+    constexpr uint32_t kTiles = kPair ? 1u : kW;        // tiles per workgroup
+    const uint32_t group = lband * ((tiles_x + kTiles - 1u) / kTiles) + gx;
     if (p.tile_cost && threadIdx.x == 0u)
         p.tile_cost[group] = (uint32_t)__builtin_amdgcn_s_memtime();
-    if (p.lds_records || kCompact) __syncthreads();
+    if (p.lds_records || kW > 1u) __syncthreads();
     const uint32_t tile = lband * tiles_x + (wave_in ? tx : 0u);
     const uint32_t ncand = (p.cand_k && wave_in) ? load_cnt(p, tile) : kCandNone;
     const size_t lbase = (size_t)tile * p.cand_k;
@@ -1318,14 +1327,21 @@ rt_bounce_kernel(const TraceParams p) {
         c = mk(acc.x, acc.y, acc.z);
         n = f2u(acc.w);
     }
-    for (uint32_t f = 0; f < p.frames; ++f) {
-        const uint32_t B = p.seed_b[f];                           // wgsl:311, 353
-        if (f == 0 && p.reset_first) {                            // wgsl:345-350
+    constexpr uint32_t kStep = kPair ? 2u : 1u;               // frames per iteration
+    for (uint32_t f0 = 0; f0 < p.frames; f0 += kStep) {
+        if (f0 == 0 && p.reset_first) {                           // wgsl:345-350
             c = mk(0.0f, 0.0f, 0.0f);
             n = 0u;
         }
-        const bool sampling = valid && n < spp;                   // wgsl:352
-        const uint32_t seed = 1u + n + B;                         // wgsl:353
+        // this wave's frame and the pixel's count before it (pairs: wave 1 takes the next
+        // frame, whose count follows from wgsl:352-362 with the f32 round trip)
+        const uint32_t f = f0 + (kPair ? wave : 0u);
+        const uint32_t n_next = f2u((float)(n < spp ? n + 1u : n));
+        const uint32_t nf = (kPair && wave == 1u) ? n_next : n;
+        const bool frame_in = f < p.frames;
+        const uint32_t B = p.seed_b[frame_in ? f : f0];           // wgsl:311, 353
+        const bool sampling = valid && frame_in && nf < spp;      // wgsl:352
+        const uint32_t seed = 1u + nf + B;                        // wgsl:353
         v3 res = mk(0.0f, 0.0f, 0.0f);                            // this pixel's colour
         if (kCompact) s_bounce.res[me] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         // bounce 0: this wave's own camera rays (wgsl:305-325), its tile's scan
@@ -1412,20 +1428,37 @@ rt_bounce_kernel(const TraceParams p) {
             const float4 r = s_bounce.res[me];
             res = mk(r.x, r.y, r.z);
         }
-        if (sampling) {                                           // wgsl:356-357
-            const float k = (float)(n + 1u);
-            c = mk(c.x + (res.x - c.x) / k, c.y + (res.y - c.y) / k, c.z + (res.z - c.z) / k);
-            n += 1u;
+        if (kPair) {                                              // wave 1's colour to wave 0
+            if (wave == 1u) s_pair_col[lane] = make_float4(res.x, res.y, res.z, 0.0f);
+            __syncthreads();
         }
-        // the images of the launch's last two frames survive (wgsl:362-363): frame f's
-        // image belongs to out for even f, out2 (the input buffer) for odd f (store_each);
-        // otherwise only the last frame's, to out
-        if (valid && (f + 1u == p.frames || (p.store_each && f + 2u == p.frames))) {
-            float4* dst = (p.store_each && (f & 1u)) ? p.out2 : p.out;
-            dst[tc.idx] = make_float4(c.x, c.y, c.z, (float)n);
+        // accumulate this iteration's frames in order (pairs: wave 0 does both; wave 1 only
+        // follows the count)
+        for (uint32_t j = 0; j < kStep; ++j) {
+            const uint32_t fj = f0 + j;
+            if (fj >= p.frames) break;
+            if (!kPair || wave == 0u) {
+                v3 col = res;
+                if (kPair && j == 1u) {
+                    const float4 r = s_pair_col[lane];
+                    col = mk(r.x, r.y, r.z);
+                }
+                if (valid && n < spp) {                           // wgsl:352, 356-357
+                    const float k = (float)(n + 1u);
+                    c = mk(c.x + (col.x - c.x) / k, c.y + (col.y - c.y) / k,
+                           c.z + (col.z - c.z) / k);
+                }
+                // the images of the launch's last two frames survive (wgsl:362-363): frame
+                // fj's image belongs to out for even fj, out2 (the input buffer) for odd fj
+                // (store_each); otherwise only the last frame's, to out
+                if (valid && (fj + 1u == p.frames || (p.store_each && fj + 2u == p.frames))) {
+                    float4* dst = (p.store_each && (fj & 1u)) ? p.out2 : p.out;
+                    dst[tc.idx] = make_float4(c.x, c.y, c.z, (float)(n < spp ? n + 1u : n));
+                }
+            }
+            n = f2u((float)(n < spp ? n + 1u : n));
         }
-        n = f2u((float)n);
-        if (kCompact) __syncthreads();                            // res reused next frame
+        if (kCompact || kPair) __syncthreads();                   // LDS reused next frame
     }
     if (p.tile_cost && threadIdx.x == 0u)
         p.tile_cost[group] = (uint32_t)__builtin_amdgcn_s_memtime() - p.tile_cost[group];
@@ -1749,15 +1782,17 @@ static void launch_trace_as(const TraceParams& p, size_t lds, hipStream_t stream
 // Workgroups of kBounceWaves tiles along a stripe band: grid (column groups, bands).
 static void launch_bounce(const TraceParams& p, hipStream_t stream) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
-    const uint32_t w = p.compact ? kBounceWaves : 1u;
+    const uint32_t w = p.compact == 1u ? kBounceWaves : 1u;   // tiles per workgroup
     const dim3 grid((tiles_x + w - 1u) / w, p.local_bands);
     if (grid.x == 0 || grid.y == 0) return;
-    if (p.compact)
-        hipLaunchKernelGGL(rt_bounce_kernel<true>, grid, dim3(64 * kBounceWaves),
-                           (size_t)p.lds_records * sizeof(float4), stream, p);
+    const size_t lds = (size_t)p.lds_records * sizeof(float4);
+    if (p.compact == 1u)
+        hipLaunchKernelGGL(rt_bounce_kernel<kBounceCompact>, grid, dim3(64 * kBounceWaves), lds,
+                           stream, p);
+    else if (p.compact == 2u)
+        hipLaunchKernelGGL(rt_bounce_kernel<kBouncePair>, grid, dim3(128), lds, stream, p);
     else
-        hipLaunchKernelGGL(rt_bounce_kernel<false>, grid, dim3(64),
-                           (size_t)p.lds_records * sizeof(float4), stream, p);
+        hipLaunchKernelGGL(rt_bounce_kernel<kBounceWave>, grid, dim3(64), lds, stream, p);
 }
 
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {

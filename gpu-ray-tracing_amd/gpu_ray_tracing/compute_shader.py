@@ -80,9 +80,11 @@ class ComputeShaderPipeline:
         _lib.call("rt_set_tile_order", self._ctx, {"auto": 0, "off": 1}[mode])
 
     def set_path_compaction(self, mode: str) -> None:
-        """rt_set_path_compaction: "per_wave" (default) or "compact" (bounce paths repacked
-        across the workgroup's waves after every bounce)."""
-        _lib.call("rt_set_path_compaction", self._ctx, {"per_wave": 0, "compact": 1}[mode])
+        """rt_set_path_compaction for bounce launches: "auto" (default), "per_wave",
+        "compact" (paths repacked across four waves after every bounce) or "pair" (two waves
+        per tile on alternate frames)."""
+        _lib.call("rt_set_path_compaction", self._ctx,
+                  {"auto": 0, "per_wave": 1, "compact": 2, "pair": 3}[mode])
 
     def frames_per_launch(self, camera) -> int:
         """rt_get_frames_per_launch: frames update_frames fuses per launch for `camera`."""

@@ -170,12 +170,13 @@ RT_API const char* rt_last_error(void);
 #define RT_KERNEL_LIST 2
 #define RT_KERNEL_LIST_PAIR 3
 #define RT_KERNEL_LIST_QUAD 4
-/* bounce rays (max_depth >= 2), several frames per launch, 4-tile workgroups: live paths
- * compacted across the workgroup's waves after every bounce, or kept by their own wave */
-#define RT_KERNEL_BOUNCE_COMPACT 5
-#define RT_KERNEL_BOUNCE 6
-/* The instance's name as rocprofv3 lists it ("rt_trace_kernel<k>", "rt_bounce_kernel<true>",
- * "rt_bounce_kernel<false>"), "rt_trace_kernel" for an unknown id. */
+/* bounce rays (max_depth >= 2), several frames per launch (rt_set_path_compaction):
+ * paths kept by the wave of their pixel, compacted across four waves, frame pairs */
+#define RT_KERNEL_BOUNCE 5
+#define RT_KERNEL_BOUNCE_COMPACT 6
+#define RT_KERNEL_BOUNCE_PAIR 7
+/* The instance's name as rocprofv3 lists it ("rt_trace_kernel<k>", "rt_bounce_kernel<m>"),
+ * "rt_trace_kernel" for an unknown id. */
 RT_API const char* rt_kernel_name(int which);
 /* What the last rt_update / rt_render / rt_render_stripes / rt_update_frames call on this
  * context launched: trace launches, frames traced, the most frames one launch carried and
@@ -267,12 +268,18 @@ RT_API rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode);
 #define RT_TILE_ORDER_AUTO 0
 #define RT_TILE_ORDER_OFF 1
 RT_API rt_status rt_set_tile_order(rt_ctx* ctx, int mode);
-/* Bounce paths (max_depth >= 2) of multi-frame launches: RT_PATHS_PER_WAVE (default) keeps
- * every path in the wave of its pixel; RT_PATHS_COMPACT repacks the live paths of a
- * workgroup's four waves into the fewest waves after every bounce (ballot + mbcnt prefix,
- * path state through LDS).  Pixel results are identical. */
-#define RT_PATHS_PER_WAVE 0
-#define RT_PATHS_COMPACT 1
+/* Bounce paths (max_depth >= 2): RT_PATHS_PER_WAVE keeps every path in the wave of its
+ * pixel (one tile per workgroup); RT_PATHS_PAIR runs two waves per tile on alternate
+ * frames, the second handing its colours to the first through LDS (shorter chains for
+ * small per-rank shares); RT_PATHS_COMPACT repacks the live paths of a workgroup's four
+ * waves into the fewest waves after every bounce (ballot + mbcnt prefix, path state through
+ * LDS).  RT_PATHS_AUTO (default) = RT_PATHS_PER_WAVE, the fastest at every rank count
+ * measured (profiles/r02_rank_sim_k5_paths_*.jsonl).  Pixel results are identical in
+ * every mode. */
+#define RT_PATHS_AUTO 0
+#define RT_PATHS_PER_WAVE 1
+#define RT_PATHS_COMPACT 2
+#define RT_PATHS_PAIR 3
 RT_API rt_status rt_set_path_compaction(rt_ctx* ctx, int mode);
 /* The frames per launch rt_update_frames would use for `camera` (its max_depth) now. */
 RT_API rt_status rt_get_frames_per_launch(const rt_ctx* ctx, const rt_scene_camera* camera,

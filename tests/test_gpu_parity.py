@@ -187,7 +187,7 @@ def test_bench_k5_launches_match_golden(rt):
         newest = p.update_frames(a, b, w, h, rt.SceneCamera(g["camera"]),
                                  rt.SphereCollection(g["spheres"]), g["seeds"])
         info = p.last_launch_info()
-        assert info["frames"] == 64 and info["kernel_name"] == "rt_bounce_kernel<false>"
+        assert info["frames"] == 64 and info["kernel_name"] == "rt_bounce_kernel<0>"
         img = host(b if newest == 1 else a)
         assert_same(img[g["py"], g["px"]], g["pixels"])
     finally:
@@ -569,7 +569,7 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, s
         assert_same(got_prev, want_prev)
 
 
-@pytest.mark.parametrize("paths", ["per_wave", "compact"])
+@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "auto"])
 @pytest.mark.parametrize("w,h,depth,frames,scene,nranks", [
     (56, 40, 2, 5, "n120", 1), (67, 45, 8, 3, "default", 1), (64, 48, 3, 1, "n120", 1),
     (50, 37, 8, 6, "default", 3), (40, 32, 0, 2, "n120", 1), (72, 48, 5, 4, "three", 2)])
@@ -598,8 +598,8 @@ def test_bounce_launches_match_oracle(rt, oracle, paths, w, h, depth, frames, sc
             newest = p.update_frames(a, b, w, h, cam, sc, seeds, r, nranks)
             info = p.last_launch_info()
             if depth >= 2:
-                assert info["kernel_name"] == ("rt_bounce_kernel<true>" if paths == "compact"
-                                               else "rt_bounce_kernel<false>")
+                assert info["kernel_name"] == "rt_bounce_kernel<%d>" % {
+                    "per_wave": 0, "compact": 1, "pair": 2, "auto": 0}[paths]
             img_new, img_prev = (host(a), host(b)) if newest == 0 else (host(b), host(a))
             for lr in range(rt.stripe_local_rows(h, r, nranks)):
                 y = (r + (lr // 8) * nranks) * 8 + lr % 8

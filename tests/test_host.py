@@ -149,9 +149,8 @@ def test_argument_errors_without_device(rt):
     assert L.rt_selftest_fastmath(None, 0, None) == 6
     assert L.rt_last_launch_info(None, None) == 6
     # instance names are the ones rocprofv3 lists (rt_kernels.h asserts the ids)
-    assert [L.rt_kernel_name(k).decode() for k in range(7)] == [
-        f"rt_trace_kernel<{k}>" for k in range(5)] + ["rt_bounce_kernel<true>",
-                                                    "rt_bounce_kernel<false>"]
+    assert [L.rt_kernel_name(k).decode() for k in range(8)] == [
+        f"rt_trace_kernel<{k}>" for k in range(5)] + [f"rt_bounce_kernel<{m}>" for m in range(3)]
     assert L.rt_set_path_compaction(None, 0) == 6
     assert L.rt_kernel_name(99).decode() == "rt_trace_kernel"
 

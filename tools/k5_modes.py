@@ -11,7 +11,7 @@ import gpu_ray_tracing as rt
 g = dict(np.load(ROOT / "tests" / "golden" / "k5.npz"))
 w, h = int(g["width"]), int(g["height"])
 cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
-for mode in (sys.argv[1:] or ["per_wave", "compact"]):
+for mode in (sys.argv[1:] or ["auto", "per_wave", "pair", "compact"]):
     p = rt.ComputeShaderPipeline(0)
     p.set_path_compaction(mode)
     a, b = p.new_image(w, h), p.new_image(w, h)

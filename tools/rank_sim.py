@@ -1,7 +1,7 @@
 """Per-rank frame time of the stripe partition on ONE GPU (diagnostic, not the bench): times
 rank 0's share of a W x H progressive render for world sizes 1, 2, 4, 8, i.e. what each rank
 of `bench.py --gpus N` computes per step, to predict strong-scaling efficiency without an
-8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] python tools/rank_sim.py [K3|K2|K5] [steps]"""
+8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] [RT_PATHS=auto|per_wave|pair|compact] python tools/rank_sim.py [K3|K2|K5] [steps]"""
 import json
 import sys
 from pathlib import Path
@@ -29,6 +29,7 @@ def main(cfg="K3", steps=50):
     pipe.set_frame_pairs(os.environ.get("RT_FRAME_PAIRS", "auto"))
     # RT_FPL=1: one launch per frame (the reference's dispatch structure)
     pipe.set_frames_per_launch(int(os.environ.get("RT_FPL", "0")))
+    pipe.set_path_compaction(os.environ.get("RT_PATHS", "auto"))   # bounce launches
     if hasattr(rt._lib.lib(), "rt_set_tile_order"):
         pipe.set_tile_order(os.environ.get("RT_TILE_ORDER", "auto"))
     base = None
