@@ -73,3 +73,90 @@ def test_stripe_gather_gloo(world, w, h):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert q.get(timeout=5) is True
+
+
+class _OraclePipeline:
+    """Test double for ComputeShaderPipeline behind StripeRenderer on CPU: the same method
+    contract (render_stripes / update_frames / deinterleave on this rank's packed bands),
+    computed by the CPU oracle (test infrastructure; the HIP versions of these three calls
+    are checked against the oracle by tests/test_gpu_parity.py)."""
+
+    def __init__(self, O):
+        self.O = O
+
+    def new_image(self, width, height):
+        return torch.zeros((height, width, 4), dtype=torch.float32)
+
+    def _bands(self, width, height, rank, world, src, dst, camera, spheres, seeds):
+        ys = [b * 8 + r for b in range(rank, (height + 7) // 8, world) for r in range(8)
+              if b * 8 + r < height]
+        yy = np.repeat(np.array(ys, np.uint32), width)
+        xx = np.tile(np.arange(width, dtype=np.uint32), len(ys))
+        st0 = src[: len(ys)].numpy().reshape(-1, 4)
+        st, _ = self.O.render_pixels(st0, xx, yy, camera, spheres, seeds)
+        dst[: len(ys)] = torch.from_numpy(st.reshape(len(ys), width, 4))
+
+    def render_stripes(self, inp, out, width, height, rank, nranks, camera, spheres, seeds):
+        self._bands(width, height, rank, nranks, inp, out, camera, spheres, seeds)
+
+    def update_frames(self, a, b, width, height, camera, spheres, seeds, rank=0, nranks=1):
+        newest = len(seeds) % 2           # a -> b -> a ...: b holds an odd count
+        self._bands(width, height, rank, nranks, a, (b if newest else a), camera, spheres,
+                    seeds)
+        return newest
+
+    def deinterleave(self, gathered, out, width, height, nranks):
+        rows0 = gathered.shape[0] // nranks
+        g = gathered.reshape(nranks, rows0, width, 4)
+        for y in range(height):
+            band = y // 8
+            out[y] = g[band % nranks, (band // nranks) * 8 + y % 8]
+
+
+def _renderer_worker(rank, world, port, w, h, dst, q):
+    sys.path[:0] = [str(PKG_DIR), str(ROOT)]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gpu_ray_tracing.distributed import StripeRenderer
+        from oracle import host_ref as H
+        from oracle import oracle as O
+        spheres = H.generate_scene(1, 0, 5)
+        seeds = H.frame_seeds(11, 6)
+        moved = H.scene_camera_from(max_depth=4, width=w, height=h, random_seed=float(seeds[0]))
+        still = H.scene_camera_from(max_depth=4, width=w, height=h, moved=False,
+                                    random_seed=float(seeds[2]))
+        r = StripeRenderer(_OraclePipeline(O), w, h, rank, world)
+        # bench.py's step shape: a fused first call, then per-dispatch frames, then ONE gather
+        r.frame(moved, spheres, seeds[:2])
+        r.frames(still, spheres, seeds[2:5])
+        r.frames(still, spheres, seeds[5:6])
+        img = r.finish(dst=dst)
+        if rank == dst:
+            full, _ = O.render(np.zeros((h, w, 4), np.float32), moved, spheres, seeds[:2])
+            full, _ = O.render(full, still, spheres, seeds[2:6])
+            q.put(bool(img.shape == (h, w, 4)
+                       and np.array_equal(img.numpy().view(np.uint32), full.view(np.uint32))))
+        else:
+            assert img is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,w,h,dst", [(2, 16, 24, 0), (3, 9, 8, 0), (3, 12, 20, 1)])
+def test_stripe_renderer_finish_gloo(world, w, h, dst):
+    """StripeRenderer end to end over gloo: ping-pong buffers across frame()/frames() calls
+    with odd and even frame counts, ranks that own no bands (world 3, height 8), the root's
+    pre-allocated gather buffers (dst 0) and a non-zero root (dst 1); the root's finish()
+    must equal the single-process render bit for bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_renderer_worker, args=(r, world, port, w, h, dst, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert q.get(timeout=5) is True
