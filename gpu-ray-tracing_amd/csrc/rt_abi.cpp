@@ -60,9 +60,9 @@ struct rt_ctx {
     bool cost_groups = false;       // tile_cost/tile_order count bounce workgroups, not tiles
     int tile_order_mode = RT_TILE_ORDER_AUTO;
     float* d_srgb = nullptr;  // rt_srgb_thresholds table on the device (256 floats)
-    // hash(x*73) for x < hx_len and hash(y*51) for y < hy_len (wgsl:309-310)
+    // hash(x*73) for x < hx_len (= rtk::hy_offset(width)), then hash(y*51) for y < hy_len
+    // (wgsl:309-310), one buffer
     uint32_t* d_hx = nullptr;
-    uint32_t* d_hy = nullptr;
     uint32_t hx_len = 0, hy_len = 0;
     // Sample counts of images this context wrote, when every pixel holds the same count:
     // the source of TraceParams::hint_n (a hint only: the kernel verifies it per pixel).
@@ -562,31 +562,29 @@ void finish_tile_order(rt_ctx* ctx, const rtk::TraceParams& p) {
 }
 
 // Per-column / per-row halves of the pixel-invariant seed hash (wgsl:309-310), built on
-// the host once per image size.
+// the host once per image size: one buffer, hash(x*73) for x < rtk::hy_offset(w), then
+// hash(y*51) for y < h (the trace kernel derives the row table from the column table's
+// pointer and the width: one preloaded pointer for both).
 rt_status ensure_hash_tables(rt_ctx* ctx, uint32_t w, uint32_t h, hipStream_t stream) {
-    struct Table {
-        uint32_t** dev;
-        uint32_t* len;
-        uint32_t need, mul;
-    } tabs[2] = {{&ctx->d_hx, &ctx->hx_len, w, 73u}, {&ctx->d_hy, &ctx->hy_len, h, 51u}};
-    for (Table& t : tabs) {
-        if (*t.dev && *t.len >= t.need) continue;
-        std::vector<uint32_t> v(t.need);
-        for (uint32_t i = 0; i < t.need; ++i) v[i] = rtd::hash(i * t.mul);
-        uint32_t* d = nullptr;
-        hipError_t e = hipMalloc(&d, t.need * sizeof(uint32_t));
-        if (e != hipSuccess) return hip_fail(e, "hipMalloc(hash table)");
-        e = hipMemcpyAsync(d, v.data(), t.need * sizeof(uint32_t), hipMemcpyHostToDevice,
-                           stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(stream);  // also retires old readers
-        if (e != hipSuccess) {
-            (void)hipFree(d);
-            return hip_fail(e, "hipMemcpyAsync(hash table)");
-        }
-        (void)hipFree(*t.dev);
-        *t.dev = d;
-        *t.len = t.need;
+    const uint32_t xpad = rtk::hy_offset(w);
+    if (ctx->d_hx && ctx->hx_len == xpad && ctx->hy_len >= h) return RT_OK;
+    const uint32_t ylen = std::max(h, ctx->hx_len == xpad ? ctx->hy_len : 0u);
+    std::vector<uint32_t> v((size_t)xpad + ylen);
+    for (uint32_t i = 0; i < xpad; ++i) v[i] = rtd::hash(i * 73u);
+    for (uint32_t i = 0; i < ylen; ++i) v[xpad + i] = rtd::hash(i * 51u);
+    uint32_t* d = nullptr;
+    hipError_t e = hipMalloc(&d, v.size() * sizeof(uint32_t));
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(hash table)");
+    e = hipMemcpyAsync(d, v.data(), v.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);  // also retires old readers
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return hip_fail(e, "hipMemcpyAsync(hash table)");
     }
+    (void)hipFree(ctx->d_hx);
+    ctx->d_hx = d;
+    ctx->hx_len = xpad;
+    ctx->hy_len = ylen;
     return RT_OK;
 }
 
@@ -713,7 +711,7 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
                                                          : 0u;
     if (rt_status s = ensure_hash_tables(ctx, w, h, stream)) return s;
     p.hx = ctx->d_hx;
-    p.hy = ctx->d_hy;
+    p.hy = ctx->d_hx + rtk::hy_offset(w);
     if (ctx->scan_mode == RT_SCAN_CULLED) {
         // Camera rays use the per-tile candidate lists; the LDS copy of the records only
         // serves the per-wave cone culling of bounce rays, so it is skipped at depth <= 1
@@ -847,7 +845,6 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->d_sph);
         (void)hipFree(ctx->d_srgb);
         (void)hipFree(ctx->d_hx);
-        (void)hipFree(ctx->d_hy);
         (void)hipFree(ctx->tile_cost);
         (void)hipFree(ctx->tile_order);
         (void)hipFree(ctx->d_grid);

@@ -124,6 +124,15 @@ constexpr bool is_group_kernel(int k) { return k == kTraceListPair || k == kTrac
 constexpr bool is_list_kernel(int k) { return k == kTraceList || is_group_kernel(k); }
 // Tiles per launch at or below which frame groups of four are used.
 constexpr uint64_t kQuadMaxTiles = 6144;
+// The seed-hash tables share one buffer: hash(x*73) for x < hy_offset(width), then
+// hash(y*51) per row (TraceParams::hy == hx + hy_offset(width)).
+constexpr uint32_t hy_offset(uint32_t width) { return (width + 63u) & ~63u; }
+// Stripe map packed for rt_trace_kernel's preloaded arguments: band_first (16 bits),
+// min(band_step, 0x7FFF) (15 bits; exact: a rank with two or more bands has band_step <
+// bands <= 8192) and bit 31 = TraceParams::tile_order is set.
+constexpr uint32_t pack_bands(uint32_t first, uint32_t step, bool ordered) {
+    return first | ((step < 0x7FFFu ? step : 0x7FFFu) << 16) | (ordered ? 1u << 31 : 0u);
+}
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream);
 hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream);
 // Builds the per-tile candidate lists for p's camera/scene/stripes (p.cand_k slots each).

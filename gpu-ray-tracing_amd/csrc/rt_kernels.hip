@@ -559,18 +559,18 @@ __device__ __forceinline__ Hit scan_culled(const TraceParams& p, const float4* _
 // rt_candidates_kernel, and each frame's camera rays test only that list.
 __device__ __forceinline__ float len3(v3 v) { return __builtin_amdgcn_sqrtf(dot(v, v)); }
 
-__device__ __forceinline__ bool tile_cone(const TraceParams& p, uint32_t tx, uint32_t lband,
-                                          Cone& k) {
-    const float x0 = (float)(tx * 8u);
-    const float y0 = (float)((p.band_first + lband * p.band_step) * RT_STRIPE_ROWS);
+// The cone of the camera rays through the focus-plane rectangle of pixel columns [x0, x1)
+// and rows [y0, y1) (one tile: 8 x 8).
+__device__ __forceinline__ bool footprint_cone(const TraceParams& p, float x0, float x1,
+                                               float y0, float y1, Cone& k) {
     const v3 vul = mk(p.vul[0], p.vul[1], p.vul[2]), pdu = mk(p.pdu[0], p.pdu[1], p.pdu[2]),
              pdv = mk(p.pdv[0], p.pdv[1], p.pdv[2]);
     const v3 ctr = mk(p.center[0], p.center[1], p.center[2]);
-    const v3 pc = fmas(y0 + 4.0f, pdv, fmas(x0 + 4.0f, pdu, vul));
+    const v3 pc = fmas(0.5f * (y0 + y1), pdv, fmas(0.5f * (x0 + x1), pdu, vul));
     float rq = 0.0f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const v3 q = fmas(y0 + (c & 2 ? 8.0f : 0.0f), pdv, fmas(x0 + (c & 1 ? 8.0f : 0.0f), pdu, vul));
+        const v3 q = fmas(c & 2 ? y1 : y0, pdv, fmas(c & 1 ? x1 : x0, pdu, vul));
         rq = fmaxf(rq, len3(sub(q, pc)));
     }
     float rl = 0.0f;
@@ -835,16 +835,21 @@ struct TileCoord {
 };
 
 // Launch grid: blockIdx.y = local stripe band, blockIdx.x * 4 + wave = tile column.
-__device__ __forceinline__ TileCoord tile_coord(const TraceParams& p, uint32_t tx,
-                                                uint32_t lband, uint32_t lane) {
+__device__ __forceinline__ TileCoord tile_coord(uint32_t width, uint32_t height,
+                                                uint32_t band_first, uint32_t band_step,
+                                                uint32_t tx, uint32_t lband, uint32_t lane) {
     TileCoord t;
     t.x = tx * 8u + (lane & 7u);
-    const uint32_t gband = p.band_first + lband * p.band_step;
+    const uint32_t gband = band_first + lband * band_step;
     t.y = gband * RT_STRIPE_ROWS + (lane >> 3);
     const uint32_t ly = lband * RT_STRIPE_ROWS + (lane >> 3);
-    t.valid = (t.x < p.width) && (t.y < p.height);
-    t.idx = (size_t)ly * p.width + t.x;
+    t.valid = (t.x < width) && (t.y < height);
+    t.idx = (size_t)ly * width + t.x;
     return t;
+}
+__device__ __forceinline__ TileCoord tile_coord(const TraceParams& p, uint32_t tx,
+                                                uint32_t lband, uint32_t lane) {
+    return tile_coord(p.width, p.height, p.band_first, p.band_step, tx, lband, lane);
 }
 
 // One sample of one frame for the pixels with `live` set, traced with sample count n
@@ -1027,12 +1032,23 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
 // the compiler loads each just before its use — a chain of dependent scalar-cache misses at
 // every wave start.  One scalar load per line, all in flight together and awaited once,
 // brings them into the scalar cache first (K3 single-frame 30.56 -> 30.28 us, K2 23.72 ->
-// 23.40, profiles/r02_ab_single_frame.log).
+// 23.40, profiles/r02_ab_single_frame.log).  Adding the first lines of the tile's candidate
+// and sphere records to it measured +1.0 us (the wave then waits for two HBM misses before
+// its first instruction of ray setup).
 #ifndef RT_KARG_PREFETCH
 #define RT_KARG_PREFETCH 1
 #endif
+// Leading scalar arguments of rt_trace_kernel (before the TraceParams block): what a wave
+// needs before its first ray — the tile's candidate count, the seed-hash tables, the
+// accumulator and the tile geometry.  Built with -mllvm -amdgpu-kernarg-preload-count=9
+// (Makefile), the command processor places these 9 dwords in SGPRs at wave launch, so the
+// count, hash and accumulator loads issue at once, together with the kernel-argument
+// prefetch, instead of after a kernarg round trip (K3 single-frame 30.7 -> 29.6 us, K2 23.7
+// -> 22.9, profiles/r02_ab_single_frame.log).  TraceParams (alignment 16) starts at byte 48.
+constexpr uint32_t kParamsOff = 48;
 __device__ __forceinline__ void karg_prefetch() {
-    const void kconst* kp = (const void kconst*)__builtin_amdgcn_kernarg_segment_ptr();
+    const char kconst* kp =
+        (const char kconst*)__builtin_amdgcn_kernarg_segment_ptr() + kParamsOff;
     uint32_t d0, d1, d2, d3, d4, d5, d6, d7, d8, d9, d10;
     asm volatile(
         "s_load_dword %0, %11, 0x0\n\t"
@@ -1084,12 +1100,13 @@ __device__ __forceinline__ void record_cost(const TraceParams& p, uint32_t tile,
 
 template <int kScan>
 __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt_trace_kernel(
+    const uint32_t* __restrict__ a_cnt, const uint32_t* __restrict__ a_hx,
+    const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const TraceParams p) {
     STAMP(-2);
     WAVE_TRACE(0);
-    if (RT_KARG_PREFETCH && kScan == kTraceList) karg_prefetch();
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t tiles_x = (p.width + 7u) >> 3;
+    const uint32_t tiles_x = (a_width + 7u) >> 3;
     // The wave index is uniform, but the compiler's divergence analysis does not know it;
     // readfirstlane makes the tile (and the candidate-list pointers and counts derived from
     // it) scalar, so list records are read with s_load into SGPRs.
@@ -1097,7 +1114,8 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     // (frame groups: all waves of the workgroup own the same tile)
     uint32_t tx = is_group_kernel(kScan) ? blockIdx.x : blockIdx.x * wg_waves<kScan>() + wave;
     uint32_t lband = blockIdx.y;
-    if (kOrdered<kScan> && p.tile_order) {            // costliest tiles first
+    const uint32_t band_first = a_bands & 0xFFFFu, band_step = (a_bands >> 16) & 0x7FFFu;
+    if (kOrdered<kScan> && (a_bands >> 31)) {         // costliest tiles first (tile_order)
         const uint32_t slot = blockIdx.y * gridDim.x + blockIdx.x;
         // (readfirstlane: the loaded value is uniform, but only the scalar form keeps the
         // list pointer and records in SGPRs — s_load chunks instead of vector loads)
@@ -1106,7 +1124,29 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
         lband = t >> 16;
     }
     const bool wave_in = tx < tiles_x;
-    const TileCoord tc = tile_coord(p, tx, lband, lane);
+    const TileCoord tc = tile_coord(a_width, a_height, band_first, band_step, tx, lband, lane);
+    const uint32_t tile = lband * tiles_x + tx;
+    // the tile's candidate count (kCandNone: no list), the accumulator (wgsl:339; a frame-0
+    // reset discards it: no load) and hash(x*73) ^ hash(y*51) (wgsl:309-310) from the
+    // per-column / per-row tables: issued from the preloaded arguments, before the
+    // kernel-argument prefetch below is awaited
+    const uint32_t ncand = (kScan != kTraceExhaustive && a_cnt && wave_in)
+                               ? ((const kconst uint32_t*)a_cnt)[tile]
+                               : kCandNone;
+#if RT_KO & 8
+    const float4 acc = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+#elif RT_KO & 32
+    // knock-out: no accumulator load; the count the hint expects (so no retrace)
+    const float4 acc = make_float4(0.0f, 0.0f, 0.0f, (float)p.hint_n[0]);
+#else
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    // (loaded even when frame 0 resets the pixel or the wave has no tile, so that the load
+    // waits for no kernarg read and no branch; the value is discarded then)
+    acc = a_in[tc.valid ? tc.idx : 0];
+#endif
+    const uint32_t hxy =
+        a_hx[min(tc.x, a_width - 1u)] ^ a_hx[hy_offset(a_width) + min(tc.y, a_height - 1u)];
+    if (RT_KARG_PREFETCH && kScan == kTraceList) karg_prefetch();
     // Culled scan: the workgroup stages the scan records (count padded to 64) in LDS once;
     // the per-block cone test then reads them at LDS latency instead of L2 latency.
     if (kScan == kTraceCulled && p.lds_records) {
@@ -1123,23 +1163,7 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
         __syncthreads();
     }
     if (!wave_in) return;                                         // whole wave exits
-    const uint32_t tile = lband * tiles_x + tx;
     cost_start<kScan>(p, tile, wave, lane);
-    // the tile's candidate count (kCandNone: no list)
-    const uint32_t ncand =
-        (kScan != kTraceExhaustive && p.cand_k) ? load_cnt(p, tile) : kCandNone;
-#if RT_KO & 8
-    const float4 acc = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-#elif RT_KO & 32
-    // knock-out: no accumulator load; the count the hint expects (so no retrace)
-    const float4 acc = make_float4(0.0f, 0.0f, 0.0f, (float)p.hint_n[0]);
-#else
-    // wgsl:339 (a frame-0 reset discards the value: no load)
-    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (!p.reset_first) acc = p.in[tc.valid ? tc.idx : 0];
-#endif
-    // hash(x*73) ^ hash(y*51) (wgsl:309-310) from the per-column / per-row tables
-    const uint32_t hxy = p.hx[min(tc.x, p.width - 1u)] ^ p.hy[min(tc.y, p.height - 1u)];
 
     Cam cam;
     cam.center = mk(p.center[0], p.center[1], p.center[2]);
@@ -1542,45 +1566,106 @@ hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, ui
     return hipGetLastError();
 }
 
-// One wave per tile: list the spheres the tile's camera rays can hit (see tile_cone).
-__global__ __launch_bounds__(256) void rt_candidates_kernel(const TraceParams p,
-                                                            uint32_t* __restrict__ cnt,
-                                                            float4* __restrict__ rec,
-                                                            float4* __restrict__ sph) {
-    const uint32_t lane = threadIdx.x & 63u;
+// List the spheres the camera rays of each tile can hit (see footprint_cone).
+// One wave per block of 8 x 8 tiles (8 columns of tiles x 8 local bands), one lane per
+// tile.  The wave first tests the spheres, 64 at a time, against the cone of the whole
+// block's footprint and stages the survivors (scan + sphere records, index order) in LDS,
+// up to kCandStage at a time; then every lane tests the staged spheres against its own
+// tile's cone, one sphere per step (an LDS broadcast), appending hits to its tile's list.
+// A sphere the block cone rejects provably misses every camera ray of the block (the same
+// exact margins as the tile test), so the lists hold every sphere a camera ray of the tile
+// can hit, in index order, and the scans over them return the full scan's bits.  (A block
+// whose cone is degenerate stages every sphere.)  Per tile the cone setup is done once per
+// lane and a sphere costs one cone test, instead of 64 lanes repeating the setup and
+// testing all spheres per tile.
+constexpr uint32_t kCandBlock = 8;     // tiles per block side
+constexpr uint32_t kCandStage = 256;   // block survivors staged per pass
+__global__ __launch_bounds__(64) void rt_candidates_kernel(const TraceParams p,
+                                                           uint32_t* __restrict__ cnt,
+                                                           float4* __restrict__ rec,
+                                                           float4* __restrict__ sph) {
+    __shared__ float4 s_rec[kCandStage];
+    __shared__ float4 s_sph[2 * kCandStage];
+    const float4* __restrict__ geom = p.geom;
+    const float4* __restrict__ gsph = p.sph;
+    const uint32_t count = p.count;
+    const uint32_t lane = threadIdx.x;
     const uint32_t tiles_x = (p.width + 7u) >> 3;
-    const uint32_t tx = blockIdx.x * 4u + (threadIdx.x >> 6), lband = blockIdx.y;
-    if (tx >= tiles_x) return;
-    const uint32_t tile = lband * tiles_x + tx;
-    const uint32_t K = p.cand_k;
+    const uint32_t tx0 = blockIdx.x * kCandBlock, lb0 = blockIdx.y * kCandBlock;
+    const uint32_t tx1 = min(tx0 + kCandBlock, tiles_x);
+    const uint32_t lb1 = min(lb0 + kCandBlock, p.local_bands);
+    const auto row0 = [&](uint32_t lb) {
+        return (float)((p.band_first + lb * p.band_step) * RT_STRIPE_ROWS);
+    };
+    Cone kb;
+    const bool blk = footprint_cone(p, (float)(tx0 * 8u), (float)(tx1 * 8u), row0(lb0),
+                                    row0(lb1 - 1u) + 8.0f, kb);
+    // this lane's tile and its cone
+    const uint32_t tx = tx0 + (lane & 7u), lb = lb0 + (lane >> 3);
+    const bool mine = tx < tx1 && lb < lb1;
     Cone k;
-    if (!tile_cone(p, tx, lband, k)) {
-        if (lane == 0) cnt[tile] = kCandNone;
-        return;
-    }
+    const bool ok = mine && footprint_cone(p, (float)(tx * 8u), (float)(tx * 8u + 8u), row0(lb),
+                                           row0(lb) + 8.0f, k);
+    const uint32_t tile = lb * tiles_x + tx;
+    const uint32_t K = p.cand_k;
+    const size_t tb = (size_t)tile * K;
     uint32_t n = 0;
-    for (uint32_t base = 0; base < p.count; base += 64u) {
-        const uint32_t i = base + lane;
-        const float4 g = p.geom[i < p.count ? i : 0u];
-        const bool keep = i < p.count && !cone_misses(k, g);
-        const unsigned long long mask = __ballot(keep);
-        if (keep) {
-            const uint32_t pos = n + __builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-            if (pos < K) {
-                const size_t slot = (size_t)tile * K + pos;
-                rec[slot] = g;
-                sph[2 * slot] = p.sph[2 * i];
-                sph[2 * slot + 1] = p.sph[2 * i + 1];
+    uint32_t base = 0;
+    // next block of 64 spheres, loaded one block ahead
+    uint32_t i = lane;
+    float4 g = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s0 = g, s1 = g;
+    if (count) {                                            // (no sphere: nothing to read)
+        const uint32_t ic = i < count ? i : 0u;
+        g = geom[ic];
+        s0 = gsph[2u * ic];
+        s1 = gsph[2u * ic + 1u];
+    }
+    while (base < count) {                                  // (uniform)
+        uint32_t m = 0;
+        while (base < count && m + 64u <= kCandStage) {     // stage block survivors
+            const float4 gc = g, c0 = s0, c1 = s1;
+            const bool keep = i < count && (!blk || !cone_misses(kb, gc));
+            base += 64u;
+            i = base + lane;
+            const uint32_t ic = i < count ? i : 0u;
+            g = geom[ic];
+            s0 = gsph[2u * ic];
+            s1 = gsph[2u * ic + 1u];
+            const unsigned long long mask = __ballot(keep);
+            if (keep) {
+                const uint32_t pos = m + __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                s_rec[pos] = gc;
+                s_sph[2u * pos] = c0;
+                s_sph[2u * pos + 1u] = c1;
+            }
+            m += (uint32_t)__builtin_popcountll(mask);
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (uint32_t j = 0; j < m; ++j) {                  // this lane's tile test
+            const float4 gj = s_rec[j];
+            if (ok && !cone_misses(k, gj)) {
+                if (n < K) {
+                    rec[tb + n] = gj;
+                    sph[2u * (tb + n)] = s_sph[2u * j];
+                    sph[2u * (tb + n) + 1u] = s_sph[2u * j + 1u];
+                }
+                ++n;
             }
         }
-        n += (uint32_t)__builtin_popcountll(mask);
+        __syncthreads();                                    // (the next pass restages)
+    }
+    if (!mine) return;
+    if (!ok) {
+        cnt[tile] = kCandNone;
+        return;
     }
     // zero the chunk padding after the last record
-    const uint32_t pad = ((n + 3u) & ~3u) - n;
-    if (n <= K && lane < pad && n + lane < K)
-        rec[(size_t)tile * K + n + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (lane == 0) cnt[tile] = n <= K ? n : kCandNone;
+    if (n <= K)
+        for (uint32_t q = n; q < ((n + 3u) & ~3u) && q < K; ++q)
+            rec[tb + q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    cnt[tile] = n <= K ? n : kCandNone;
 }
 
 __global__ __launch_bounds__(256) void rt_init_kernel(float4* __restrict__ out, uint64_t n) {
@@ -1776,7 +1861,9 @@ static void launch_trace_as(const TraceParams& p, size_t lds, hipStream_t stream
     constexpr uint32_t w = wg_waves<kScan>();
     const dim3 grid = tile_grid(p, is_group_kernel(kScan) ? 1u : w);
     if (grid.x == 0 || grid.y == 0) return;
-    hipLaunchKernelGGL(rt_trace_kernel<kScan>, grid, dim3(64 * w), lds, stream, p);
+    hipLaunchKernelGGL(rt_trace_kernel<kScan>, grid, dim3(64 * w), lds, stream, p.cand_cnt,
+                       p.hx, p.in, p.width, p.height,
+                       pack_bands(p.band_first, p.band_step, p.tile_order != nullptr), p);
 }
 
 // Workgroups of kBounceWaves tiles along a stripe band: grid (column groups, bands).
@@ -1815,9 +1902,11 @@ hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
 
 hipError_t launch_candidates(const TraceParams& p, uint32_t* cnt, float4* rec, float4* sph,
                              hipStream_t stream) {
-    const dim3 grid = tile_grid(p);
+    const uint32_t tiles_x = (p.width + 7u) >> 3;
+    const dim3 grid((tiles_x + kCandBlock - 1u) / kCandBlock,
+                    (p.local_bands + kCandBlock - 1u) / kCandBlock);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    hipLaunchKernelGGL(rt_candidates_kernel, grid, dim3(256), 0, stream, p, cnt, rec, sph);
+    hipLaunchKernelGGL(rt_candidates_kernel, grid, dim3(64), 0, stream, p, cnt, rec, sph);
     return hipGetLastError();
 }
 
