@@ -1570,7 +1570,8 @@ hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, ui
 // One wave per block of 8 x 8 tiles (8 columns of tiles x 8 local bands), one lane per
 // tile.  The wave first tests the spheres, 64 at a time, against the cone of the whole
 // block's footprint and stages the survivors (scan + sphere records, index order) in LDS,
-// up to kCandStage at a time; then every lane tests the staged spheres against its own
+// kCandStage spheres per pass with all their loads in flight together; then every lane
+// tests the staged spheres against its own
 // tile's cone, one sphere per step (an LDS broadcast), appending hits to its tile's list.
 // A sphere the block cone rejects provably misses every camera ray of the block (the same
 // exact margins as the tile test), so the lists hold every sphere a camera ray of the tile
@@ -1578,22 +1579,32 @@ hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, ui
 // whose cone is degenerate stages every sphere.)  Per tile the cone setup is done once per
 // lane and a sphere costs one cone test, instead of 64 lanes repeating the setup and
 // testing all spheres per tile.
-constexpr uint32_t kCandBlock = 8;     // tiles per block side
-constexpr uint32_t kCandStage = 256;   // block survivors staged per pass
+#ifndef RT_CAND_BX
+#define RT_CAND_BX 8
+#endif
+#ifndef RT_CAND_BY
+#define RT_CAND_BY 8
+#endif
+constexpr uint32_t kCandBX = RT_CAND_BX;   // block width in tiles
+constexpr uint32_t kCandBY = RT_CAND_BY;   // block height in local bands (kCandBX * kCandBY <= 64)
+static_assert(kCandBX * kCandBY <= 64, "one lane per tile");
+constexpr uint32_t kCandGroup = 8;                 // blocks of 64 spheres per pass
+constexpr uint32_t kCandStage = 64 * kCandGroup;   // spheres per pass
 __global__ __launch_bounds__(64) void rt_candidates_kernel(const TraceParams p,
                                                            uint32_t* __restrict__ cnt,
                                                            float4* __restrict__ rec,
                                                            float4* __restrict__ sph) {
     __shared__ float4 s_rec[kCandStage];
     __shared__ float4 s_sph[2 * kCandStage];
+    __shared__ uint32_t s_idx[kCandStage];
     const float4* __restrict__ geom = p.geom;
     const float4* __restrict__ gsph = p.sph;
     const uint32_t count = p.count;
     const uint32_t lane = threadIdx.x;
     const uint32_t tiles_x = (p.width + 7u) >> 3;
-    const uint32_t tx0 = blockIdx.x * kCandBlock, lb0 = blockIdx.y * kCandBlock;
-    const uint32_t tx1 = min(tx0 + kCandBlock, tiles_x);
-    const uint32_t lb1 = min(lb0 + kCandBlock, p.local_bands);
+    const uint32_t tx0 = blockIdx.x * kCandBX, lb0 = blockIdx.y * kCandBY;
+    const uint32_t tx1 = min(tx0 + kCandBX, tiles_x);
+    const uint32_t lb1 = min(lb0 + kCandBY, p.local_bands);
     const auto row0 = [&](uint32_t lb) {
         return (float)((p.band_first + lb * p.band_step) * RT_STRIPE_ROWS);
     };
@@ -1601,7 +1612,7 @@ __global__ __launch_bounds__(64) void rt_candidates_kernel(const TraceParams p,
     const bool blk = footprint_cone(p, (float)(tx0 * 8u), (float)(tx1 * 8u), row0(lb0),
                                     row0(lb1 - 1u) + 8.0f, kb);
     // this lane's tile and its cone
-    const uint32_t tx = tx0 + (lane & 7u), lb = lb0 + (lane >> 3);
+    const uint32_t tx = tx0 + lane % kCandBX, lb = lb0 + lane / kCandBX;
     const bool mine = tx < tx1 && lb < lb1;
     Cone k;
     const bool ok = mine && footprint_cone(p, (float)(tx * 8u), (float)(tx * 8u + 8u), row0(lb),
@@ -1610,40 +1621,36 @@ __global__ __launch_bounds__(64) void rt_candidates_kernel(const TraceParams p,
     const uint32_t K = p.cand_k;
     const size_t tb = (size_t)tile * K;
     uint32_t n = 0;
-    uint32_t base = 0;
-    // next block of 64 spheres, loaded one block ahead
-    uint32_t i = lane;
-    float4 g = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s0 = g, s1 = g;
-    if (count) {                                            // (no sphere: nothing to read)
-        const uint32_t ic = i < count ? i : 0u;
-        g = geom[ic];
-        s0 = gsph[2u * ic];
-        s1 = gsph[2u * ic + 1u];
-    }
-    while (base < count) {                                  // (uniform)
+    for (uint32_t gbase = 0; gbase < count; gbase += kCandStage) {   // (uniform)
+        // the group's scan records, all loads in flight together
+        float4 gv[kCandGroup];
+#pragma unroll
+        for (uint32_t b = 0; b < kCandGroup; ++b) {
+            const uint32_t i = gbase + b * 64u + lane;
+            gv[b] = geom[i < count ? i : 0u];
+        }
         uint32_t m = 0;
-        while (base < count && m + 64u <= kCandStage) {     // stage block survivors
-            const float4 gc = g, c0 = s0, c1 = s1;
-            const bool keep = i < count && (!blk || !cone_misses(kb, gc));
-            base += 64u;
-            i = base + lane;
-            const uint32_t ic = i < count ? i : 0u;
-            g = geom[ic];
-            s0 = gsph[2u * ic];
-            s1 = gsph[2u * ic + 1u];
+#pragma unroll
+        for (uint32_t b = 0; b < kCandGroup; ++b) {             // block-cone survivors
+            const uint32_t i = gbase + b * 64u + lane;
+            const bool keep = i < count && (!blk || !cone_misses(kb, gv[b]));
             const unsigned long long mask = __ballot(keep);
             if (keep) {
                 const uint32_t pos = m + __builtin_amdgcn_mbcnt_hi(
                     (uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                s_rec[pos] = gc;
-                s_sph[2u * pos] = c0;
-                s_sph[2u * pos + 1u] = c1;
+                s_rec[pos] = gv[b];
+                s_idx[pos] = i;
             }
             m += (uint32_t)__builtin_popcountll(mask);
         }
         __syncthreads();
-#pragma unroll 4
-        for (uint32_t j = 0; j < m; ++j) {                  // this lane's tile test
+        for (uint32_t j = lane; j < m; j += 64u) {              // their sphere records
+            const uint32_t i = s_idx[j];
+            s_sph[2u * j] = gsph[2u * i];
+            s_sph[2u * j + 1u] = gsph[2u * i + 1u];
+        }
+        __syncthreads();
+        for (uint32_t j = 0; j < m; ++j) {                      // this lane's tile test
             const float4 gj = s_rec[j];
             if (ok && !cone_misses(k, gj)) {
                 if (n < K) {
@@ -1654,7 +1661,7 @@ __global__ __launch_bounds__(64) void rt_candidates_kernel(const TraceParams p,
                 ++n;
             }
         }
-        __syncthreads();                                    // (the next pass restages)
+        __syncthreads();                                        // (the next group restages)
     }
     if (!mine) return;
     if (!ok) {
@@ -1903,8 +1910,8 @@ hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
 hipError_t launch_candidates(const TraceParams& p, uint32_t* cnt, float4* rec, float4* sph,
                              hipStream_t stream) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
-    const dim3 grid((tiles_x + kCandBlock - 1u) / kCandBlock,
-                    (p.local_bands + kCandBlock - 1u) / kCandBlock);
+    const dim3 grid((tiles_x + kCandBX - 1u) / kCandBX,
+                    (p.local_bands + kCandBY - 1u) / kCandBY);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
     hipLaunchKernelGGL(rt_candidates_kernel, grid, dim3(64), 0, stream, p, cnt, rec, sph);
     return hipGetLastError();
