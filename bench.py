@@ -11,7 +11,7 @@ Configs (BASELINE.json `configs`):
                     step is one 64-spp render from a reset accumulator: 64 chained updates
                     issued by one rt_update_frames call (fused launches of up to 64 frames).
   K5                3840x2160, 500 spheres, 64 spp, 8 bounces — the multi-GPU config.  A step
-                    is one 64-spp render (bounce instance, one launch per frame).
+                    is one 64-spp render (one 64-frame launch of the bounce instance).
 With N GPUs (one process per GPU, torch.distributed.run) the image is split into 8-row bands
 dealt round-robin; after the K timed steps the finished tiles are gathered to rank 0 with ONE
 RCCL gather + the de-interleave kernel, both inside the timed region.
