@@ -42,9 +42,7 @@ struct rt_ctx {
         float x0, z0, s, inv_s, ylo, yhi, cx, cy, cz, reach, m, e;
     } grid;
     // Per-tile candidate lists of camera rays (culled scan), valid for cand_key.
-    uint32_t* cand_cnt = nullptr;
-    float4* cand_rec = nullptr;
-    float4* cand_sph = nullptr;
+    float4* cand = nullptr;   // [tile][rtk::kCandStride] candidate blocks
     uint64_t cand_tiles = 0;        // allocated tiles
     std::vector<unsigned char> cand_key;
     uint64_t cand_gen = 0;          // bumped whenever the lists are rebuilt
@@ -426,12 +424,8 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
 }
 
 void free_candidates(rt_ctx* ctx) {
-    (void)hipFree(ctx->cand_cnt);
-    (void)hipFree(ctx->cand_rec);
-    (void)hipFree(ctx->cand_sph);
-    ctx->cand_cnt = nullptr;
-    ctx->cand_rec = nullptr;
-    ctx->cand_sph = nullptr;
+    (void)hipFree(ctx->cand);
+    ctx->cand = nullptr;
     ctx->cand_tiles = 0;
     ctx->cand_key.clear();
 }
@@ -471,26 +465,19 @@ rt_status ensure_candidates(rt_ctx* ctx, rtk::TraceParams& p, hipStream_t stream
                 if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
             }
             free_candidates(ctx);
-            const uint64_t slots = tiles * rtk::kCandMax;
-            hipError_t e = hipMalloc(&ctx->cand_cnt, tiles * sizeof(uint32_t));
-            // + one chunk: the scan prefetches a chunk past the last tile's list
-            if (e == hipSuccess) e = hipMalloc(&ctx->cand_rec, (slots + 4) * sizeof(float4));
-            if (e == hipSuccess) e = hipMalloc(&ctx->cand_sph, slots * 2 * sizeof(float4));
+            hipError_t e = hipMalloc(&ctx->cand, tiles * rtk::kCandStride * sizeof(float4));
             if (e != hipSuccess) {
                 free_candidates(ctx);
                 return hip_fail(e, "hipMalloc(candidate lists)");
             }
             ctx->cand_tiles = tiles;
         }
-        hipError_t e = rtk::launch_candidates(p, ctx->cand_cnt, ctx->cand_rec, ctx->cand_sph,
-                                              stream);
+        hipError_t e = rtk::launch_candidates(p, ctx->cand, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_candidates_kernel launch");
         ctx->cand_key.assign(kb, kb + sizeof(key));
         ctx->cand_gen++;
     }
-    p.cand_cnt = ctx->cand_cnt;
-    p.cand_rec = ctx->cand_rec;
-    p.cand_sph = ctx->cand_sph;
+    p.cand = ctx->cand;
     return RT_OK;
 }
 
@@ -507,7 +494,7 @@ rt_status plan_tile_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
     // (single-frame launches keep raster order: their accumulator traffic is a large part
     // of the frame, and scattered tiles cost more in HBM than the tail they save)
     const bool bounce = kernel == rtk::kTraceBounce;
-    if (!(rtk::is_list_kernel(kernel) || bounce) || ctx->tile_order_mode == RT_TILE_ORDER_OFF ||
+    if (!(rtk::trace_ordered(kernel) || bounce) || ctx->tile_order_mode == RT_TILE_ORDER_OFF ||
         p.cand_k == 0 || p.frames < 2)
         return RT_OK;
     // scheduling units: 8x8 tiles, or the compacting bounce instance's workgroups of
@@ -840,7 +827,7 @@ rt_status rt_destroy(rt_ctx* ctx) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     {
         DeviceGuard guard(ctx->device);
-        if (ctx->d_geom || ctx->d_sph || ctx->cand_cnt) (void)hipDeviceSynchronize();
+        if (ctx->d_geom || ctx->d_sph || ctx->cand) (void)hipDeviceSynchronize();
         (void)hipFree(ctx->d_geom);
         (void)hipFree(ctx->d_sph);
         (void)hipFree(ctx->d_srgb);

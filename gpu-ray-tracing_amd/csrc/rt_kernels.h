@@ -14,9 +14,19 @@ namespace rtk {
 constexpr uint32_t kMaxFramesPerLaunch = 128;
 // Culled scan: lists up to this many spheres are staged in LDS (64 KiB per workgroup).
 constexpr uint32_t kLdsMaxRecords = 4096;
-// Per-tile candidate lists of camera rays (culled scan): capacity and the "no list" mark.
-constexpr uint32_t kCandMax = 32;
+// Per-tile candidate blocks of camera rays (culled scan), kCandStride float4 (1 KB) per
+// tile: [0] the count (u32 bits of .x; kCandNone = no list), [kCandRecOff + j] the scan
+// record of entry j (index order; the record slots past the count are zero up to a whole
+// chunk of 4 and anything after — the scans read whole chunks and a chunk ahead, but only
+// consider indices < count), [kCandSphOff + 2j, +1] entry j's 32-B sphere record.  A wave
+// can fetch its tile's whole list with one 16-B load per lane.
+constexpr uint32_t kCandStride = 64;
+constexpr uint32_t kCandMax = 19;
+constexpr uint32_t kCandRecOff = 1;
+constexpr uint32_t kCandSphOff = 21;
 constexpr uint32_t kCandNone = 0xFFFFFFFFu;
+static_assert(kCandRecOff + ((kCandMax + 3u) & ~3u) <= kCandSphOff, "record chunks fit");
+static_assert(kCandSphOff + 2u * kCandMax <= kCandStride, "sphere records fit");
 // Sample-count hint (see TraceParams::hint_n): per-(frame, bounce) random numbers of the
 // scatter step for at most kHintEntries (frame, bounce) pairs of the first kHintFrames
 // frames of a launch.
@@ -44,9 +54,7 @@ struct TraceParams {
     uint32_t reset_first;  // camera_has_moved > 0.5 applies to frame 0 only
     uint32_t lds_records;  // culled scan: records staged in LDS (0 = read from HBM/L2)
     uint32_t cand_k;       // per-tile candidate list capacity (0 = no lists)
-    const uint32_t* cand_cnt;  // [tile] listed spheres, kCandNone = no list
-    const float4* cand_rec;    // [tile][cand_k] their scan records, in index order, padded
-    const float4* cand_sph;    // [tile][cand_k][2] their 32-B GpuSphere records
+    const float4* cand;    // [tile][kCandStride] candidate blocks (see kCandStride)
     // Uniform XZ grid over the small spheres for bounce rays (rt_kernels.hip scan_grid;
     // built by rt_abi.cpp build_grid): per cell the range of its items, each item a copy
     // of the sphere's scan record and its index (every small sphere is registered in the
@@ -122,6 +130,17 @@ constexpr int kTraceBounce = 5;
 constexpr uint32_t kBounceWaves = 4;   // tiles (waves) per bounce workgroup
 constexpr bool is_group_kernel(int k) { return k == kTraceListPair || k == kTraceListQuad; }
 constexpr bool is_list_kernel(int k) { return k == kTraceList || is_group_kernel(k); }
+// Waves (tiles) per workgroup of the one-wave-per-tile instances (kTraceExhaustive,
+// kTraceList): four-wave workgroups dispatch faster than one-wave ones (K3 single-frame
+// update 29.9 -> 29.1 us, K2 23.0 -> 22.1, profiles/r02_ab_single_frame.log).
+#ifndef RT_WG_WAVES
+#define RT_WG_WAVES 4
+#endif
+// Instances that run cost-ordered tiles (one tile per workgroup): the frame groups, and
+// kTraceList when its workgroups are one wave.
+constexpr bool trace_ordered(int k) {
+    return is_list_kernel(k) && (is_group_kernel(k) || RT_WG_WAVES == 1);
+}
 // Tiles per launch at or below which frame groups of four are used.
 constexpr uint64_t kQuadMaxTiles = 6144;
 // The seed-hash tables share one buffer: hash(x*73) for x < hy_offset(width), then
@@ -135,9 +154,9 @@ constexpr uint32_t pack_bands(uint32_t first, uint32_t step, bool ordered) {
 }
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream);
 hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream);
-// Builds the per-tile candidate lists for p's camera/scene/stripes (p.cand_k slots each).
-hipError_t launch_candidates(const TraceParams& p, uint32_t* cnt, float4* rec, float4* sph,
-                             hipStream_t stream);
+// Builds the per-tile candidate blocks for p's camera/scene/stripes (p.cand_k entries at
+// most per tile).
+hipError_t launch_candidates(const TraceParams& p, float4* cand, hipStream_t stream);
 hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t width,
                                uint32_t height, uint32_t nranks, uint32_t max_local_rows,
                                hipStream_t stream);

@@ -26,7 +26,8 @@ using namespace rtd;
 // Knock-out builds for cost attribution only (tools; never the product): RT_KO bit 1 skips
 // the sphere scan, 2 the shading, 4 the random camera ray, 8 the accumulator load, 16 the
 // store, 32 the accumulator load (keeping the hinted count), 64 the accumulator's divisions
-// of the frame-group path (c = col), 128 the sky's normalisation (uy = d.y).
+// of the frame-group path (c = col), 128 the sky's normalisation (uy = d.y), 256 every
+// tile walks tile 0's candidate list (L2-resident lists: the cost of the list misses).
 #ifndef RT_KO
 #define RT_KO 0
 #endif
@@ -249,8 +250,8 @@ __device__ __forceinline__ float4 load_rec(const float4* __restrict__ geom, uint
 
 // A tile's candidate count through the constant address space: a scalar load (the lists do
 // not change during a launch), not a vector load + readfirstlane.
-__device__ __forceinline__ uint32_t load_cnt(const TraceParams& p, uint32_t tile) {
-    return ((const kconst uint32_t*)p.cand_cnt)[tile];
+__device__ __forceinline__ uint32_t load_cnt(const float4* cand, uint32_t tile) {
+    return ((const kconst uint32_t*)cand)[(size_t)tile * (4u * kCandStride)];
 }
 
 // kFast: camera rays in the host-proven domain (consider_fast).  kScalar: read the records
@@ -710,7 +711,7 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
         // so the same chunk loop applies; hit.idx then indexes the tile's copy of the
         // sphere records.
         const bool listed = kScan != kTraceExhaustive && i == 0 && ncand != kCandNone;
-        const size_t lbase = (size_t)tile * p.cand_k;
+        const float4* blk = p.cand + ((RT_KO & 256) ? 0 : (size_t)tile * kCandStride);
 #if RT_KO & 1
         const Hit hit = Hit{-1, 0.0f};
 #else
@@ -718,12 +719,12 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
         const Hit hit =
             (kScan != kTraceCulled || listed)
                 ? scan_exhaustive<scan_chunk<kScan>(), fast_core<kScan>(1), kScan != kTraceList>(
-                      listed ? p.cand_rec + lbase : p.geom, listed ? ncand : p.count, o, d)
+                      listed ? blk + kCandRecOff : p.geom, listed ? ncand : p.count, o, d)
             : p.lds_records ? scan_culled<true>(p, p.geom, p.count, o, d, live, i > 0)
                             : scan_culled<false>(p, p.geom, p.count, o, d, live, i > 0);
 #endif
         if (kScan != kTraceCulled) STAMP(2);                      // (culled: inside the scan)
-        const float4* hs = listed ? p.cand_sph + 2 * lbase : p.sph;
+        const float4* hs = listed ? blk + kCandSphOff : p.sph;
         if (!live) continue;
         if (hit.idx < 0) {                                        // wgsl:288-290
             live = false;
@@ -1022,11 +1023,7 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
 #define RT_TRACE_MIN_WAVES 7
 #endif
 // Waves (tiles) per workgroup: the culled instance shares the LDS copy of the records
-// among 4 waves; the others use one-wave workgroups, so a finished tile frees its slot
-// without waiting for slower neighbours.
-#ifndef RT_WG_WAVES
-#define RT_WG_WAVES 1
-#endif
+// among 4 waves; the others use RT_WG_WAVES (rt_kernels.h).
 // Kernel-argument prefetch (single-frame list instance, one tile per wave): the launch
 // parameters a wave reads are spread over ~12 cache lines of the 2.6-KB kernarg segment and
 // the compiler loads each just before its use — a chain of dependent scalar-cache misses at
@@ -1035,6 +1032,20 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
 // 23.40, profiles/r02_ab_single_frame.log).  Adding the first lines of the tile's candidate
 // and sphere records to it measured +1.0 us (the wave then waits for two HBM misses before
 // its first instruction of ray setup).
+// Image accesses of the trace kernel as non-temporal (streaming) loads (bit 1) / stores
+// (bit 2), so that the per-frame image traffic does not evict the candidate lists from L2.
+#ifndef RT_NT_IMAGE
+#define RT_NT_IMAGE 0
+#endif
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 nt_load(const float4* a) {
+    const f32x4 v = __builtin_nontemporal_load((const f32x4*)a);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nt_store(float4 v, float4* a) {
+    const f32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (f32x4*)a);
+}
 #ifndef RT_KARG_PREFETCH
 #define RT_KARG_PREFETCH 1
 #endif
@@ -1082,8 +1093,7 @@ constexpr uint32_t wg_waves() {
 // instances, whose workgroups are one tile each.
 
 template <int kScan>
-constexpr bool kOrdered =
-    is_list_kernel(kScan) && (is_group_kernel(kScan) || wg_waves<kScan>() == 1u);
+constexpr bool kOrdered = trace_ordered(kScan);
 // (the start time is parked in tile_cost itself: no register stays live for it)
 template <int kScan>
 __device__ __forceinline__ void cost_start(const TraceParams& p, uint32_t tile, uint32_t wave,
@@ -1100,7 +1110,7 @@ __device__ __forceinline__ void record_cost(const TraceParams& p, uint32_t tile,
 
 template <int kScan>
 __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt_trace_kernel(
-    const uint32_t* __restrict__ a_cnt, const uint32_t* __restrict__ a_hx,
+    const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const TraceParams p) {
     STAMP(-2);
@@ -1130,8 +1140,8 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     // reset discards it: no load) and hash(x*73) ^ hash(y*51) (wgsl:309-310) from the
     // per-column / per-row tables: issued from the preloaded arguments, before the
     // kernel-argument prefetch below is awaited
-    const uint32_t ncand = (kScan != kTraceExhaustive && a_cnt && wave_in)
-                               ? ((const kconst uint32_t*)a_cnt)[tile]
+    const uint32_t ncand = (kScan != kTraceExhaustive && a_cand && wave_in)
+                               ? load_cnt(a_cand, (RT_KO & 256) ? 0 : tile)
                                : kCandNone;
 #if RT_KO & 8
     const float4 acc = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
@@ -1142,7 +1152,10 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     // (loaded even when frame 0 resets the pixel or the wave has no tile, so that the load
     // waits for no kernarg read and no branch; the value is discarded then)
-    acc = a_in[tc.valid ? tc.idx : 0];
+    if (RT_NT_IMAGE & 1)
+        acc = nt_load(&a_in[tc.valid ? tc.idx : 0]);
+    else
+        acc = a_in[tc.valid ? tc.idx : 0];
 #endif
     const uint32_t hxy =
         a_hx[min(tc.x, a_width - 1u)] ^ a_hx[hy_offset(a_width) + min(tc.y, a_height - 1u)];
@@ -1191,7 +1204,12 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
 #if RT_KO & 16
     if (res.x == 12345.678f) p.out[tc.idx] = res;
 #else
-    if (tc.valid && !(kStoreEach<kScan> && p.store_each)) p.out[tc.idx] = res;  // wgsl:363
+    if (tc.valid && !(kStoreEach<kScan> && p.store_each)) {      // wgsl:363
+        if (RT_NT_IMAGE & 2)
+            nt_store(res, &p.out[tc.idx]);
+        else
+            p.out[tc.idx] = res;
+    }
 #endif
     record_cost<kScan>(p, tile, wave, lane);
     WAVE_TRACE(1);
@@ -1331,8 +1349,8 @@ rt_bounce_kernel(const TraceParams p) {
         p.tile_cost[group] = (uint32_t)__builtin_amdgcn_s_memtime();
     if (p.lds_records || kW > 1u) __syncthreads();
     const uint32_t tile = lband * tiles_x + (wave_in ? tx : 0u);
-    const uint32_t ncand = (p.cand_k && wave_in) ? load_cnt(p, tile) : kCandNone;
-    const size_t lbase = (size_t)tile * p.cand_k;
+    const uint32_t ncand = (p.cand_k && wave_in) ? load_cnt(p.cand, tile) : kCandNone;
+    const float4* blk = p.cand + (size_t)tile * kCandStride;
     const uint32_t hxy = p.hx[min(tc.x, p.width - 1u)] ^ p.hy[min(tc.y, p.height - 1u)];
     Cam cam;
     cam.center = mk(p.center[0], p.center[1], p.center[2]);
@@ -1384,11 +1402,11 @@ rt_bounce_kernel(const TraceParams p) {
             const float4* hs = p.sph;
             if (__ballot(live) != 0ull) {
                 const bool listed = i == 0u && ncand != kCandNone;
-                hit = listed ? scan_exhaustive<RT_SCAN_CHUNK, false, true>(p.cand_rec + lbase,
+                hit = listed ? scan_exhaustive<RT_SCAN_CHUNK, false, true>(blk + kCandRecOff,
                                                                           ncand, o, d)
                       : p.lds_records ? scan_culled<true>(p, p.geom, p.count, o, d, live, i > 0)
                                       : scan_culled<false>(p, p.geom, p.count, o, d, live, i > 0);
-                if (listed) hs = p.cand_sph + 2 * lbase;
+                if (listed) hs = blk + kCandSphOff;
             }
             bool done = false, keep = false;
             v3 col = mk(0.0f, 0.0f, 0.0f);
@@ -1591,9 +1609,7 @@ static_assert(kCandBX * kCandBY <= 64, "one lane per tile");
 constexpr uint32_t kCandGroup = 8;                 // blocks of 64 spheres per pass
 constexpr uint32_t kCandStage = 64 * kCandGroup;   // spheres per pass
 __global__ __launch_bounds__(64) void rt_candidates_kernel(const TraceParams p,
-                                                           uint32_t* __restrict__ cnt,
-                                                           float4* __restrict__ rec,
-                                                           float4* __restrict__ sph) {
+                                                           float4* __restrict__ cand) {
     __shared__ float4 s_rec[kCandStage];
     __shared__ float4 s_sph[2 * kCandStage];
     __shared__ uint32_t s_idx[kCandStage];
@@ -1609,7 +1625,7 @@ __global__ __launch_bounds__(64) void rt_candidates_kernel(const TraceParams p,
         return (float)((p.band_first + lb * p.band_step) * RT_STRIPE_ROWS);
     };
     Cone kb;
-    const bool blk = footprint_cone(p, (float)(tx0 * 8u), (float)(tx1 * 8u), row0(lb0),
+    const bool in_blk = footprint_cone(p, (float)(tx0 * 8u), (float)(tx1 * 8u), row0(lb0),
                                     row0(lb1 - 1u) + 8.0f, kb);
     // this lane's tile and its cone
     const uint32_t tx = tx0 + lane % kCandBX, lb = lb0 + lane / kCandBX;
@@ -1619,7 +1635,9 @@ __global__ __launch_bounds__(64) void rt_candidates_kernel(const TraceParams p,
                                            row0(lb) + 8.0f, k);
     const uint32_t tile = lb * tiles_x + tx;
     const uint32_t K = p.cand_k;
-    const size_t tb = (size_t)tile * K;
+    float4* const own = cand + (size_t)tile * kCandStride;
+    float4* const rec = own + kCandRecOff;
+    float4* const sph = own + kCandSphOff;
     uint32_t n = 0;
     for (uint32_t gbase = 0; gbase < count; gbase += kCandStage) {   // (uniform)
         // the group's scan records, all loads in flight together
@@ -1633,7 +1651,7 @@ __global__ __launch_bounds__(64) void rt_candidates_kernel(const TraceParams p,
 #pragma unroll
         for (uint32_t b = 0; b < kCandGroup; ++b) {             // block-cone survivors
             const uint32_t i = gbase + b * 64u + lane;
-            const bool keep = i < count && (!blk || !cone_misses(kb, gv[b]));
+            const bool keep = i < count && (!in_blk || !cone_misses(kb, gv[b]));
             const unsigned long long mask = __ballot(keep);
             if (keep) {
                 const uint32_t pos = m + __builtin_amdgcn_mbcnt_hi(
@@ -1654,9 +1672,9 @@ __global__ __launch_bounds__(64) void rt_candidates_kernel(const TraceParams p,
             const float4 gj = s_rec[j];
             if (ok && !cone_misses(k, gj)) {
                 if (n < K) {
-                    rec[tb + n] = gj;
-                    sph[2u * (tb + n)] = s_sph[2u * j];
-                    sph[2u * (tb + n) + 1u] = s_sph[2u * j + 1u];
+                    rec[n] = gj;
+                    sph[2u * n] = s_sph[2u * j];
+                    sph[2u * n + 1u] = s_sph[2u * j + 1u];
                 }
                 ++n;
             }
@@ -1664,15 +1682,12 @@ __global__ __launch_bounds__(64) void rt_candidates_kernel(const TraceParams p,
         __syncthreads();                                        // (the next group restages)
     }
     if (!mine) return;
-    if (!ok) {
-        cnt[tile] = kCandNone;
-        return;
-    }
+    const uint32_t c = ok && n <= K ? n : kCandNone;
     // zero the chunk padding after the last record
-    if (n <= K)
-        for (uint32_t q = n; q < ((n + 3u) & ~3u) && q < K; ++q)
-            rec[tb + q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    cnt[tile] = n <= K ? n : kCandNone;
+    if (c != kCandNone)
+        for (uint32_t q = n; q < ((n + 3u) & ~3u); ++q)
+            rec[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    own[0] = make_float4(__uint_as_float(c), 0.0f, 0.0f, 0.0f);
 }
 
 __global__ __launch_bounds__(256) void rt_init_kernel(float4* __restrict__ out, uint64_t n) {
@@ -1868,7 +1883,7 @@ static void launch_trace_as(const TraceParams& p, size_t lds, hipStream_t stream
     constexpr uint32_t w = wg_waves<kScan>();
     const dim3 grid = tile_grid(p, is_group_kernel(kScan) ? 1u : w);
     if (grid.x == 0 || grid.y == 0) return;
-    hipLaunchKernelGGL(rt_trace_kernel<kScan>, grid, dim3(64 * w), lds, stream, p.cand_cnt,
+    hipLaunchKernelGGL(rt_trace_kernel<kScan>, grid, dim3(64 * w), lds, stream, p.cand,
                        p.hx, p.in, p.width, p.height,
                        pack_bands(p.band_first, p.band_step, p.tile_order != nullptr), p);
 }
@@ -1907,13 +1922,12 @@ hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_candidates(const TraceParams& p, uint32_t* cnt, float4* rec, float4* sph,
-                             hipStream_t stream) {
+hipError_t launch_candidates(const TraceParams& p, float4* cand, hipStream_t stream) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     const dim3 grid((tiles_x + kCandBX - 1u) / kCandBX,
                     (p.local_bands + kCandBY - 1u) / kCandBY);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    hipLaunchKernelGGL(rt_candidates_kernel, grid, dim3(64), 0, stream, p, cnt, rec, sph);
+    hipLaunchKernelGGL(rt_candidates_kernel, grid, dim3(64), 0, stream, p, cand);
     return hipGetLastError();
 }
 
