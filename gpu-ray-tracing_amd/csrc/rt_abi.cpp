@@ -73,6 +73,7 @@ struct rt_ctx {
     rt_launch_info last = {0, 0, 0, -1};  // the last call's launches (rt_last_launch_info)
     int path_compaction = RT_PATHS_AUTO;
     int frame_pairs = RT_FRAME_PAIRS_AUTO;
+    int single_kernel = RT_SINGLE_AUTO;
 };
 
 namespace {
@@ -174,6 +175,15 @@ int trace_kernel_for(const rt_ctx* ctx, const rtk::TraceParams& p) {
     if (p.depth >= 2u) return rtk::kTraceBounce;
 #endif
     return rtk::kTraceCulled;
+}
+
+// One-frame launches of the camera-ray-only instance run rt_single_kernel (rt_kernels.hip)
+// unless rt_set_single_kernel(OFF).
+int single_or(const rt_ctx* ctx, const rtk::TraceParams& p, int kernel) {
+    if (kernel == rtk::kTraceList && p.frames == 1u && ctx->single_kernel == RT_SINGLE_AUTO &&
+        p.cand)
+        return rtk::kTraceSingle;
+    return kernel;
 }
 
 // Frames per rt_update_frames launch (see rt_update_frames).  Only the camera-ray-only
@@ -774,7 +784,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         p.reset_first = (f0 == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
         for (uint32_t f = 0; f < nf; ++f) p.seed_b[f] = host_f2u(seeds[f0 + f] * 4294967296.0f);
         plan_hint(ctx, p, src, dst);
-        const int kernel = trace_kernel_for(ctx, p);
+        const int kernel = single_or(ctx, p, trace_kernel_for(ctx, p));
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
@@ -797,7 +807,8 @@ const char* rt_kernel_name(int which) {
     static const char* const names[] = {"rt_trace_kernel<0>",      "rt_trace_kernel<1>",
                                         "rt_trace_kernel<2>",      "rt_trace_kernel<3>",
                                         "rt_trace_kernel<4>",      "rt_bounce_kernel<0>",
-                                        "rt_bounce_kernel<1>",     "rt_bounce_kernel<2>"};
+                                        "rt_bounce_kernel<1>",     "rt_bounce_kernel<2>",
+                                        rtk::single_kernel_name()};
     if (which >= 0 && which < (int)(sizeof(names) / sizeof(names[0]))) return names[which];
     return rtk::trace_kernel_name();
 }
@@ -870,6 +881,14 @@ rt_status rt_set_path_compaction(rt_ctx* ctx, int mode) {
         mode != RT_PATHS_PAIR)
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown path-compaction mode");
     ctx->path_compaction = mode;
+    return RT_OK;
+}
+
+rt_status rt_set_single_kernel(rt_ctx* ctx, int mode) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (mode != RT_SINGLE_AUTO && mode != RT_SINGLE_OFF)
+        return fail(RT_ERR_INVALID_ARGUMENT, "unknown single-kernel mode");
+    ctx->single_kernel = mode;
     return RT_OK;
 }
 
@@ -991,6 +1010,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
                               (ctx->frame_pairs == RT_FRAME_PAIRS_AUTO && tiles <= rtk::kQuadMaxTiles);
             kernel = quad ? rtk::kTraceListQuad : rtk::kTraceListPair;
         }
+        kernel = single_or(ctx, p, kernel);
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");

@@ -128,6 +128,10 @@ static_assert(kTraceExhaustive == RT_KERNEL_EXHAUSTIVE && kTraceCulled == RT_KER
 // the workgroup's waves after every bounce (rt_kernels.hip, rt_bounce_kernel).
 constexpr int kTraceBounce = 5;
 constexpr uint32_t kBounceWaves = 4;   // tiles (waves) per bounce workgroup
+// One frame per launch of the camera-ray-only case (rt_update / a one-frame rt_update_frames
+// launch with the kTraceList conditions): rt_kernels.hip, rt_single_kernel.
+constexpr int kTraceSingle = 8;
+static_assert(kTraceSingle == RT_KERNEL_SINGLE, "instance id is the ABI's RT_KERNEL_SINGLE");
 constexpr bool is_group_kernel(int k) { return k == kTraceListPair || k == kTraceListQuad; }
 constexpr bool is_list_kernel(int k) { return k == kTraceList || is_group_kernel(k); }
 // Waves (tiles) per workgroup of the one-wave-per-tile instances (kTraceExhaustive,
@@ -165,6 +169,8 @@ hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t wid
 hipError_t launch_present(const float4* in, uchar4* out, uint64_t texels,
                           const float* srgb_t, hipStream_t stream);
 const char* trace_kernel_name();
+// "rt_single_kernel<p>" with p = the pixels per lane it was built with
+const char* single_kernel_name();
 // tile_order for launch_trace: the local tiles by decreasing recorded cost (quantised
 // log2 of tile_cost), so the slowest tiles start first and the cheap ones fill the tail.
 hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, uint32_t tiles,

@@ -1216,6 +1216,358 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     STAMP(5);
 }
 
+// ---- Single-frame update (kTraceSingle): one `update` dispatch, camera rays only --------
+//
+// The reference's step (lib.rs:408-417: one `update` per frame, wgsl:333-364) at
+// max_depth <= 1 for cameras in the proven domain (the kTraceList conditions) and one frame
+// per launch.  rt_trace_kernel<kTraceList> pays its general machinery (frame loop, retrace
+// loop, per-frame kernarg reads spread over a 2.6-KB parameter block) for the one frame;
+// this kernel does the one frame only, with its parameters in one compact block, and gives
+// each lane kSinglePix pixels — the same column of kSinglePix horizontally adjacent 8x8
+// tiles — so that a wave's fixed costs (launch, parameter and list loads, the disk table)
+// are shared and its independent pixel chains interleave (more instructions in flight per
+// wave while the list and accumulator loads are outstanding).  The per-pixel arithmetic is
+// ray_color's (wgsl:261-297) for depth <= 1, operation for operation: the image bits are
+// those of rt_trace_kernel (every parity test runs both, rt_set_single_kernel).
+struct SingleParams {
+    float4* out;
+    const float4* geom;    // full scan records (tiles without a candidate list)
+    const float4* sph;     // full sphere records
+    uint32_t count, depth, spp, reset;
+    uint32_t hinted;       // hint_n / hint_rcp / hint_rs of frame 0 are valid
+    uint32_t n_hint;       // every pixel's count before the frame (0 on reset)
+    uint32_t seed_b;       // B = u32(random_seed * 2^32) (wgsl:311, 353)
+    uint32_t hy_off;       // hash(y * 51) table offset in the hx buffer
+    double rcp_hint;       // RN64(1 / (n_hint + 1))
+    float4 rs;             // (rf(sb), random_unit_vector(sb)) of frame 0, bounce 0
+    double disk_rcp[8];
+    float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3];
+    float defocus_angle;
+};
+
+#ifndef RT_SINGLE_PIX
+#define RT_SINGLE_PIX 2
+#endif
+constexpr uint32_t kSinglePix = RT_SINGLE_PIX;
+#ifndef RT_SINGLE_MIN_WAVES
+#define RT_SINGLE_MIN_WAVES 5
+#endif
+#ifndef RT_SINGLE_ACC_F64
+#define RT_SINGLE_ACC_F64 1
+#endif
+
+// Shading of a camera ray's hit at depth 1 (ray_color's loop body at i = 0, wgsl:266-286):
+// sets the scattered direction and attenuation, or black (metal absorbed).  r_sb / ruv are
+// the scatter's random numbers.  Lanes with !hit compute garbage that the caller drops.
+__device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, v3 d,
+                                          float r_sb, v3 ruv, bool hit, v3& nd, v3& att,
+                                          bool& black) {
+    const v3 hp = fmas(t, d, o);
+    const v3 rel = sub(hp, mk(pr.x, pr.y, pr.z));
+    v3 outward;                                                   // wgsl:209
+    if (__ballot(hit && min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z)) <
+                            kBits2m100) == 0ull) {
+        const float y = rcp_refined(pr.w);
+        outward = mk(div_core(rel.x, pr.w, y), div_core(rel.y, pr.w, y),
+                     div_core(rel.z, pr.w, y));
+    } else {
+        outward = divs(rel, pr.w);
+    }
+    const bool front = dot(d, outward) < 0.0f;
+    const v3 n = front ? outward : neg(outward);
+    // lambertian (wgsl:84-93), computed for every lane; the other materials below
+    v3 dir = add(n, ruv);
+    if (dot(dir, dir) < 0x1.0c6f7ap-20f) dir = n;
+    nd = dir;
+    att = mk(mat.x, mat.y, mat.z);
+    black = false;
+    const bool other = hit && !(mat.w < -1.0f);
+    if (__ballot(other) != 0ull && other) {
+        if (mat.w <= 1.0f) {                                      // metal wgsl:95-100
+            const v3 refl = fmas(mat.w, ruv, normalize_w<true>(reflect(d, n)));
+            black = !(dot(refl, n) > 0.0f);                       // wgsl:277-279
+            nd = normalize_w<true>(refl);
+        } else {                                                  // dielectric wgsl:102-135
+            att = mk(1.0f, 1.0f, 1.0f);
+            const float ratio = front ? 1.0f / mat.x : mat.x;
+            const v3 u = normalize_w<true>(d);
+            const float cos_t = fminf(dot(neg(u), n), 1.0f);
+            const float sin_t = sqrtf(fmaf(-cos_t, cos_t, 1.0f));
+            const bool cannot = ratio * sin_t > 1.0f;
+            const bool refl = cannot || reflectance(cos_t, ratio) > r_sb;
+            nd = normalize_w<true>(refl ? reflect(u, n) : refract(u, n, ratio));
+        }
+    }
+}
+
+// normalize(d).y of the sky (wgsl:293-296) and its colour times cf
+__device__ __forceinline__ v3 sky_w(v3 cf, v3 d) {
+    const float dd = dot(d, d);
+    float uy;
+    if (__ballot(__float_as_uint(dd) - kBits2m20 >= kBits2p40 - kBits2m20) == 0ull) {
+        const float len = sqrt_core(dd);
+        uy = div_core(d.y, len, rcp_refined(len));
+    } else {
+        uy = d.y / sqrtf(dd);
+    }
+    const float a = 0.5f * (uy + 1.0f);
+    const float om = 1.0f - a;
+    return mul(cf, mk(fmaf(a, 0.5f, om), fmaf(a, 0x1.666666p-1f, om), fmaf(a, 1.0f, om)));
+}
+
+// One sample of kSinglePix pixels per lane (get_ray + ray_color at depth <= 1).  seed[s] =
+// 1 + n + B (wgsl:353) of pixel s; kUniRs: every live pixel holds the hinted count, and the
+// scatter's random numbers come from p.rs.  Tiles: blk[s] = the tile's candidate block,
+// ncand[s] its count (kCandNone: the full list; 0 for a tile past the image edge).
+template <bool kUniRs>
+__device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& cam,
+                                              const TileCoord (&tc)[kSinglePix],
+                                              const uint32_t (&hxy)[kSinglePix],
+                                              const uint32_t (&seed)[kSinglePix],
+                                              const float4* const (&blk)[kSinglePix],
+                                              const uint32_t (&ncand)[kSinglePix],
+                                              const bool (&live)[kSinglePix],
+                                              v3 (&col)[kSinglePix]) {
+    constexpr uint32_t S = kSinglePix;
+    constexpr int K = RT_LIST_CHUNK;
+    v3 o[S], d[S];
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s)                              // wgsl:311, 305-325
+        get_ray<true>(cam, tc[s].x, tc[s].y, hxy[s], seed[s] * 25u + p.seed_b, o[s], d[s]);
+    v3 cf[S], dsky[S];
+    bool black[S];
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s) {
+        cf[s] = mk(1.0f, 1.0f, 1.0f);
+        dsky[s] = d[s];
+        black[s] = false;
+    }
+    if (p.depth != 0u) {                                          // wgsl:264
+        // sphere_list_hit over each tile's list, the tiles' chunks interleaved
+        float tmax[S], a[S], ya[S];
+        int idx[S];
+        bool joint = true;
+        uint32_t m = 0;
+#pragma unroll
+        for (uint32_t s = 0; s < S; ++s) {
+            tmax[s] = 0x1.05ed2ep+118f;                           // 3.4e35 (wgsl:266)
+            idx[s] = -1;
+            a[s] = dot(d[s], d[s]);
+            ya[s] = rcp_refined(a[s]);
+            joint = joint && ncand[s] != kCandNone;
+            m = max(m, ncand[s]);
+        }
+        if (joint) {
+            for (uint32_t i = 0; i < m; i += K) {
+                float hh[S][K], dd[S][K];
+                int mx = (int)0x80000000;
+#pragma unroll
+                for (uint32_t s = 0; s < S; ++s)
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const float4 g = load_rec<true>(blk[s] + kCandRecOff, i + k);
+                        dd[s][k] = discriminant(g, o[s], d[s], a[s], hh[s][k]);
+                        mx = max(mx, __float_as_int(dd[s][k]));
+                    }
+                if (__builtin_expect(mx > (int)0xFF800000, 0)) {
+#pragma unroll
+                    for (uint32_t s = 0; s < S; ++s)
+#pragma unroll
+                        for (int k = 0; k < K; ++k)
+                            if (i + k < ncand[s])
+                                consider_fast(dd[s][k], hh[s][k], a[s], ya[s], i + k, tmax[s],
+                                              idx[s]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (uint32_t s = 0; s < S; ++s) {
+                const bool listed = ncand[s] != kCandNone;
+                const Hit h = scan_exhaustive<K, true, true>(
+                    listed ? blk[s] + kCandRecOff : p.geom, listed ? ncand[s] : p.count, o[s],
+                    d[s]);
+                idx[s] = h.idx;
+                tmax[s] = h.t;
+            }
+        }
+        // hit records and the scatter (wgsl:205-218, 268-286)
+        bool hit[S];
+        bool any = false;
+#pragma unroll
+        for (uint32_t s = 0; s < S; ++s) {
+            hit[s] = live[s] && idx[s] >= 0;
+            any = any || hit[s];
+        }
+        if (__ballot(any) != 0ull) {
+            float4 pr[S], mat[S];
+#pragma unroll
+            for (uint32_t s = 0; s < S; ++s) {
+                const float4* hs = ncand[s] != kCandNone ? blk[s] + kCandSphOff : p.sph;
+                const uint32_t j = hit[s] ? (uint32_t)idx[s] : 0u;
+                pr[s] = hs[2u * j];
+                mat[s] = hs[2u * j + 1u];
+            }
+#pragma unroll
+            for (uint32_t s = 0; s < S; ++s) {
+                float r_sb;
+                v3 ruv;
+                if (kUniRs) {
+                    r_sb = p.rs.x;
+                    ruv = mk(p.rs.y, p.rs.z, p.rs.w);
+                } else {
+                    const uint32_t sb = hash(seed[s] + 1u);       // wgsl:268, 355 (i = 0)
+                    r_sb = rf(sb);
+                    ruv = random_unit_vector(r_sb, sb);
+                }
+                v3 nd, att;
+                bool blk_s;
+                shade_hit(pr[s], mat[s], tmax[s], o[s], d[s], r_sb, ruv, hit[s], nd, att,
+                          blk_s);
+                if (hit[s]) {                                     // wgsl:285-286
+                    cf[s] = att;
+                    dsky[s] = nd;
+                    black[s] = blk_s;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s) {
+        const v3 c = sky_w(cf[s], dsky[s]);                       // wgsl:293-296
+        col[s] = black[s] ? mk(0.0f, 0.0f, 0.0f) : c;             // wgsl:277-279
+    }
+}
+
+template <int kPix>
+__global__ __launch_bounds__(256, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
+    const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
+    const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
+    const SingleParams p) {
+    static_assert(kPix == (int)kSinglePix, "one instance");
+    constexpr uint32_t S = kSinglePix;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t tiles_x = (a_width + 7u) >> 3;
+    const uint32_t tx0 = (blockIdx.x * 4u + wave) * S;
+    const uint32_t lband = blockIdx.y;
+    const uint32_t band_first = a_bands & 0xFFFFu, band_step = (a_bands >> 16) & 0x7FFFu;
+    TileCoord tc[S];
+    uint32_t ncand[S], hxy[S];
+    const float4* blk[S];
+    float4 acc[S];
+    const uint32_t hy = a_hx[p.hy_off + min(band_first * RT_STRIPE_ROWS +
+                                                lband * band_step * RT_STRIPE_ROWS +
+                                                (lane >> 3),
+                                            a_height - 1u)];
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s) {
+        const uint32_t tx = tx0 + s;
+        const bool in = tx < tiles_x;
+        const uint32_t tile = lband * tiles_x + (in ? tx : tx0);
+        tc[s] = tile_coord(a_width, a_height, band_first, band_step, tx, lband, lane);
+        blk[s] = a_cand + (size_t)tile * kCandStride;
+        ncand[s] = in ? load_cnt(a_cand, tile) : 0u;
+        hxy[s] = a_hx[min(tc[s].x, a_width - 1u)] ^ hy;           // wgsl:309-310
+    }
+    // (issued after the seed-table loads: vmcnt waits in issue order, and the camera rays
+    // need the seeds long before the accumulation needs these)
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s) acc[s] = a_in[tc[s].valid ? tc[s].idx : 0];   // wgsl:339
+    if (p.defocus_angle > 0.0f) {                                 // (disk_unit's table)
+        if (threadIdx.x < 8u) {
+            double v = 0.0;
+#pragma unroll
+            for (uint32_t k = 0; k < 8u; ++k)
+                if (threadIdx.x == k) v = p.disk_rcp[k];
+            s_disk_rcp[threadIdx.x] = v;
+        }
+        __syncthreads();
+    }
+    if (tx0 >= tiles_x) return;
+
+    Cam cam;
+    cam.center = mk(p.center[0], p.center[1], p.center[2]);
+    cam.vul = mk(p.vul[0], p.vul[1], p.vul[2]);
+    cam.pdu = mk(p.pdu[0], p.pdu[1], p.pdu[2]);
+    cam.pdv = mk(p.pdv[0], p.pdv[1], p.pdv[2]);
+    cam.ddu = mk(p.ddu[0], p.ddu[1], p.ddu[2]);
+    cam.ddv = mk(p.ddv[0], p.ddv[1], p.ddv[2]);
+    cam.defocus_angle = p.defocus_angle;
+    const uint32_t spp = p.spp;                                   // wgsl:343
+
+    v3 c[S];
+    uint32_t n[S];
+    bool pending[S];
+    bool any_pending = true;
+    if (p.hinted) {
+        // Every pixel is expected to hold n_hint (the host's count bookkeeping): trace with
+        // it while the accumulator loads are in flight, then verify.
+        const uint32_t ng = p.n_hint;
+        v3 col[S];
+        if (ng < spp) {                                           // wgsl:352
+            uint32_t seed[S];
+            bool live[S];
+#pragma unroll
+            for (uint32_t s = 0; s < S; ++s) {
+                seed[s] = 1u + ng + p.seed_b;                     // wgsl:353
+                live[s] = tc[s].valid;
+            }
+            single_sample<true>(p, cam, tc, hxy, seed, blk, ncand, live, col);
+        }
+        any_pending = false;
+#pragma unroll
+        for (uint32_t s = 0; s < S; ++s) {
+            c[s] = p.reset ? mk(0.0f, 0.0f, 0.0f) : mk(acc[s].x, acc[s].y, acc[s].z);
+            n[s] = p.reset ? 0u : f2u(acc[s].w);                  // wgsl:339-350
+            pending[s] = tc[s].valid && n[s] != ng;               // a foreign count
+            any_pending = any_pending || pending[s];
+            if (ng < spp) {                                       // wgsl:352-357
+                const v3 num = sub(col[s], c[s]);
+                if (RT_SINGLE_ACC_F64 && ng < (1u << 24) &&
+                    __ballot(tc[s].valid && !acc_f64_ok(num)) == 0ull) {
+                    c[s] = acc_f64(c[s], num, p.rcp_hint);
+                } else {
+                    const float k = (float)(ng + 1u);             // wgsl:356
+                    c[s] = mk(c[s].x + num.x / k, c[s].y + num.y / k, c[s].z + num.z / k);
+                }
+                n[s] = ng + 1u;
+            }
+        }
+    } else {
+#pragma unroll
+        for (uint32_t s = 0; s < S; ++s) pending[s] = tc[s].valid;
+    }
+    if (__ballot(any_pending) != 0ull) {
+        // pixels whose count is not the hinted one (or no hint): traced with their own
+        // count and per-pixel random numbers
+        uint32_t seed[S];
+        bool live[S];
+        v3 col[S];
+#pragma unroll
+        for (uint32_t s = 0; s < S; ++s) {
+            if (pending[s]) {
+                c[s] = p.reset ? mk(0.0f, 0.0f, 0.0f) : mk(acc[s].x, acc[s].y, acc[s].z);
+                n[s] = p.reset ? 0u : f2u(acc[s].w);
+            }
+            live[s] = pending[s] && n[s] < spp;                   // wgsl:352
+            seed[s] = 1u + n[s] + p.seed_b;                       // wgsl:353
+        }
+        single_sample<false>(p, cam, tc, hxy, seed, blk, ncand, live, col);
+#pragma unroll
+        for (uint32_t s = 0; s < S; ++s)
+            if (live[s]) {                                        // wgsl:356-357
+                const float k = (float)(n[s] + 1u);
+                c[s] = mk(c[s].x + (col[s].x - c[s].x) / k, c[s].y + (col[s].y - c[s].y) / k,
+                          c[s].z + (col[s].z - c[s].z) / k);
+                n[s] += 1u;
+            }
+    }
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s)
+        if (tc[s].valid)                                          // wgsl:362-363
+            p.out[tc[s].idx] = make_float4(c[s].x, c[s].y, c[s].z, (float)n[s]);
+}
+
 // ---- Bounce paths with workgroup-wide compaction (kTraceBounce) -----------------------
 //
 // rt_update_frames with bounce rays (max_depth >= 2), several frames per launch.  One
@@ -1904,8 +2256,46 @@ static void launch_bounce(const TraceParams& p, hipStream_t stream) {
         hipLaunchKernelGGL(rt_bounce_kernel<kBounceWave>, grid, dim3(64), lds, stream, p);
 }
 
+// Four waves of kSinglePix tiles each per workgroup along a stripe band.
+static void launch_single(const TraceParams& p, hipStream_t stream) {
+    const uint32_t tiles_x = (p.width + 7u) >> 3;
+    const uint32_t per = 4u * kSinglePix;
+    const dim3 grid((tiles_x + per - 1u) / per, p.local_bands);
+    if (grid.x == 0 || grid.y == 0) return;
+    SingleParams q;
+    std::memset(&q, 0, sizeof(q));
+    q.out = p.out;
+    q.geom = p.geom;
+    q.sph = p.sph;
+    q.count = p.count;
+    q.depth = p.depth;
+    q.spp = p.spp;
+    q.reset = p.reset_first;
+    q.hinted = p.hint_frames != 0u;
+    q.n_hint = p.hint_n[0];
+    q.seed_b = p.seed_b[0];
+    q.hy_off = (uint32_t)(p.hy - p.hx);
+    q.rcp_hint = p.hint_rcp[0];
+    q.rs = p.hint_rs[0];
+    for (int k = 0; k < 8; ++k) q.disk_rcp[k] = p.disk_rcp[k];
+    for (int i = 0; i < 3; ++i) {
+        q.center[i] = p.center[i];
+        q.vul[i] = p.vul[i];
+        q.pdu[i] = p.pdu[i];
+        q.pdv[i] = p.pdv[i];
+        q.ddu[i] = p.ddu[i];
+        q.ddv[i] = p.ddv[i];
+    }
+    q.defocus_angle = p.defocus_angle;
+    hipLaunchKernelGGL(rt_single_kernel<(int)kSinglePix>, grid, dim3(256), 0, stream, p.cand,
+                       p.hx, p.in, p.width, p.height, pack_bands(p.band_first, p.band_step, false),
+                       q);
+}
+
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
-    if (kernel == kTraceCulled)
+    if (kernel == kTraceSingle)
+        launch_single(p, stream);
+    else if (kernel == kTraceCulled)
         launch_trace_as<kTraceCulled>(p, (size_t)p.lds_records * sizeof(float4), stream);
     else if (kernel == kTraceList)
         launch_trace_as<kTraceList>(p, 0, stream);
@@ -1967,6 +2357,9 @@ hipError_t launch_present(const float4* in, uchar4* out, uint64_t texels,
 }
 
 const char* trace_kernel_name() { return "rt_trace_kernel"; }
+const char* single_kernel_name() {
+    return kSinglePix == 1 ? "rt_single_kernel<1>" : "rt_single_kernel<2>";
+}
 
 }  // namespace rtk
 

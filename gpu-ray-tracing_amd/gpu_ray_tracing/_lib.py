@@ -119,6 +119,7 @@ _SIGS = {
     "rt_set_tile_order": (ctypes.c_int, [P, ctypes.c_int]),
     "rt_last_launch_info": (ctypes.c_int, [P, P]),
     "rt_set_path_compaction": (ctypes.c_int, [P, ctypes.c_int]),
+    "rt_set_single_kernel": (ctypes.c_int, [P, ctypes.c_int]),
 }
 
 

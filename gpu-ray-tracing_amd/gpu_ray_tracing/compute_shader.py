@@ -86,6 +86,11 @@ class ComputeShaderPipeline:
         _lib.call("rt_set_path_compaction", self._ctx,
                   {"auto": 0, "per_wave": 1, "compact": 2, "pair": 3}[mode])
 
+    def set_single_kernel(self, mode: str) -> None:
+        """rt_set_single_kernel: "auto" (one-frame launches of the camera-ray-only case run
+        rt_single_kernel) or "off" (the general rt_trace_kernel<2>); identical pixels."""
+        _lib.call("rt_set_single_kernel", self._ctx, {"auto": 0, "off": 1}[mode])
+
     def frames_per_launch(self, camera) -> int:
         """rt_get_frames_per_launch: frames update_frames fuses per launch for `camera`."""
         out = _lib.U32(0)

@@ -175,8 +175,11 @@ RT_API const char* rt_last_error(void);
 #define RT_KERNEL_BOUNCE 5
 #define RT_KERNEL_BOUNCE_COMPACT 6
 #define RT_KERNEL_BOUNCE_PAIR 7
-/* The instance's name as rocprofv3 lists it ("rt_trace_kernel<k>", "rt_bounce_kernel<m>"),
- * "rt_trace_kernel" for an unknown id. */
+/* one `update` dispatch (one frame per launch) of the camera-ray-only case: several
+ * adjacent tiles per wave, parameters in one compact block (rt_set_single_kernel) */
+#define RT_KERNEL_SINGLE 8
+/* The instance's name as rocprofv3 lists it ("rt_trace_kernel<k>", "rt_bounce_kernel<m>",
+ * "rt_single_kernel<p>"), "rt_trace_kernel" for an unknown id. */
 RT_API const char* rt_kernel_name(int which);
 /* What the last rt_update / rt_render / rt_render_stripes / rt_update_frames call on this
  * context launched: trace launches, frames traced, the most frames one launch carried and
@@ -281,6 +284,12 @@ RT_API rt_status rt_set_tile_order(rt_ctx* ctx, int mode);
 #define RT_PATHS_COMPACT 2
 #define RT_PATHS_PAIR 3
 RT_API rt_status rt_set_path_compaction(rt_ctx* ctx, int mode);
+/* One-frame launches of the camera-ray-only case (rt_update, rt_render / rt_update_frames
+ * launches carrying one frame): AUTO (default) runs RT_KERNEL_SINGLE, OFF the general
+ * RT_KERNEL_LIST instance.  Pixel results are identical. */
+#define RT_SINGLE_AUTO 0
+#define RT_SINGLE_OFF 1
+RT_API rt_status rt_set_single_kernel(rt_ctx* ctx, int mode);
 /* The frames per launch rt_update_frames would use for `camera` (its max_depth) now. */
 RT_API rt_status rt_get_frames_per_launch(const rt_ctx* ctx, const rt_scene_camera* camera,
                                           uint32_t* out_frames);

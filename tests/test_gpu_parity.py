@@ -11,12 +11,15 @@ from conftest import bits_equal, load_golden
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["culled", "exhaustive"])
+@pytest.fixture(scope="module", params=["culled", "culled_general", "exhaustive"])
 def pipe(rt, request):
-    """Every parity test runs against both sphere-scan strategies."""
+    """Every parity test runs against both sphere-scan strategies, and the culled one with
+    and without the dedicated one-frame kernel (rt_set_single_kernel)."""
     assert torch.cuda.is_available(), "GPU tests need a HIP device"
     p = rt.ComputeShaderPipeline(0)
-    p.set_scan_mode(request.param)
+    p.set_scan_mode(request.param.split("_")[0])
+    if request.param == "culled_general":
+        p.set_single_kernel("off")
     yield p
     p.close()
 
@@ -148,8 +151,9 @@ def test_bench_k4_launches_match_golden(rt, pairs):
         p.close()
 
 
+@pytest.mark.parametrize("single", ["auto", "off"])
 @pytest.mark.parametrize("cfg", ["k2", "k3"])
-def test_bench_dispatch_chain_matches_fixture(rt, cfg):
+def test_bench_dispatch_chain_matches_fixture(rt, cfg, single):
     """bench.py --config K2/K3's timed structure: one update launch per frame
     (rt_set_frames_per_launch(1)), 5 + 20 frames from a reset at 1920x1080 (the driver's
     --warmup 5 --steps 20), checked against the oracle's sampled pixels
@@ -159,6 +163,7 @@ def test_bench_dispatch_chain_matches_fixture(rt, cfg):
     cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
     p = rt.ComputeShaderPipeline(0)
     p.set_frames_per_launch(1)
+    p.set_single_kernel(single)
     try:
         a, b = p.new_image(w, h), p.new_image(w, h)
         n0 = p.update_frames(a, b, w, h, cam, sc, g["seeds"][:5])
@@ -168,7 +173,8 @@ def test_bench_dispatch_chain_matches_fixture(rt, cfg):
                                  g["seeds"][5:25])
         info = p.last_launch_info()
         assert info["launches"] == 20 and info["max_frames_per_launch"] == 1
-        assert info["kernel_name"] == "rt_trace_kernel<2>"
+        assert info["kernel_name"] == ("rt_trace_kernel<2>" if single == "off"
+                                       else "rt_single_kernel<2>")
         img = host(b if newest == 1 else a)
         k = list(g["frame_counts"]).index(25)
         assert_same(img[g["py"], g["px"]], g["pixels"][k])

@@ -21,7 +21,7 @@ def header_functions():
 
 def test_library_exports_every_declared_symbol(rt):
     declared = header_functions()
-    assert len(declared) == 31
+    assert len(declared) == 32
     nm = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True,
                         text=True, check=True).stdout
     exported = set(re.findall(r" T (rt_\w+)$", nm, flags=re.M))
@@ -152,6 +152,8 @@ def test_argument_errors_without_device(rt):
     assert [L.rt_kernel_name(k).decode() for k in range(8)] == [
         f"rt_trace_kernel<{k}>" for k in range(5)] + [f"rt_bounce_kernel<{m}>" for m in range(3)]
     assert L.rt_set_path_compaction(None, 0) == 6
+    assert L.rt_set_single_kernel(None, 0) == 6
+    assert L.rt_kernel_name(8).decode() == "rt_single_kernel<2>"
     assert L.rt_kernel_name(99).decode() == "rt_trace_kernel"
 
 

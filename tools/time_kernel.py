@@ -16,6 +16,8 @@ def main(cfg="k3", iters=40):
     pipe.set_scan_mode(os.environ.get('RT_SCAN_MODE', 'culled'))
     if hasattr(pipe, "set_tile_order") and hasattr(rt._lib.lib(), "rt_set_tile_order"):
         pipe.set_tile_order(os.environ.get("RT_TILE_ORDER", "auto"))
+    if hasattr(rt._lib.lib(), "rt_set_single_kernel"):
+        pipe.set_single_kernel(os.environ.get("RT_SINGLE", "auto"))
     a, b = pipe.new_image(w, h), pipe.new_image(w, h)
     pipe.update(a, b, w, h, cam, sc); torch.cuda.synchronize()
     ok = hashlib.sha256(b.cpu().numpy().tobytes()).hexdigest() == str(g["sha256"]) if "sha256" in g else None
