@@ -1249,11 +1249,15 @@ struct SingleParams {
 #define RT_SINGLE_PIX 2
 #endif
 constexpr uint32_t kSinglePix = RT_SINGLE_PIX;
+static_assert(kSinglePix >= 1 && kSinglePix <= 4, "1 to 4 tiles per wave");
 #ifndef RT_SINGLE_MIN_WAVES
 #define RT_SINGLE_MIN_WAVES 5
 #endif
 #ifndef RT_SINGLE_ACC_F64
 #define RT_SINGLE_ACC_F64 1
+#endif
+#ifndef RT_SINGLE_WT
+#define RT_SINGLE_WT 1
 #endif
 
 // Shading of a camera ray's hit at depth 1 (ray_color's loop body at i = 0, wgsl:266-286):
@@ -1445,6 +1449,7 @@ __global__ __launch_bounds__(256, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
     const SingleParams p) {
     static_assert(kPix == (int)kSinglePix, "one instance");
     constexpr uint32_t S = kSinglePix;
+    WAVE_TRACE(0);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t tiles_x = (a_width + 7u) >> 3;
@@ -1562,10 +1567,28 @@ __global__ __launch_bounds__(256, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
                 n[s] += 1u;
             }
     }
+#if RT_SINGLE_WT
+    // write-through (sc1) stores: the lines leave the XCD's L2 as they are written, so the
+    // launch ends with no dirty image lines to write back at the kernel boundary
+    float4* band = p.out + (size_t)lband * RT_STRIPE_ROWS * a_width;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        band, 0, (int)(RT_STRIPE_ROWS * 16u * a_width), 0x00020000);
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s)
+        if (tc[s].valid) {                                        // wgsl:362-363
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 v = {__float_as_uint(c[s].x), __float_as_uint(c[s].y),
+                             __float_as_uint(c[s].z), __float_as_uint((float)n[s])};
+            __builtin_amdgcn_raw_buffer_store_b128(
+                v, rsrc, (int)(((lane >> 3) * a_width + tc[s].x) * 16u), 0, 16);
+        }
+#else
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s)
         if (tc[s].valid)                                          // wgsl:362-363
             p.out[tc[s].idx] = make_float4(c[s].x, c[s].y, c[s].z, (float)n[s]);
+#endif
+    WAVE_TRACE(1);
 }
 
 // ---- Bounce paths with workgroup-wide compaction (kTraceBounce) -----------------------
@@ -2358,7 +2381,9 @@ hipError_t launch_present(const float4* in, uchar4* out, uint64_t texels,
 
 const char* trace_kernel_name() { return "rt_trace_kernel"; }
 const char* single_kernel_name() {
-    return kSinglePix == 1 ? "rt_single_kernel<1>" : "rt_single_kernel<2>";
+    static const char* const names[] = {"rt_single_kernel<1>", "rt_single_kernel<2>",
+                                        "rt_single_kernel<3>", "rt_single_kernel<4>"};
+    return names[kSinglePix - 1];
 }
 
 }  // namespace rtk
