@@ -180,10 +180,13 @@ int trace_kernel_for(const rt_ctx* ctx, const rtk::TraceParams& p) {
 // One-frame launches of the camera-ray-only instance run rt_single_kernel (rt_kernels.hip)
 // unless rt_set_single_kernel(OFF).
 int single_or(const rt_ctx* ctx, const rtk::TraceParams& p, int kernel) {
-    if (kernel == rtk::kTraceList && p.frames == 1u && ctx->single_kernel == RT_SINGLE_AUTO &&
-        p.cand)
-        return rtk::kTraceSingle;
-    return kernel;
+    if (kernel != rtk::kTraceList || p.frames != 1u || !p.cand ||
+        ctx->single_kernel == RT_SINGLE_OFF)
+        return kernel;
+    if (ctx->single_kernel == RT_SINGLE_PAIR) return rtk::kTraceSingle;
+    if (ctx->single_kernel == RT_SINGLE_ONE) return rtk::kTraceSingleOne;
+    const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
+    return tiles <= rtk::kSingleOneMaxTiles ? rtk::kTraceSingleOne : rtk::kTraceSingle;
 }
 
 // Frames per rt_update_frames launch (see rt_update_frames).  Only the camera-ray-only
@@ -808,7 +811,8 @@ const char* rt_kernel_name(int which) {
                                         "rt_trace_kernel<2>",      "rt_trace_kernel<3>",
                                         "rt_trace_kernel<4>",      "rt_bounce_kernel<0>",
                                         "rt_bounce_kernel<1>",     "rt_bounce_kernel<2>",
-                                        rtk::single_kernel_name()};
+                                        rtk::single_kernel_name(0),
+                                        rtk::single_kernel_name(1)};
     if (which >= 0 && which < (int)(sizeof(names) / sizeof(names[0]))) return names[which];
     return rtk::trace_kernel_name();
 }
@@ -886,7 +890,8 @@ rt_status rt_set_path_compaction(rt_ctx* ctx, int mode) {
 
 rt_status rt_set_single_kernel(rt_ctx* ctx, int mode) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
-    if (mode != RT_SINGLE_AUTO && mode != RT_SINGLE_OFF)
+    if (mode != RT_SINGLE_AUTO && mode != RT_SINGLE_OFF && mode != RT_SINGLE_PAIR &&
+        mode != RT_SINGLE_ONE)
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown single-kernel mode");
     ctx->single_kernel = mode;
     return RT_OK;

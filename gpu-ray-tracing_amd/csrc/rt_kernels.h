@@ -131,7 +131,17 @@ constexpr uint32_t kBounceWaves = 4;   // tiles (waves) per bounce workgroup
 // One frame per launch of the camera-ray-only case (rt_update / a one-frame rt_update_frames
 // launch with the kTraceList conditions): rt_kernels.hip, rt_single_kernel.
 constexpr int kTraceSingle = 8;
-static_assert(kTraceSingle == RT_KERNEL_SINGLE, "instance id is the ABI's RT_KERNEL_SINGLE");
+// the same with one tile per wave (small per-rank shares)
+constexpr int kTraceSingleOne = 9;
+static_assert(kTraceSingle == RT_KERNEL_SINGLE && kTraceSingleOne == RT_KERNEL_SINGLE_ONE,
+              "instance ids are the ABI's RT_KERNEL_SINGLE*");
+// Tiles per launch below which one-frame launches use one tile per wave (kTraceSingleOne).
+// (K3 per-update rank shares, profiles/r02_rank_sim_k3_single_*.jsonl: two tiles per wave
+// 24.1 / 14.4 / 9.8 / 8.6 us at 1 / 2 / 4 / 8 ranks, one tile 26.6 / 15.0 / 9.6 / 7.1)
+#ifndef RT_SINGLE_ONE_MAX_TILES
+#define RT_SINGLE_ONE_MAX_TILES 9000
+#endif
+constexpr uint64_t kSingleOneMaxTiles = RT_SINGLE_ONE_MAX_TILES;
 constexpr bool is_group_kernel(int k) { return k == kTraceListPair || k == kTraceListQuad; }
 constexpr bool is_list_kernel(int k) { return k == kTraceList || is_group_kernel(k); }
 // Waves (tiles) per workgroup of the one-wave-per-tile instances (kTraceExhaustive,
@@ -169,8 +179,8 @@ hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t wid
 hipError_t launch_present(const float4* in, uchar4* out, uint64_t texels,
                           const float* srgb_t, hipStream_t stream);
 const char* trace_kernel_name();
-// "rt_single_kernel<p>" with p = the pixels per lane it was built with
-const char* single_kernel_name();
+// "rt_single_kernel<p>": p = pix tiles per wave (0: kTraceSingle's)
+const char* single_kernel_name(uint32_t pix);
 // tile_order for launch_trace: the local tiles by decreasing recorded cost (quantised
 // log2 of tile_cost), so the slowest tiles start first and the cheap ones fill the tail.
 hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, uint32_t tiles,

@@ -1245,6 +1245,8 @@ struct SingleParams {
     float defocus_angle;
 };
 
+// Tiles per wave of the two instances: kTraceSingle (whole-image launches) and
+// kTraceSingleOne (small per-rank shares, where more, shorter waves fill the chip).
 #ifndef RT_SINGLE_PIX
 #define RT_SINGLE_PIX 2
 #endif
@@ -1255,6 +1257,35 @@ static_assert(kSinglePix >= 1 && kSinglePix <= 4, "1 to 4 tiles per wave");
 #endif
 #ifndef RT_SINGLE_ACC_F64
 #define RT_SINGLE_ACC_F64 1
+#endif
+// Knock-out builds of the one-frame kernel (cost attribution only, never the product):
+// bit 1 no accumulator load, 2 no sphere scan, 4 no random camera ray, 8 no hit shading,
+// 16 no image store.
+#ifndef RT_SKO
+#define RT_SKO 0
+#endif
+// waves per workgroup of the one-frame kernel
+#ifndef RT_SINGLE_WG
+#define RT_SINGLE_WG 4
+#endif
+constexpr uint32_t kSingleWg = RT_SINGLE_WG;
+// sphere scan of the one-frame kernel: 0 = both tiles' lists in one loop, RT_LIST_CHUNK
+// records of each per step; k > 0 = each tile's list on its own, k records per step
+#ifndef RT_SINGLE_SCAN
+#define RT_SINGLE_SCAN 0
+#endif
+// skip the hit shading of a tile none of whose rays hit
+#ifndef RT_SINGLE_GATE
+#define RT_SINGLE_GATE 0
+#endif
+// The tiles' 1-KB candidate blocks are loaded whole at wave start (one 16-B load per lane,
+// beside the seed and accumulator loads) and kept in LDS: the scan records and the hit
+// records are then LDS reads instead of dependent L2/HBM round trips.  It shortens a
+// wave's memory chain (8-rank K3 share, one tile per wave: 7.10 -> 6.64 us per update) but
+// costs a whole launch more than it saves (K3 24.9 -> 25.8 us, K2 18.3 -> 19.9;
+// profiles/r02_ab_single_lds_k*.log): 1 = the one-tile instance only, 2 = both, 0 = none.
+#ifndef RT_SINGLE_LDS
+#define RT_SINGLE_LDS 1
 #endif
 #ifndef RT_SINGLE_WT
 #define RT_SINGLE_WT 1
@@ -1323,21 +1354,36 @@ __device__ __forceinline__ v3 sky_w(v3 cf, v3 d) {
 // 1 + n + B (wgsl:353) of pixel s; kUniRs: every live pixel holds the hinted count, and the
 // scatter's random numbers come from p.rs.  Tiles: blk[s] = the tile's candidate block,
 // ncand[s] its count (kCandNone: the full list; 0 for a tile past the image edge).
-template <bool kUniRs>
+template <uint32_t S>
+constexpr bool kSingleLds = RT_SINGLE_LDS == 2 || (RT_SINGLE_LDS == 1 && S == 1);
+template <uint32_t S, bool kUniRs>
 __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& cam,
-                                              const TileCoord (&tc)[kSinglePix],
-                                              const uint32_t (&hxy)[kSinglePix],
-                                              const uint32_t (&seed)[kSinglePix],
-                                              const float4* const (&blk)[kSinglePix],
-                                              const uint32_t (&ncand)[kSinglePix],
-                                              const bool (&live)[kSinglePix],
-                                              v3 (&col)[kSinglePix]) {
-    constexpr uint32_t S = kSinglePix;
+                                              const TileCoord (&tc)[S],
+                                              const uint32_t (&hxy)[S],
+                                              const uint32_t (&seed)[S],
+                                              const float4* const (&blk)[S],
+                                              const uint32_t (&ncand)[S],
+                                              const bool (&live)[S],
+                                              const float4 (&bv)[S], float4* lblk,
+                                              v3 (&col)[S]) {
     constexpr int K = RT_LIST_CHUNK;
     v3 o[S], d[S];
 #pragma unroll
-    for (uint32_t s = 0; s < S; ++s)                              // wgsl:311, 305-325
+    for (uint32_t s = 0; s < S; ++s) {                            // wgsl:311, 305-325
+#if RT_SKO & 4
+        o[s] = cam.center;
+        d[s] = sub(fmas((float)tc[s].y + (float)(hxy[s] & 1u), cam.pdv,
+                        fmas((float)tc[s].x, cam.pdu, cam.vul)), o[s]);
+#else
         get_ray<true>(cam, tc[s].x, tc[s].y, hxy[s], seed[s] * 25u + p.seed_b, o[s], d[s]);
+#endif
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    if (kSingleLds<S>) {
+        // (this wave's own LDS slots: written and read by this wave only, in order)
+#pragma unroll
+        for (uint32_t s = 0; s < S; ++s) lblk[s * kCandStride + lane] = bv[s];
+    }
     v3 cf[S], dsky[S];
     bool black[S];
 #pragma unroll
@@ -1346,7 +1392,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
         dsky[s] = d[s];
         black[s] = false;
     }
-    if (p.depth != 0u) {                                          // wgsl:264
+    if (p.depth != 0u && !(RT_SKO & 2)) {                         // wgsl:264
         // sphere_list_hit over each tile's list, the tiles' chunks interleaved
         float tmax[S], a[S], ya[S];
         int idx[S];
@@ -1361,7 +1407,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
             joint = joint && ncand[s] != kCandNone;
             m = max(m, ncand[s]);
         }
-        if (joint) {
+        if (RT_SINGLE_SCAN == 0 && joint) {
             for (uint32_t i = 0; i < m; i += K) {
                 float hh[S][K], dd[S][K];
                 int mx = (int)0x80000000;
@@ -1369,7 +1415,9 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                 for (uint32_t s = 0; s < S; ++s)
 #pragma unroll
                     for (int k = 0; k < K; ++k) {
-                        const float4 g = load_rec<true>(blk[s] + kCandRecOff, i + k);
+                        const float4 g =
+                            kSingleLds<S> ? lblk[s * kCandStride + kCandRecOff + i + k]
+                                          : load_rec<true>(blk[s] + kCandRecOff, i + k);
                         dd[s][k] = discriminant(g, o[s], d[s], a[s], hh[s][k]);
                         mx = max(mx, __float_as_int(dd[s][k]));
                     }
@@ -1387,7 +1435,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
                 const bool listed = ncand[s] != kCandNone;
-                const Hit h = scan_exhaustive<K, true, true>(
+                const Hit h = scan_exhaustive<(RT_SINGLE_SCAN == 0 ? K : RT_SINGLE_SCAN), true, true>(
                     listed ? blk[s] + kCandRecOff : p.geom, listed ? ncand[s] : p.count, o[s],
                     d[s]);
                 idx[s] = h.idx;
@@ -1402,17 +1450,27 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
             hit[s] = live[s] && idx[s] >= 0;
             any = any || hit[s];
         }
-        if (__ballot(any) != 0ull) {
+        if (RT_SKO & 8) {
+#pragma unroll
+            for (uint32_t s = 0; s < S; ++s)
+                if (hit[s]) cf[s] = mk(tmax[s], 0.5f, 0.5f);
+        } else if (__ballot(any) != 0ull) {
             float4 pr[S], mat[S];
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
-                const float4* hs = ncand[s] != kCandNone ? blk[s] + kCandSphOff : p.sph;
                 const uint32_t j = hit[s] ? (uint32_t)idx[s] : 0u;
-                pr[s] = hs[2u * j];
-                mat[s] = hs[2u * j + 1u];
+                if (kSingleLds<S> && ncand[s] != kCandNone) {
+                    pr[s] = lblk[s * kCandStride + kCandSphOff + 2u * j];
+                    mat[s] = lblk[s * kCandStride + kCandSphOff + 2u * j + 1u];
+                } else {
+                    const float4* hs = ncand[s] != kCandNone ? blk[s] + kCandSphOff : p.sph;
+                    pr[s] = hs[2u * j];
+                    mat[s] = hs[2u * j + 1u];
+                }
             }
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
+                if (RT_SINGLE_GATE && __ballot(hit[s]) == 0ull) continue;   // (sky tiles)
                 float r_sb;
                 v3 ruv;
                 if (kUniRs) {
@@ -1443,23 +1501,25 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
 }
 
 template <int kPix>
-__global__ __launch_bounds__(256, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
+__global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
     const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const SingleParams p) {
-    static_assert(kPix == (int)kSinglePix, "one instance");
-    constexpr uint32_t S = kSinglePix;
+    static_assert(kPix >= 1 && kPix <= 4, "1 to 4 tiles per wave");
+    constexpr uint32_t S = kPix;
     WAVE_TRACE(0);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t tiles_x = (a_width + 7u) >> 3;
-    const uint32_t tx0 = (blockIdx.x * 4u + wave) * S;
+    const uint32_t tx0 = (blockIdx.x * kSingleWg + wave) * S;
     const uint32_t lband = blockIdx.y;
     const uint32_t band_first = a_bands & 0xFFFFu, band_step = (a_bands >> 16) & 0x7FFFu;
     TileCoord tc[S];
     uint32_t ncand[S], hxy[S];
     const float4* blk[S];
-    float4 acc[S];
+    float4 acc[S], bv[S];
+    __shared__ float4 s_blk[kSingleWg * kPix * kCandStride];
+    float4* lblk = s_blk + wave * S * kCandStride;
     const uint32_t hy = a_hx[p.hy_off + min(band_first * RT_STRIPE_ROWS +
                                                 lband * band_step * RT_STRIPE_ROWS +
                                                 (lane >> 3),
@@ -1475,9 +1535,15 @@ __global__ __launch_bounds__(256, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
         hxy[s] = a_hx[min(tc[s].x, a_width - 1u)] ^ hy;           // wgsl:309-310
     }
     // (issued after the seed-table loads: vmcnt waits in issue order, and the camera rays
-    // need the seeds long before the accumulation needs these)
+    // need the seeds long before the scan and the accumulation need these)
 #pragma unroll
-    for (uint32_t s = 0; s < S; ++s) acc[s] = a_in[tc[s].valid ? tc[s].idx : 0];   // wgsl:339
+    for (uint32_t s = 0; s < S; ++s)
+        bv[s] = (kSingleLds<S> && tx0 + s < tiles_x) ? blk[s][lane]
+                                                      : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s)
+        acc[s] = (RT_SKO & 1) ? make_float4(0.0f, 0.0f, 0.0f, (float)p.n_hint)
+                              : a_in[tc[s].valid ? tc[s].idx : 0];                // wgsl:339
     if (p.defocus_angle > 0.0f) {                                 // (disk_unit's table)
         if (threadIdx.x < 8u) {
             double v = 0.0;
@@ -1517,7 +1583,7 @@ __global__ __launch_bounds__(256, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
                 seed[s] = 1u + ng + p.seed_b;                     // wgsl:353
                 live[s] = tc[s].valid;
             }
-            single_sample<true>(p, cam, tc, hxy, seed, blk, ncand, live, col);
+            single_sample<S, true>(p, cam, tc, hxy, seed, blk, ncand, live, bv, lblk, col);
         }
         any_pending = false;
 #pragma unroll
@@ -1557,7 +1623,7 @@ __global__ __launch_bounds__(256, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
             live[s] = pending[s] && n[s] < spp;                   // wgsl:352
             seed[s] = 1u + n[s] + p.seed_b;                       // wgsl:353
         }
-        single_sample<false>(p, cam, tc, hxy, seed, blk, ncand, live, col);
+        single_sample<S, false>(p, cam, tc, hxy, seed, blk, ncand, live, bv, lblk, col);
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s)
             if (live[s]) {                                        // wgsl:356-357
@@ -1567,7 +1633,9 @@ __global__ __launch_bounds__(256, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
                 n[s] += 1u;
             }
     }
-#if RT_SINGLE_WT
+#if RT_SKO & 16
+    if (c[0].x == 12345.678f) p.out[0] = make_float4(c[1].x, c[1].y, c[1].z, (float)n[0]);
+#elif RT_SINGLE_WT
     // write-through (sc1) stores: the lines leave the XCD's L2 as they are written, so the
     // launch ends with no dirty image lines to write back at the kernel boundary
     float4* band = p.out + (size_t)lband * RT_STRIPE_ROWS * a_width;
@@ -2279,10 +2347,11 @@ static void launch_bounce(const TraceParams& p, hipStream_t stream) {
         hipLaunchKernelGGL(rt_bounce_kernel<kBounceWave>, grid, dim3(64), lds, stream, p);
 }
 
-// Four waves of kSinglePix tiles each per workgroup along a stripe band.
+// kSingleWg waves of kPix tiles each per workgroup along a stripe band.
+template <int kPix>
 static void launch_single(const TraceParams& p, hipStream_t stream) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
-    const uint32_t per = 4u * kSinglePix;
+    const uint32_t per = kSingleWg * kPix;
     const dim3 grid((tiles_x + per - 1u) / per, p.local_bands);
     if (grid.x == 0 || grid.y == 0) return;
     SingleParams q;
@@ -2310,14 +2379,16 @@ static void launch_single(const TraceParams& p, hipStream_t stream) {
         q.ddv[i] = p.ddv[i];
     }
     q.defocus_angle = p.defocus_angle;
-    hipLaunchKernelGGL(rt_single_kernel<(int)kSinglePix>, grid, dim3(256), 0, stream, p.cand,
+    hipLaunchKernelGGL(rt_single_kernel<kPix>, grid, dim3(64 * kSingleWg), 0, stream, p.cand,
                        p.hx, p.in, p.width, p.height, pack_bands(p.band_first, p.band_step, false),
                        q);
 }
 
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
     if (kernel == kTraceSingle)
-        launch_single(p, stream);
+        launch_single<(int)kSinglePix>(p, stream);
+    else if (kernel == kTraceSingleOne)
+        launch_single<1>(p, stream);
     else if (kernel == kTraceCulled)
         launch_trace_as<kTraceCulled>(p, (size_t)p.lds_records * sizeof(float4), stream);
     else if (kernel == kTraceList)
@@ -2380,10 +2451,10 @@ hipError_t launch_present(const float4* in, uchar4* out, uint64_t texels,
 }
 
 const char* trace_kernel_name() { return "rt_trace_kernel"; }
-const char* single_kernel_name() {
+const char* single_kernel_name(uint32_t pix) {
     static const char* const names[] = {"rt_single_kernel<1>", "rt_single_kernel<2>",
                                         "rt_single_kernel<3>", "rt_single_kernel<4>"};
-    return names[kSinglePix - 1];
+    return names[(pix ? pix : kSinglePix) - 1];
 }
 
 }  // namespace rtk

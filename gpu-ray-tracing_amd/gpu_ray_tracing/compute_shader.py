@@ -88,8 +88,10 @@ class ComputeShaderPipeline:
 
     def set_single_kernel(self, mode: str) -> None:
         """rt_set_single_kernel: "auto" (one-frame launches of the camera-ray-only case run
-        rt_single_kernel) or "off" (the general rt_trace_kernel<2>); identical pixels."""
-        _lib.call("rt_set_single_kernel", self._ctx, {"auto": 0, "off": 1}[mode])
+        rt_single_kernel: two tiles per wave, one for small launches), "pair", "one" (force
+        either) or "off" (the general rt_trace_kernel<2>); identical pixels."""
+        _lib.call("rt_set_single_kernel", self._ctx,
+                  {"auto": 0, "off": 1, "pair": 2, "one": 3}[mode])
 
     def frames_per_launch(self, camera) -> int:
         """rt_get_frames_per_launch: frames update_frames fuses per launch for `camera`."""

@@ -178,6 +178,8 @@ RT_API const char* rt_last_error(void);
 /* one `update` dispatch (one frame per launch) of the camera-ray-only case: several
  * adjacent tiles per wave, parameters in one compact block (rt_set_single_kernel) */
 #define RT_KERNEL_SINGLE 8
+/* the same with one tile per wave, for small per-rank shares */
+#define RT_KERNEL_SINGLE_ONE 9
 /* The instance's name as rocprofv3 lists it ("rt_trace_kernel<k>", "rt_bounce_kernel<m>",
  * "rt_single_kernel<p>"), "rt_trace_kernel" for an unknown id. */
 RT_API const char* rt_kernel_name(int which);
@@ -285,10 +287,13 @@ RT_API rt_status rt_set_tile_order(rt_ctx* ctx, int mode);
 #define RT_PATHS_PAIR 3
 RT_API rt_status rt_set_path_compaction(rt_ctx* ctx, int mode);
 /* One-frame launches of the camera-ray-only case (rt_update, rt_render / rt_update_frames
- * launches carrying one frame): AUTO (default) runs RT_KERNEL_SINGLE, OFF the general
+ * launches carrying one frame): AUTO (default) runs RT_KERNEL_SINGLE (two tiles per wave),
+ * or RT_KERNEL_SINGLE_ONE for small launches; PAIR / ONE force either; OFF runs the general
  * RT_KERNEL_LIST instance.  Pixel results are identical. */
 #define RT_SINGLE_AUTO 0
 #define RT_SINGLE_OFF 1
+#define RT_SINGLE_PAIR 2
+#define RT_SINGLE_ONE 3
 RT_API rt_status rt_set_single_kernel(rt_ctx* ctx, int mode);
 /* The frames per launch rt_update_frames would use for `camera` (its max_depth) now. */
 RT_API rt_status rt_get_frames_per_launch(const rt_ctx* ctx, const rt_scene_camera* camera,

@@ -11,15 +11,18 @@ from conftest import bits_equal, load_golden
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["culled", "culled_general", "exhaustive"])
+@pytest.fixture(scope="module", params=["culled", "culled_one", "culled_general", "exhaustive"])
 def pipe(rt, request):
     """Every parity test runs against both sphere-scan strategies, and the culled one with
-    and without the dedicated one-frame kernel (rt_set_single_kernel)."""
+    each one-frame kernel (rt_set_single_kernel: two tiles per wave, one, the general
+    instance)."""
     assert torch.cuda.is_available(), "GPU tests need a HIP device"
     p = rt.ComputeShaderPipeline(0)
     p.set_scan_mode(request.param.split("_")[0])
     if request.param == "culled_general":
         p.set_single_kernel("off")
+    elif request.param == "culled_one":
+        p.set_single_kernel("one")
     yield p
     p.close()
 
@@ -151,7 +154,7 @@ def test_bench_k4_launches_match_golden(rt, pairs):
         p.close()
 
 
-@pytest.mark.parametrize("single", ["auto", "off"])
+@pytest.mark.parametrize("single", ["auto", "one", "off"])
 @pytest.mark.parametrize("cfg", ["k2", "k3"])
 def test_bench_dispatch_chain_matches_fixture(rt, cfg, single):
     """bench.py --config K2/K3's timed structure: one update launch per frame
@@ -173,8 +176,8 @@ def test_bench_dispatch_chain_matches_fixture(rt, cfg, single):
                                  g["seeds"][5:25])
         info = p.last_launch_info()
         assert info["launches"] == 20 and info["max_frames_per_launch"] == 1
-        assert info["kernel_name"] == ("rt_trace_kernel<2>" if single == "off"
-                                       else "rt_single_kernel<2>")
+        assert info["kernel_name"] == {"off": "rt_trace_kernel<2>", "one": "rt_single_kernel<1>",
+                                       "auto": "rt_single_kernel<2>"}[single]
         img = host(b if newest == 1 else a)
         k = list(g["frame_counts"]).index(25)
         assert_same(img[g["py"], g["px"]], g["pixels"][k])

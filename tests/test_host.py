@@ -154,6 +154,7 @@ def test_argument_errors_without_device(rt):
     assert L.rt_set_path_compaction(None, 0) == 6
     assert L.rt_set_single_kernel(None, 0) == 6
     assert L.rt_kernel_name(8).decode() == "rt_single_kernel<2>"
+    assert L.rt_kernel_name(9).decode() == "rt_single_kernel<1>"
     assert L.rt_kernel_name(99).decode() == "rt_trace_kernel"
 
 

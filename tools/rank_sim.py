@@ -30,6 +30,8 @@ def main(cfg="K3", steps=50):
     # RT_FPL=1: one launch per frame (the reference's dispatch structure)
     pipe.set_frames_per_launch(int(os.environ.get("RT_FPL", "0")))
     pipe.set_path_compaction(os.environ.get("RT_PATHS", "auto"))   # bounce launches
+    if hasattr(rt._lib.lib(), "rt_set_single_kernel"):
+        pipe.set_single_kernel(os.environ.get("RT_SINGLE", "auto"))
     if hasattr(rt._lib.lib(), "rt_set_tile_order"):
         pipe.set_tile_order(os.environ.get("RT_TILE_ORDER", "auto"))
     base = None
