@@ -248,6 +248,8 @@ def main():
     # warmup (untimed); the dispatch configs' frame 0 resets the accumulator
     if args.warmup:
         step_block(args.warmup, True)
+    # (HIP events created before the timed region: their creation is host work, not steps)
+    ev0, ev1, ev2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -255,7 +257,6 @@ def main():
 
     # timed: K steps issued by rt_update_frames, then the single gather of the tiles
     t0 = time.perf_counter()
-    ev0, ev1, ev2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
     ev0.record(stream)
     step_block(args.steps, args.warmup == 0)
     ev1.record(stream)
