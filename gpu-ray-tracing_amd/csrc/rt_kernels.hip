@@ -64,7 +64,7 @@ __device__ __forceinline__ void stamp(int k) {
 #endif
 
 // ---- diagnostic wave trace (RT_WAVE_TRACE=1 builds only; never in the product) -------
-// Per wave of the camera-ray-only instances: start and end s_memrealtime, HW_ID, XCC_ID,
+// Per wave of the camera-ray-only and bounce instances: start and end s_memrealtime, HW_ID, XCC_ID,
 // indexed by workgroup * 4 + wave (tools/wave_trace.py reads them via rt_diag_wave_trace).
 #ifndef RT_WAVE_TRACE
 #define RT_WAVE_TRACE 0
@@ -1634,7 +1634,12 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
             }
     }
 #if RT_SKO & 16
-    if (c[0].x == 12345.678f) p.out[0] = make_float4(c[1].x, c[1].y, c[1].z, (float)n[0]);
+    // every result stays live; the per-lane store happens only if a never-true runtime
+    // condition holds (no image traffic, all compute kept)
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s)
+        if (__float_as_uint(c[s].x + c[s].y + c[s].z) == p.hy_off + 0x7F7FFFFFu + n[s])
+            p.out[tc[s].idx] = make_float4(c[s].x, c[s].y, c[s].z, (float)n[s]);
 #elif RT_SINGLE_WT
     // write-through (sc1) stores: the lines leave the XCD's L2 as they are written, so the
     // launch ends with no dirty image lines to write back at the kernel boundary
@@ -1766,6 +1771,7 @@ __shared__ float4 s_pair_col[64];   // kBouncePair: wave 1's colours of the curr
 template <int kMode>
 __global__ __launch_bounds__(64 * bounce_waves<kMode>(), RT_BOUNCE_MIN_WAVES) void
 rt_bounce_kernel(const TraceParams p) {
+    WAVE_TRACE(0);
     constexpr bool kCompact = kMode == kBounceCompact, kPair = kMode == kBouncePair;
     constexpr uint32_t kW = bounce_waves<kMode>();
     const uint32_t lane = threadIdx.x & 63u;
@@ -1947,6 +1953,7 @@ rt_bounce_kernel(const TraceParams p) {
     }
     if (p.tile_cost && threadIdx.x == 0u)
         p.tile_cost[group] = (uint32_t)__builtin_amdgcn_s_memtime() - p.tile_cost[group];
+    WAVE_TRACE(1);
 }
 
 // launch_tile_order: one 1024-thread workgroup; bucket = quantised log2 of the cost (four

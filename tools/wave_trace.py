@@ -20,7 +20,8 @@ from gpu_ray_tracing.distributed import StripeRenderer  # noqa: E402
 
 import os
 DEBUG = os.environ.get("WT_DEBUG") == "1"
-CONF = {"K2": (1920, 1080, rt.SCENE_THREE, 3, 1), "K3": (1920, 1080, rt.SCENE_N, 500, 1)}
+CONF = {"K2": (1920, 1080, rt.SCENE_THREE, 3, 1), "K3": (1920, 1080, rt.SCENE_N, 500, 1),
+        "K5": (3840, 2160, rt.SCENE_N, 500, 8)}
 
 
 def analyse(raw, nwaves):
@@ -50,7 +51,10 @@ def analyse(raw, nwaves):
     dur = end - start
     pct = lambda v, q: float(np.percentile(v, q))
     xspan = [int(end[xcc == x].max()) for x in np.unique(xcc)]
+    top = np.sort(dur)[::-1][:8]
     return {"waves": int(len(a)), "simds": len(simd), "span_cycles": int(span),
+            "longest_waves_frac": [round(float(v) / span, 3) for v in top],
+            "simd_resident_waves_p10_p50_p90": [round(pct(np.array([sum(e - s for s, e in v) for v in simd.values()]), q) / span, 3) for q in (10, 50, 90)],
             "xcd_span_min_max": [round(min(xspan) / span, 3), 1.0],
             "simd_first_start_max": round(float(first.max()) / span, 3),
             "simd_last_end_p10_p50_p90_max": [round(pct(last, q) / span, 3) for q in (10, 50, 90, 100)],
@@ -66,10 +70,11 @@ def main(cfg="K3"):
                                        w, h, float(seeds[0]))
     pipe = rt.ComputeShaderPipeline(0)
     pipe.set_spheres(sc)
+    pipe.set_path_compaction(os.environ.get("RT_PATHS", "auto"))
     L = rt._lib.lib()
     L.rt_diag_wave_trace.argtypes = [ctypes.c_void_p, ctypes.c_uint]
     buf = (ctypes.c_ulonglong * (4 * (1 << 18)))()
-    for world in (1, 2, 4, 8):
+    for world in ((2, 4, 8) if cfg == "K5" else (1, 2, 4, 8)):   # (K5 at 1 rank: > 2^16 WGs)
         r = StripeRenderer(pipe, w, h, 0, world)
         r.frames(cam, sc, seeds[:5])                       # reset + tile-cost recording
         r.frames(cam.with_fields(camera_has_moved=0.0), sc, seeds[69:133])  # long recording
@@ -83,7 +88,7 @@ def main(cfg="K3"):
             np.save(f"{os.environ['WT_SAVE']}_w{world}.npy",
                     np.frombuffer(raw, np.uint64).reshape(-1, 4))
         d = analyse(raw, 1 << 18)
-        d.update(cfg=cfg, world=world)
+        d.update(cfg=cfg, world=world, paths=os.environ.get("RT_PATHS", "auto"))
         print(json.dumps(d), flush=True)
     pipe.close()
 
