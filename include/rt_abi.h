@@ -196,7 +196,11 @@ RT_API rt_status rt_last_launch_info(const rt_ctx* ctx, rt_launch_info* out);
 
 /* Context ---------------------------------------------------------------------------- */
 /* Create a context on HIP device `device`.  Replaces ComputeShaderPipeline::from_world
- * (lib.rs:240-324): there is no shader compile step, code objects are linked in. */
+ * (lib.rs:240-324): there is no shader compile step, code objects are linked in.
+ * A context keeps device state its launches share (sphere records, candidate lists, tile
+ * order, hash tables) and rewrites it in stream order: issue every call on one context
+ * from one stream (as the reference's render node does), or synchronise before switching
+ * streams.  Separate contexts are independent. */
 RT_API rt_status rt_create(int device, rt_ctx** out_ctx);
 RT_API rt_status rt_destroy(rt_ctx* ctx);
 
@@ -295,7 +299,10 @@ RT_API rt_status rt_set_path_compaction(rt_ctx* ctx, int mode);
 #define RT_SINGLE_PAIR 2
 #define RT_SINGLE_ONE 3
 RT_API rt_status rt_set_single_kernel(rt_ctx* ctx, int mode);
-/* The frames per launch rt_update_frames would use for `camera` (its max_depth) now. */
+/* The frames-per-launch cap rt_update_frames applies for `camera` (its max_depth) with the
+ * context's settings.  The image size, stripe map and scene are not known here, and a
+ * launch whose camera rays fall outside the fast instances' proven domain runs one frame
+ * per launch: rt_last_launch_info reports what a call actually launched. */
 RT_API rt_status rt_get_frames_per_launch(const rt_ctx* ctx, const rt_scene_camera* camera,
                                           uint32_t* out_frames);
 RT_API rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t width,
