@@ -16,11 +16,13 @@ for c in $CFGS; do
   K=$(python3 -c "import json; print(json.loads(open('$O/pmc_bench_$c.json').read())['roofline']['kernel'])")
   F=$(python3 -c "import json; print(json.loads(open('$O/pmc_bench_$c.json').read())['roofline']['frames_per_launch'])")
   i=0
-  for CS in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+  for CS in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY"; do
     i=$((i+1))
     timeout -k 10 300 rocprofv3 --pmc $CS --output-format csv -d $O/raw -o ${c}_p$i -- python3 bench.py $ARGS \
       > $O/pmc_${c}_p$i.log 2>&1 || { echo "pmc $c pass $i failed"; tail -5 $O/pmc_${c}_p$i.log; exit 1; }
   done
   python3 tools/pmc_bench_summary.py $O/pmc_r02_$c.json "$K" "$F" $O/raw/${c}_p1_counter_collection.csv \
-    $O/raw/${c}_p2_counter_collection.csv $O/raw/${c}_p3_counter_collection.csv || exit 1
+    $O/raw/${c}_p2_counter_collection.csv $O/raw/${c}_p3_counter_collection.csv \
+    $O/raw/${c}_p4_counter_collection.csv || exit 1
 done

@@ -32,5 +32,9 @@ if "SQ_INSTS_VALU" in med:
     res["valu_insts_per_wave"] = med["SQ_INSTS_VALU"] / max(1.0, med.get("SQ_WAVES", 1.0))
 if "GRBM_GUI_ACTIVE" in med:
     res["gui_active_cycles_per_xcd"] = med["GRBM_GUI_ACTIVE"] / 8
+if "SQ_ACTIVE_INST_VALU" in med:
+    # quad-cycles (SQ_WAVE_CYCLES / SQ_WAVES in the same unit matches the measured mean wave
+    # life): the VALU pipes' busy cycles summed over all SIMDs
+    res["valu_active_cycles_per_launch"] = med["SQ_ACTIVE_INST_VALU"] * 4
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: v for k, v in res.items() if k != "dispatches"}))
