@@ -210,9 +210,17 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with "
                          f"torch.distributed.run --nproc-per-node N")
-    torch.cuda.set_device(local_rank)
+    # RT_BENCH_BACKEND=gloo rehearses the N > 1 path with every rank on the visible GPUs
+    # (several ranks per GPU; the gather staged through host memory) — a check of the
+    # multi-rank flow and its image on a one-GPU box, never a measurement
+    backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
+    device = local_rank if backend == "nccl" else local_rank % torch.cuda.device_count()
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     cfg = args.config
     w, h, kind, nsph, depth, spf, desc = CONFIGS[cfg]
@@ -232,7 +240,7 @@ def main():
         cam0 = cam_t = rt.SceneCamera(g["camera"])
         assert cam0.camera_has_moved > 0.5 and len(seeds) == spf
 
-    pipe = rt.ComputeShaderPipeline(local_rank)
+    pipe = rt.ComputeShaderPipeline(device)
     pipe.set_scan_mode(args.scan)
     pipe.set_spheres(spheres)
     if dispatch:
@@ -331,7 +339,8 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded scene + per-frame seeds; SURVEY §8d)",
+        "data": "synthetic (seeded scene + per-frame seeds; SURVEY §8d)"
+                + ("" if backend == "nccl" else f"; REHEARSAL over {backend}, not a measurement"),
         "config": {"workload": f"{cfg} {desc}, max_depth {depth}",
                    "width": w, "height": h, "spheres": nsph, "spp_per_step": spf,
                    "max_depth": depth, "parallelism": f"stripes{world}",

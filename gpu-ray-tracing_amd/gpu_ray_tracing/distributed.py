@@ -25,9 +25,18 @@ def gather_stripes(local: torch.Tensor, world: int, rank: int, dst: int = 0,
     """Gather equal-shaped (rows0, W, 4) tiles to `dst` as one (world*rows0, W, 4) tensor
     (into `out`, shaped (world, rows0, W, 4), when given).
 
-    One collective (dist.gather; RCCL on GPU, gloo on CPU)."""
+    One collective (dist.gather; RCCL on GPU, gloo on CPU — device tensors under gloo are
+    staged through host memory, which gloo's gather requires)."""
     if world == 1:
         return local
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        host = gather_stripes(local.cpu(), world, rank, dst, group)
+        if host is None:
+            return None
+        if out is None:
+            return host.to(local.device)
+        out.copy_(host.reshape(out.shape))
+        return out.reshape((world * local.shape[0],) + tuple(local.shape[1:]))
     if rank == dst:
         if out is None:
             out = torch.empty((world,) + tuple(local.shape), dtype=local.dtype,
