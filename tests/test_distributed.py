@@ -160,3 +160,62 @@ def test_stripe_renderer_finish_gloo(world, w, h, dst):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert q.get(timeout=5) is True
+
+
+def _hip_renderer_worker(rank, world, port, w, h, dst, q):
+    """One rank of a StripeRenderer job on the real HIP pipeline; every rank on GPU 0 (the
+    gather over gloo, staged through host memory by gather_stripes)."""
+    sys.path[:0] = [str(PKG_DIR), str(ROOT)]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        import gpu_ray_tracing as rt
+        from gpu_ray_tracing.distributed import StripeRenderer
+        from oracle import oracle as O
+        sc = rt.create_default_spheres(seed=5)
+        seeds = rt.frame_seeds(12, 7)
+        moved = rt.SceneCamera.from_settings(
+            rt.CameraSettings(max_depth=4, samples_per_pixel=500), w, h, float(seeds[0]))
+        still = moved.with_fields(camera_has_moved=0.0)
+        pipe = rt.ComputeShaderPipeline(0)
+        r = StripeRenderer(pipe, w, h, rank, world)
+        # bench.py's step shape: a fused first call, then per-dispatch frames, then the gather
+        r.frame(moved, sc, seeds[:2])
+        r.frames(still, sc, seeds[2:5])
+        pipe.set_frames_per_launch(1)
+        r.frames(still, sc, seeds[5:7])
+        img = r.finish(dst=dst)
+        if rank == dst:
+            full, _ = O.render(np.zeros((h, w, 4), np.float32), moved.blob, sc.spheres, seeds[:2])
+            full, _ = O.render(full, still.blob, sc.spheres, seeds[2:7])
+            got = img.cpu().numpy()
+            q.put(bool(got.shape == (h, w, 4)
+                       and np.array_equal(got.view(np.uint32), full.view(np.uint32))))
+        else:
+            assert img is None
+        torch.cuda.synchronize()
+        pipe.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,w,h,dst", [(2, 40, 32, 0), (3, 33, 41, 0), (3, 24, 16, 1)])
+def test_stripe_renderer_hip_multiprocess(world, w, h, dst):
+    """The product's multi-rank path on the GPU: `world` processes (all on GPU 0) each render
+    their bands with the HIP kernels (rt_update_frames, fused and one launch per frame), the
+    tiles are gathered to `dst` and de-interleaved by rt_deinterleave_stripes; the image must
+    equal the oracle's single-process render bit for bit (ragged bands, ranks without bands,
+    a non-zero root).  Only the RCCL transport is replaced by gloo here."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hip_renderer_worker, args=(r, world, port, w, h, dst, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=100)
+        assert p.exitcode == 0
+    assert q.get(timeout=5) is True
