@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -43,6 +44,12 @@ struct rt_ctx {
     } grid;
     // Per-tile candidate lists of camera rays (culled scan), valid for cand_key.
     float4* cand = nullptr;   // [tile][rtk::kCandStride] candidate blocks
+    // band order of one-frame launches (rtk::launch_band_order), for candidate generation
+    // band_gen; built when a generation is used a second time (a camera that moves every
+    // frame never pays for it)
+    uint32_t* band_order = nullptr;
+    uint32_t band_cap = 0;
+    uint64_t band_gen = ~0ull, band_seen_gen = ~0ull;
     uint64_t cand_tiles = 0;        // allocated tiles
     std::vector<unsigned char> cand_key;
     uint64_t cand_gen = 0;          // bumped whenever the lists are rebuilt
@@ -554,6 +561,46 @@ rt_status plan_tile_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
     return RT_OK;
 }
 
+// Band order of one-frame launches (rt_single_kernel): the rows of the current candidate
+// generation by decreasing list load, costliest first (scheduling only; see
+// rtk::launch_band_order).  Built on the second launch of a generation.
+rt_status plan_band_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t stream) {
+    p.band_order = nullptr;
+    static const bool off = [] {   // RT_BAND_ORDER=0: top to bottom (measurements)
+        const char* e = std::getenv("RT_BAND_ORDER");
+        return e && e[0] == '0';
+    }();
+    if (off || (kernel != rtk::kTraceSingle && kernel != rtk::kTraceSingleOne) || p.cand_k == 0 ||
+        p.local_bands < 2 || p.local_bands > rtk::kBandOrderMax ||
+        ctx->tile_order_mode == RT_TILE_ORDER_OFF)
+        return RT_OK;
+    const uint64_t gen = ctx->cand_gen;
+    if (ctx->band_gen != gen) {
+        if (ctx->band_seen_gen != gen) {        // first launch of this generation
+            ctx->band_seen_gen = gen;
+            return RT_OK;
+        }
+        if (p.local_bands > ctx->band_cap) {
+            if (ctx->band_cap) {
+                hipError_t e = hipStreamSynchronize(stream);   // old order may be in use
+                if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+            }
+            (void)hipFree(ctx->band_order);
+            ctx->band_order = nullptr;
+            ctx->band_cap = 0;
+            hipError_t e = hipMalloc(&ctx->band_order, rtk::kBandOrderMax * sizeof(uint32_t));
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc(band order)");
+            ctx->band_cap = rtk::kBandOrderMax;
+        }
+        hipError_t e = rtk::launch_band_order(p.cand, (p.width + 7u) >> 3, p.local_bands,
+                                              ctx->band_order, stream);
+        if (e != hipSuccess) return hip_fail(e, "rt_band_order_kernel launch");
+        ctx->band_gen = gen;
+    }
+    p.band_order = ctx->band_order;
+    return RT_OK;
+}
+
 // After a launch that recorded tile costs.
 void finish_tile_order(rt_ctx* ctx, const rtk::TraceParams& p) {
     if (!p.tile_cost) return;
@@ -789,6 +836,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         plan_hint(ctx, p, src, dst);
         const int kernel = single_or(ctx, p, trace_kernel_for(ctx, p));
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
+        if (rt_status s = plan_band_order(ctx, p, kernel, stream)) return s;
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         finish_tile_order(ctx, p);
@@ -850,6 +898,7 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->tile_cost);
         (void)hipFree(ctx->tile_order);
         (void)hipFree(ctx->d_grid);
+        (void)hipFree(ctx->band_order);
         free_candidates(ctx);
     }
     delete ctx;
@@ -1017,6 +1066,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         }
         kernel = single_or(ctx, p, kernel);
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
+        if (rt_status s = plan_band_order(ctx, p, kernel, stream)) return s;
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         finish_tile_order(ctx, p);

@@ -55,6 +55,9 @@ struct TraceParams {
     uint32_t lds_records;  // culled scan: records staged in LDS (0 = read from HBM/L2)
     uint32_t cand_k;       // per-tile candidate list capacity (0 = no lists)
     const float4* cand;    // [tile][kCandStride] candidate blocks (see kCandStride)
+    // one-frame launches (rt_single_kernel): local bands in decreasing candidate-list load
+    // (launch_band_order), null = top to bottom
+    const uint32_t* band_order;
     // Uniform XZ grid over the small spheres for bounce rays (rt_kernels.hip scan_grid;
     // built by rt_abi.cpp build_grid): per cell the range of its items, each item a copy
     // of the sphere's scan record and its index (every small sphere is registered in the
@@ -171,6 +174,12 @@ hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream);
 // Builds the per-tile candidate blocks for p's camera/scene/stripes (p.cand_k entries at
 // most per tile).
 hipError_t launch_candidates(const TraceParams& p, float4* cand, hipStream_t stream);
+// band_order for one-frame launches: the local bands by decreasing load of their tiles'
+// candidate lists (sum over tiles of 4 + count for tiles with a list entry, 64 for tiles
+// without a list), ties in band order.  At most kBandOrderMax bands.
+constexpr uint32_t kBandOrderMax = 1024;
+hipError_t launch_band_order(const float4* cand, uint32_t tiles_x, uint32_t bands,
+                             uint32_t* band_order, hipStream_t stream);
 hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t width,
                                uint32_t height, uint32_t nranks, uint32_t max_local_rows,
                                hipStream_t stream);

@@ -1238,6 +1238,7 @@ struct SingleParams {
     uint32_t n_hint;       // every pixel's count before the frame (0 on reset)
     uint32_t seed_b;       // B = u32(random_seed * 2^32) (wgsl:311, 353)
     uint32_t hy_off;       // hash(y * 51) table offset in the hx buffer
+    const uint32_t* band_order;   // local band of blockIdx.y (null: blockIdx.y)
     double rcp_hint;       // RN64(1 / (n_hint + 1))
     float4 rs;             // (rf(sb), random_unit_vector(sb)) of frame 0, bounce 0
     double disk_rcp[8];
@@ -1290,6 +1291,7 @@ constexpr uint32_t kSingleWg = RT_SINGLE_WG;
 #ifndef RT_SINGLE_WT
 #define RT_SINGLE_WT 1
 #endif
+
 
 // Shading of a camera ray's hit at depth 1 (ray_color's loop body at i = 0, wgsl:266-286):
 // sets the scattered direction and attenuation, or black (metal absorbed).  r_sb / ruv are
@@ -1512,7 +1514,11 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t tiles_x = (a_width + 7u) >> 3;
     const uint32_t tx0 = (blockIdx.x * kSingleWg + wave) * S;
-    const uint32_t lband = blockIdx.y;
+    // bands by decreasing candidate-list load (launch_band_order): the costliest rows are
+    // dispatched first and the cheap ones fill the tail (rows stay whole, so the
+    // accumulator traffic keeps its locality)
+    const uint32_t lband =
+        p.band_order ? __builtin_amdgcn_readfirstlane(p.band_order[blockIdx.y]) : blockIdx.y;
     const uint32_t band_first = a_bands & 0xFFFFu, band_step = (a_bands >> 16) & 0x7FFFu;
     TileCoord tc[S];
     uint32_t ncand[S], hxy[S];
@@ -2034,6 +2040,37 @@ hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, ui
     return hipGetLastError();
 }
 
+// launch_band_order: one 1024-thread workgroup.  Each wave sums its bands' tile loads (lane
+// per tile column, a DPP reduction), then every thread ranks its bands against all others
+// (LDS broadcast reads): rank = bands with a larger load, or an equal load and a lower
+// index.  Scheduling only: which band a workgroup row traces, never what it computes.
+__global__ __launch_bounds__(1024) void rt_band_order_kernel(const float4* __restrict__ cand,
+                                                             uint32_t tiles_x, uint32_t bands,
+                                                             uint32_t* __restrict__ order) {
+    __shared__ uint32_t s_load[kBandOrderMax];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    for (uint32_t b = wave; b < bands; b += 16u) {
+        uint32_t sum = 0u;
+        for (uint32_t tx = lane; tx < tiles_x; tx += 64u) {
+            const uint32_t c = load_cnt(cand, b * tiles_x + tx);
+            sum += c == kCandNone ? 64u : (c ? 4u + c : 0u);
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
+        if (lane == 0u) s_load[b] = sum;
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < bands; b += 1024u) {
+        const uint32_t mine = s_load[b];
+        uint32_t rank = 0u;
+        for (uint32_t o = 0; o < bands; ++o) {
+            const uint32_t v = s_load[o];
+            rank += (v > mine || (v == mine && o < b)) ? 1u : 0u;
+        }
+        order[rank] = b;
+    }
+}
+
 // List the spheres the camera rays of each tile can hit (see footprint_cone).
 // One wave per block of 8 x 8 tiles (8 columns of tiles x 8 local bands), one lane per
 // tile.  The wave first tests the spheres, 64 at a time, against the cone of the whole
@@ -2374,6 +2411,7 @@ static void launch_single(const TraceParams& p, hipStream_t stream) {
     q.n_hint = p.hint_n[0];
     q.seed_b = p.seed_b[0];
     q.hy_off = (uint32_t)(p.hy - p.hx);
+    q.band_order = p.band_order;
     q.rcp_hint = p.hint_rcp[0];
     q.rs = p.hint_rs[0];
     for (int k = 0; k < 8; ++k) q.disk_rcp[k] = p.disk_rcp[k];
@@ -2419,6 +2457,14 @@ hipError_t launch_candidates(const TraceParams& p, float4* cand, hipStream_t str
                     (p.local_bands + kCandBY - 1u) / kCandBY);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
     hipLaunchKernelGGL(rt_candidates_kernel, grid, dim3(64), 0, stream, p, cand);
+    return hipGetLastError();
+}
+
+hipError_t launch_band_order(const float4* cand, uint32_t tiles_x, uint32_t bands,
+                             uint32_t* band_order, hipStream_t stream) {
+    if (bands == 0 || bands > kBandOrderMax) return hipSuccess;
+    hipLaunchKernelGGL(rt_band_order_kernel, dim3(1), dim3(1024), 0, stream, cand, tiles_x,
+                       bands, band_order);
     return hipGetLastError();
 }
 
