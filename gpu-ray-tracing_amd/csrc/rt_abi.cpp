@@ -49,6 +49,9 @@ struct rt_ctx {
     // frame never pays for it)
     uint32_t* band_order = nullptr;
     uint32_t band_cap = 0;
+    uint32_t* wg_buf = nullptr;      // wg_order (RT_BAND_ORDER=2): cost + order words
+    uint64_t wg_cap = 0;
+    uint32_t wg_pix = 0;
     uint64_t band_gen = ~0ull, band_seen_gen = ~0ull;
     uint64_t cand_tiles = 0;        // allocated tiles
     std::vector<unsigned char> cand_key;
@@ -561,15 +564,20 @@ rt_status plan_tile_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
     return RT_OK;
 }
 
-// Band order of one-frame launches (rt_single_kernel): the rows of the current candidate
-// generation by decreasing list load, costliest first (scheduling only; see
-// rtk::launch_band_order).  Built on the second launch of a generation.
+// Dispatch order of one-frame launches (rt_single_kernel): the workgroups (or whole rows)
+// of the current candidate generation by decreasing list load, costliest first (scheduling
+// only; rtk::launch_wg_order, rtk::launch_band_order).  Built on the second launch of a
+// generation.
 rt_status plan_band_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t stream) {
     p.band_order = nullptr;
-    static const bool off = [] {   // RT_BAND_ORDER=0: top to bottom (measurements)
+    p.wg_order = nullptr;
+    // RT_BAND_ORDER (measurements): 0 = top to bottom, 1 = whole bands by load, 2 (default)
+    // = workgroups by load
+    static const int mode = [] {
         const char* e = std::getenv("RT_BAND_ORDER");
-        return e && e[0] == '0';
+        return e ? (int)std::strtol(e, nullptr, 10) : 2;
     }();
+    const bool off = mode == 0;
     if (off || (kernel != rtk::kTraceSingle && kernel != rtk::kTraceSingleOne) || p.cand_k == 0 ||
         p.local_bands < 2 || p.local_bands > rtk::kBandOrderMax ||
         ctx->tile_order_mode == RT_TILE_ORDER_OFF)
@@ -596,6 +604,31 @@ rt_status plan_band_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
                                               ctx->band_order, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_band_order_kernel launch");
         ctx->band_gen = gen;
+        ctx->wg_pix = 0;
+    }
+    if (mode == 2) {
+        const uint32_t pix = kernel == rtk::kTraceSingle ? rtk::single_pix() : 1u;
+        const uint32_t per = rtk::single_wg_tiles(pix);
+        const uint64_t units = (uint64_t)((((p.width + 7u) >> 3) + per - 1u) / per) * p.local_bands;
+        if (units > ctx->wg_cap) {
+            hipError_t e = hipStreamSynchronize(stream);
+            if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+            (void)hipFree(ctx->wg_buf);
+            ctx->wg_buf = nullptr;
+            ctx->wg_cap = 0;
+            e = hipMalloc(&ctx->wg_buf, (2 * units + 1) * sizeof(uint32_t));
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc(workgroup order)");
+            ctx->wg_cap = units;
+            ctx->wg_pix = 0;
+        }
+        if (ctx->wg_pix != pix) {
+            hipError_t e = rtk::launch_wg_order(p.cand, (p.width + 7u) >> 3, p.local_bands, pix,
+                                                ctx->wg_buf, ctx->wg_buf + units, stream);
+            if (e != hipSuccess) return hip_fail(e, "workgroup order launch");
+            ctx->wg_pix = pix;
+        }
+        p.wg_order = ctx->wg_buf + units;
+        return RT_OK;
     }
     p.band_order = ctx->band_order;
     return RT_OK;
@@ -899,6 +932,7 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->tile_order);
         (void)hipFree(ctx->d_grid);
         (void)hipFree(ctx->band_order);
+        (void)hipFree(ctx->wg_buf);
         free_candidates(ctx);
     }
     delete ctx;

@@ -58,6 +58,9 @@ struct TraceParams {
     // one-frame launches (rt_single_kernel): local bands in decreasing candidate-list load
     // (launch_band_order), null = top to bottom
     const uint32_t* band_order;
+    // one-frame launches: workgroup u traces (band << 16 | column group) wg_order[u]
+    // (launch_wg_order), null = band_order / natural order
+    const uint32_t* wg_order;
     // Uniform XZ grid over the small spheres for bounce rays (rt_kernels.hip scan_grid;
     // built by rt_abi.cpp build_grid): per cell the range of its items, each item a copy
     // of the sphere's scan record and its index (every small sphere is registered in the
@@ -180,6 +183,13 @@ hipError_t launch_candidates(const TraceParams& p, float4* cand, hipStream_t str
 constexpr uint32_t kBandOrderMax = 1024;
 hipError_t launch_band_order(const float4* cand, uint32_t tiles_x, uint32_t bands,
                              uint32_t* band_order, hipStream_t stream);
+// wg_order for one-frame launches of `pix` tiles per wave: the workgroups by decreasing
+// candidate-list load (the same per-tile load), sorted by launch_tile_order's buckets;
+// wg_cost is scratch of one word per workgroup.
+hipError_t launch_wg_order(const float4* cand, uint32_t tiles_x, uint32_t bands, uint32_t pix,
+                           uint32_t* wg_cost, uint32_t* wg_order, hipStream_t stream);
+uint32_t single_wg_tiles(uint32_t pix);
+uint32_t single_pix();   // tiles per wave of kTraceSingle
 hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t width,
                                uint32_t height, uint32_t nranks, uint32_t max_local_rows,
                                hipStream_t stream);

@@ -1239,6 +1239,7 @@ struct SingleParams {
     uint32_t seed_b;       // B = u32(random_seed * 2^32) (wgsl:311, 353)
     uint32_t hy_off;       // hash(y * 51) table offset in the hx buffer
     const uint32_t* band_order;   // local band of blockIdx.y (null: blockIdx.y)
+    const uint32_t* wg_order;     // (band << 16 | column group) of workgroup u (null: none)
     double rcp_hint;       // RN64(1 / (n_hint + 1))
     float4 rs;             // (rf(sb), random_unit_vector(sb)) of frame 0, bounce 0
     double disk_rcp[8];
@@ -1513,12 +1514,19 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t tiles_x = (a_width + 7u) >> 3;
-    const uint32_t tx0 = (blockIdx.x * kSingleWg + wave) * S;
     // bands by decreasing candidate-list load (launch_band_order): the costliest rows are
     // dispatched first and the cheap ones fill the tail (rows stay whole, so the
-    // accumulator traffic keeps its locality)
-    const uint32_t lband =
-        p.band_order ? __builtin_amdgcn_readfirstlane(p.band_order[blockIdx.y]) : blockIdx.y;
+    // accumulator traffic keeps its locality); or workgroups by decreasing load (wg_order)
+    uint32_t gx = blockIdx.x, lband = blockIdx.y;
+    if (p.wg_order) {
+        const uint32_t e = __builtin_amdgcn_readfirstlane(
+            p.wg_order[blockIdx.y * gridDim.x + blockIdx.x]);
+        gx = e & 0xFFFFu;
+        lband = e >> 16;
+    } else if (p.band_order) {
+        lband = __builtin_amdgcn_readfirstlane(p.band_order[blockIdx.y]);
+    }
+    const uint32_t tx0 = (gx * kSingleWg + wave) * S;
     const uint32_t band_first = a_bands & 0xFFFFu, band_step = (a_bands >> 16) & 0x7FFFu;
     TileCoord tc[S];
     uint32_t ncand[S], hxy[S];
@@ -2071,6 +2079,25 @@ __global__ __launch_bounds__(1024) void rt_band_order_kernel(const float4* __res
     }
 }
 
+// Per-workgroup candidate-list load of one-frame launches (wg_order's sort key): the sum of
+// its `per` tiles' loads, as rt_band_order_kernel weighs them.
+__global__ __launch_bounds__(256) void rt_wg_cost_kernel(const float4* __restrict__ cand,
+                                                         uint32_t tiles_x, uint32_t cols,
+                                                         uint32_t per, uint32_t units,
+                                                         uint32_t* __restrict__ cost) {
+    const uint32_t u = blockIdx.x * 256u + threadIdx.x;
+    if (u >= units) return;
+    const uint32_t b = u / cols, g = u % cols;
+    uint32_t sum = 1u;                                  // (cost 0 sorts last)
+    for (uint32_t k = 0; k < per; ++k) {
+        const uint32_t tx = g * per + k;
+        if (tx >= tiles_x) break;
+        const uint32_t c = load_cnt(cand, b * tiles_x + tx);
+        sum += c == kCandNone ? 64u : (c ? 4u + c : 0u);
+    }
+    cost[u] = sum;
+}
+
 // List the spheres the camera rays of each tile can hit (see footprint_cone).
 // One wave per block of 8 x 8 tiles (8 columns of tiles x 8 local bands), one lane per
 // tile.  The wave first tests the spheres, 64 at a time, against the cone of the whole
@@ -2412,6 +2439,7 @@ static void launch_single(const TraceParams& p, hipStream_t stream) {
     q.seed_b = p.seed_b[0];
     q.hy_off = (uint32_t)(p.hy - p.hx);
     q.band_order = p.band_order;
+    q.wg_order = p.wg_order;
     q.rcp_hint = p.hint_rcp[0];
     q.rs = p.hint_rs[0];
     for (int k = 0; k < 8; ++k) q.disk_rcp[k] = p.disk_rcp[k];
@@ -2466,6 +2494,22 @@ hipError_t launch_band_order(const float4* cand, uint32_t tiles_x, uint32_t band
     hipLaunchKernelGGL(rt_band_order_kernel, dim3(1), dim3(1024), 0, stream, cand, tiles_x,
                        bands, band_order);
     return hipGetLastError();
+}
+
+uint32_t single_wg_tiles(uint32_t pix) { return kSingleWg * pix; }
+uint32_t single_pix() { return kSinglePix; }
+
+hipError_t launch_wg_order(const float4* cand, uint32_t tiles_x, uint32_t bands, uint32_t pix,
+                           uint32_t* wg_cost, uint32_t* wg_order, hipStream_t stream) {
+    const uint32_t per = kSingleWg * pix;
+    const uint32_t cols = (tiles_x + per - 1u) / per;
+    const uint32_t units = cols * bands;
+    if (units == 0) return hipSuccess;
+    hipLaunchKernelGGL(rt_wg_cost_kernel, dim3((units + 255u) / 256u), dim3(256), 0, stream, cand,
+                       tiles_x, cols, per, units, wg_cost);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_tile_order(wg_cost, wg_order, units, cols, stream);
 }
 
 hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream) {
