@@ -268,12 +268,14 @@ RT_API rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launc
 #define RT_FRAME_PAIRS_ON 2
 #define RT_FRAME_PAIRS_QUAD 3
 RT_API rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode);
-/* Tile scheduling of the fused multi-frame launches of the camera-ray-only kernels
- * (max_depth <= 1, culled scan mode).  AUTO (default): the first such launch for a camera
+/* Tile scheduling (culled scan mode).  AUTO (default): fused multi-frame launches (the
+ * camera-ray-only kernels and the bounce instance): the first such launch for a camera
  * geometry / image / stripe map / scene records each 8x8 tile's duration on the device,
  * and later launches hand the costliest tiles to the first workgroups so that cheap tiles
- * fill the tail (strong scaling: a rank's share is only a few workgroups per SIMD).  OFF,
- * and single-frame launches: tiles in raster order.  Pixel results are identical. */
+ * fill the tail (strong scaling: a rank's share is only a few workgroups per SIMD);
+ * one-frame launches (rt_single_kernel): from the second launch of a camera geometry on,
+ * workgroups are dispatched by decreasing load of their tiles' candidate lists.  OFF:
+ * raster order everywhere.  Pixel results are identical. */
 #define RT_TILE_ORDER_AUTO 0
 #define RT_TILE_ORDER_OFF 1
 RT_API rt_status rt_set_tile_order(rt_ctx* ctx, int mode);
