@@ -671,6 +671,12 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
     d = sub(pc, o);
 }
 
+// component-wise select of two v3 (a select of whole v3 values can leave them in
+// scratch memory)
+__device__ __forceinline__ v3 sel3(bool c, v3 a, v3 b) {
+    return mk(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z);
+}
+
 // normalize(v) = v / sqrt(v.v) (WGSL normalize).  kFast: when every active lane's |v|^2 is
 // in [2^-20, 2^40] (NaN, 0 and inf are not) and its components are >= 2^-100 in
 // magnitude, sqrt_core and div_core with the shared reciprocal of |v| in [2^-10, 2^20]
@@ -769,12 +775,11 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
             outward = divs(rel, pr.w);
         }
         const bool front = dot(d, outward) < 0.0f;
-        const v3 n = front ? outward : neg(outward);
-        v3 att, nd;
+        const v3 n = sel3(front, outward, neg(outward));
+        v3 att = mk(1.0f, 1.0f, 1.0f), nd = d;   // (defined on every path: kept in registers)
         if (mat.w < -1.0f) {                                      // lambertian wgsl:84-93
-            v3 dir = add(n, ruv);
-            if (dot(dir, dir) < 0x1.0c6f7ap-20f) dir = n;
-            nd = dir;
+            const v3 dir = add(n, ruv);
+            nd = sel3(dot(dir, dir) < 0x1.0c6f7ap-20f, n, dir);
             att = mk(mat.x, mat.y, mat.z);
         } else if (mat.w <= 1.0f) {                               // metal wgsl:95-100
             constexpr bool kF = fast_core<kScan>(8);
@@ -795,8 +800,7 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
             const float sin_t = sqrtf(fmaf(-cos_t, cos_t, 1.0f));
             const bool cannot = ratio * sin_t > 1.0f;
             const bool refl = cannot || reflectance(cos_t, ratio) > r_sb;
-            const v3 dir = refl ? reflect(u, n) : refract(u, n, ratio);
-            nd = normalize_w<kF>(dir);
+            nd = normalize_w<kF>(sel3(refl, reflect(u, n), refract(u, n, ratio)));
         }
         cf = mul(cf, att);                                        // wgsl:285-286
         o = hp;
@@ -1705,24 +1709,32 @@ struct BounceLds {
 };
 __shared__ BounceLds s_bounce;
 
+
 // One bounce of a path after its hit (wgsl:205-218 record, wgsl:268-286 scatter): the new
 // direction and attenuation, or false when the metal scatter absorbs it.
-__device__ __forceinline__ bool scatter_path(float4 pr, float4 mat, float t, v3 o, v3 d,
-                                             uint32_t sb, v3& hp, v3& nd, v3& att) {
+struct Scatter {
+    v3 hp, nd, att;
+    bool ok;   // false: the metal scatter absorbed the path
+};
+__device__ __forceinline__ Scatter scatter_path(float4 pr, float4 mat, float t, v3 o, v3 d,
+                                                uint32_t sb) {
+    // (results returned by value: out-parameters through references stayed in scratch)
     const float r_sb = rf(sb);
     const v3 ruv = random_unit_vector(r_sb, sb);
-    hp = fmas(t, d, o);
+    const v3 hp = fmas(t, d, o);
+    v3 nd, att;
     const v3 outward = divs(sub(hp, mk(pr.x, pr.y, pr.z)), pr.w);          // wgsl:209
     const bool front = dot(d, outward) < 0.0f;
-    const v3 n = front ? outward : neg(outward);
+    // (component selects: a select of whole v3 values made the compiler keep them in
+    // scratch memory)
+    const v3 n = sel3(front, outward, neg(outward));
     if (mat.w < -1.0f) {                                      // lambertian wgsl:84-93
-        v3 dir = add(n, ruv);
-        if (dot(dir, dir) < 0x1.0c6f7ap-20f) dir = n;
-        nd = dir;
+        const v3 dir = add(n, ruv);
+        nd = sel3(dot(dir, dir) < 0x1.0c6f7ap-20f, n, dir);
         att = mk(mat.x, mat.y, mat.z);
     } else if (mat.w <= 1.0f) {                               // metal wgsl:95-100
         const v3 refl = fmas(mat.w, ruv, normalize(reflect(d, n)));
-        if (!(dot(refl, n) > 0.0f)) return false;             // wgsl:277-279
+        if (!(dot(refl, n) > 0.0f)) return Scatter{hp, d, d, false};   // wgsl:277-279
         nd = normalize(refl);
         att = mk(mat.x, mat.y, mat.z);
     } else {                                                  // dielectric wgsl:102-135
@@ -1733,9 +1745,9 @@ __device__ __forceinline__ bool scatter_path(float4 pr, float4 mat, float t, v3 
         const float sin_t = sqrtf(fmaf(-cos_t, cos_t, 1.0f));
         const bool cannot = ratio * sin_t > 1.0f;
         const bool refl = cannot || reflectance(cos_t, ratio) > r_sb;
-        nd = normalize(refl ? reflect(u, n) : refract(u, n, ratio));
+        nd = normalize(sel3(refl, reflect(u, n), refract(u, n, ratio)));
     }
-    return true;
+    return Scatter{hp, nd, att, true};
 }
 
 // Sky colour of the final direction times the throughput (wgsl:293-296).
@@ -1879,9 +1891,10 @@ rt_bounce_kernel(const TraceParams p) {
                     col = sky(cf, d);
                 } else {
                     const float4 pr = hs[2 * hit.idx], mat = hs[2 * hit.idx + 1];
-                    v3 hp, nd, att;
                     const uint32_t sb = hash(pseed + i * 1000u);  // wgsl:268
-                    if (!scatter_path(pr, mat, hit.t, o, d, sb, hp, nd, att)) {
+                    const Scatter sc = scatter_path(pr, mat, hit.t, o, d, sb);
+                    const v3 hp = sc.hp, nd = sc.nd, att = sc.att;
+                    if (!sc.ok) {
                         done = true;                              // absorbed: black
                     } else {
                         cf = mul(cf, att);                        // wgsl:285-286
