@@ -1243,7 +1243,6 @@ struct SingleParams {
     uint32_t seed_b;       // B = u32(random_seed * 2^32) (wgsl:311, 353)
     uint32_t hy_off;       // hash(y * 51) table offset in the hx buffer
     const uint32_t* band_order;   // local band of blockIdx.y (null: blockIdx.y)
-    const uint32_t* wg_order;     // (band << 16 | column group) of workgroup u (null: none)
     double rcp_hint;       // RN64(1 / (n_hint + 1))
     float4 rs;             // (rf(sb), random_unit_vector(sb)) of frame 0, bounce 0
     double disk_rcp[8];
@@ -1511,6 +1510,7 @@ template <int kPix>
 __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
     const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
+    const uint32_t* __restrict__ a_order,
     const SingleParams p) {
     static_assert(kPix >= 1 && kPix <= 4, "1 to 4 tiles per wave");
     constexpr uint32_t S = kPix;
@@ -1522,9 +1522,9 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
     // dispatched first and the cheap ones fill the tail (rows stay whole, so the
     // accumulator traffic keeps its locality); or workgroups by decreasing load (wg_order)
     uint32_t gx = blockIdx.x, lband = blockIdx.y;
-    if (p.wg_order) {
+    if (a_order) {   // (a leading, preloadable argument: one scalar load to the entry)
         const uint32_t e = __builtin_amdgcn_readfirstlane(
-            p.wg_order[blockIdx.y * gridDim.x + blockIdx.x]);
+            a_order[blockIdx.y * gridDim.x + blockIdx.x]);
         gx = e & 0xFFFFu;
         lband = e >> 16;
     } else if (p.band_order) {
@@ -2452,7 +2452,6 @@ static void launch_single(const TraceParams& p, hipStream_t stream) {
     q.seed_b = p.seed_b[0];
     q.hy_off = (uint32_t)(p.hy - p.hx);
     q.band_order = p.band_order;
-    q.wg_order = p.wg_order;
     q.rcp_hint = p.hint_rcp[0];
     q.rs = p.hint_rs[0];
     for (int k = 0; k < 8; ++k) q.disk_rcp[k] = p.disk_rcp[k];
@@ -2467,7 +2466,7 @@ static void launch_single(const TraceParams& p, hipStream_t stream) {
     q.defocus_angle = p.defocus_angle;
     hipLaunchKernelGGL(rt_single_kernel<kPix>, grid, dim3(64 * kSingleWg), 0, stream, p.cand,
                        p.hx, p.in, p.width, p.height, pack_bands(p.band_first, p.band_step, false),
-                       q);
+                       p.wg_order, q);
 }
 
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
