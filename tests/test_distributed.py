@@ -215,7 +215,13 @@ def test_stripe_renderer_hip_multiprocess(world, w, h, dst):
              for r in range(world)]
     for p in procs:
         p.start()
-    for p in procs:
-        p.join(timeout=100)
-        assert p.exitcode == 0
-    assert q.get(timeout=5) is True
+    try:
+        for p in procs:
+            p.join(timeout=240)
+            assert p.exitcode == 0
+        assert q.get(timeout=5) is True
+    finally:
+        for p in procs:               # (a rank left waiting on a failed peer)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
