@@ -69,10 +69,16 @@ def test_stripe_gather_gloo(world, w, h):
     procs = [ctx.Process(target=_worker, args=(r, world, port, w, h, q)) for r in range(world)]
     for p in procs:
         p.start()
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
-    assert q.get(timeout=5) is True
+    try:
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        assert q.get(timeout=5) is True
+    finally:
+        for p in procs:               # (a rank left waiting on a failed peer)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
 
 
 class _OraclePipeline:
@@ -156,10 +162,16 @@ def test_stripe_renderer_finish_gloo(world, w, h, dst):
              for r in range(world)]
     for p in procs:
         p.start()
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
-    assert q.get(timeout=5) is True
+    try:
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        assert q.get(timeout=5) is True
+    finally:
+        for p in procs:               # (a rank left waiting on a failed peer)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
 
 
 def _hip_renderer_worker(rank, world, port, w, h, dst, q):
