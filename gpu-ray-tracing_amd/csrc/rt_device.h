@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <string.h>
 
 #define RT_HD __host__ __device__ __forceinline__
 
@@ -53,6 +54,15 @@ RT_HD uint32_t f2u(float f) {
     return f >= 4294967296.0f ? 0xFFFFFFFFu : t;
 }
 
+// x with its sign bit xor-ed with m (0 or 0x80000000): the bits of x or -x
+RT_HD float flip_sign(float x, uint32_t m) {
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    u ^= m;
+    memcpy(&x, &u, 4);
+    return x;
+}
+
 // Canonical sin/cos: Cody-Waite by pi/2 in three parts, Cephes minimax.
 RT_HD void sincos_c(float x, float& s, float& c) {
     const float q = rintf(x * 0x1.45f306p-1f);
@@ -68,8 +78,9 @@ RT_HD void sincos_c(float x, float& s, float& c) {
     const bool swap = (k & 1) != 0;
     const float s0 = swap ? cr : sr;
     const float c0 = swap ? sr : cr;
-    s = (k & 2) ? -s0 : s0;
-    c = ((k + 1) & 2) ? -c0 : c0;
+    // the quadrant's signs as sign-bit flips (the bits of -x; no compare + select)
+    s = flip_sign(s0, ((uint32_t)k << 30) & 0x80000000u);
+    c = flip_sign(c0, ((uint32_t)(k + 1) << 30) & 0x80000000u);
 }
 
 // wgsl:234-243; rf_seed = rf(seed)
