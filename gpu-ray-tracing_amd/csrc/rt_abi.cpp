@@ -588,7 +588,7 @@ rt_status plan_band_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
             ctx->band_seen_gen = gen;
             return RT_OK;
         }
-        if (p.local_bands > ctx->band_cap) {
+        if (mode == 1 && p.local_bands > ctx->band_cap) {
             if (ctx->band_cap) {
                 hipError_t e = hipStreamSynchronize(stream);   // old order may be in use
                 if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
@@ -600,9 +600,11 @@ rt_status plan_band_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
             if (e != hipSuccess) return hip_fail(e, "hipMalloc(band order)");
             ctx->band_cap = rtk::kBandOrderMax;
         }
-        hipError_t e = rtk::launch_band_order(p.cand, (p.width + 7u) >> 3, p.local_bands,
-                                              ctx->band_order, stream);
-        if (e != hipSuccess) return hip_fail(e, "rt_band_order_kernel launch");
+        if (mode == 1) {
+            hipError_t e = rtk::launch_band_order(p.cand, (p.width + 7u) >> 3, p.local_bands,
+                                                  ctx->band_order, stream);
+            if (e != hipSuccess) return hip_fail(e, "rt_band_order_kernel launch");
+        }
         ctx->band_gen = gen;
         ctx->wg_pix = 0;
     }
