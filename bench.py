@@ -14,7 +14,8 @@ Configs (BASELINE.json `configs`):
                     is one 64-spp render (one 64-frame launch of the bounce instance).
 With N GPUs (one process per GPU, torch.distributed.run) the image is split into 8-row bands
 dealt round-robin; after the K timed steps the finished tiles are gathered to rank 0 with ONE
-RCCL gather + the de-interleave kernel, both inside the timed region.
+RCCL gather + the de-interleave kernel, both inside the timed region: rt_gather_stripes, the
+ncclGather behind librt_hip.so's C ABI (RT_GATHER=torch: torch.distributed.gather instead).
 
 value = W*H*spp_per_step*K camera rays / max-over-ranks wall time (Mrays/s, whole job).
 image_ok: the timed image against committed fixtures (K2/K3: 4096 sampled pixels after W+K
@@ -48,7 +49,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import gpu_ray_tracing as rt  # noqa: E402
-from gpu_ray_tracing.distributed import StripeRenderer  # noqa: E402
+from gpu_ray_tracing.distributed import StripeComm, StripeRenderer  # noqa: E402
 
 BASELINE = json.loads((ROOT / "BASELINE.json").read_text())
 GOLDEN = ROOT / "tests" / "golden"
@@ -101,14 +102,20 @@ def parse():
     return a
 
 
-def host_threads():
-    """Host cores for the threaded baseline: this process's CPU set, at most 16 (the GPU
-    box's per-GPU share)."""
+def host_cpus():
+    """(nproc, this process's CPU-affinity size): the whole machine and what we may use."""
+    nproc = os.cpu_count() or 1
     try:
-        n = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
+        aff = nproc
+    return nproc, aff
+
+
+def host_threads():
+    """Host cores for the threaded baseline: this process's CPU set, at most 16 (a GPU
+    box's per-GPU share of host cores: OMP_NUM_THREADS / MAX_JOBS are 16 there)."""
+    return max(1, min(16, host_cpus()[1]))
 
 
 def cpu_model():
@@ -151,19 +158,33 @@ def cpu_baseline(cam, spheres, w, h, seconds):
                       f"max_depth {int(cam.max_depth)}",
             "single_thread": {"value": round(single, 3), "cores": 1,
                               "sample": f"{w}x{rows1} rows of one update"},
-            "cpu_model": cpu_model()}
+            "cpu_model": cpu_model(),
+            "nproc": host_cpus()[0], "affinity_cpus": host_cpus()[1],
+            "cores_rule": "min(16, affinity): the per-GPU share of the box's host cores"}
 
 
 def load_pmc(config, kernel, frames_per_launch):
-    """The committed rocprofv3 PMC summary of the timed kernel (tools/pmc_bench.sh), if it
-    was taken for the same kernel instance at the same frames per launch."""
-    p = ROOT / "profiles" / f"pmc_r02_{config}.json"
+    """The newest committed rocprofv3 PMC summary of the timed kernel (tools/pmc_bench.sh),
+    if it was taken for the same kernel instance at the same frames per launch, and its
+    path."""
+    for rnd in ("r03", "r02"):
+        p = ROOT / "profiles" / f"pmc_{rnd}_{config}.json"
+        if not p.exists():
+            continue
+        d = json.loads(p.read_text())
+        if d.get("kernel") == kernel and d.get("frames_per_launch") == frames_per_launch:
+            return d, p.relative_to(ROOT).as_posix()
+    return None, None
+
+
+def load_weighted(config, kernel):
+    """The weighted VALU cycles per launch of the timed kernel (tools/valu_weighted.py over
+    the PMC instruction classes and the instance's disassembly), if committed."""
+    p = ROOT / "profiles" / f"valu_weighted_r03_{config}.json"
     if not p.exists():
-        return None
+        return None, None
     d = json.loads(p.read_text())
-    if d.get("kernel") != kernel or d.get("frames_per_launch") != frames_per_launch:
-        return None
-    return d
+    return (d, p.relative_to(ROOT).as_posix()) if d.get("kernel") == kernel else (None, None)
 
 
 def image_check(config, image, frames, cam, w, h):
@@ -245,7 +266,13 @@ def main():
     pipe.set_spheres(spheres)
     if dispatch:
         pipe.set_frames_per_launch(1)          # one `update` launch per frame
-    r = StripeRenderer(pipe, w, h, rank, world)
+    # the job's one gather: RCCL behind the C ABI (rt_comm_create + rt_gather_stripes)
+    use_abi = world > 1 and backend == "nccl" and os.environ.get("RT_GATHER", "abi") == "abi"
+    comm = StripeComm.from_process_group(pipe) if use_abi else None
+    gather_how = ("rt_gather_stripes: ncclGather + de-interleave in librt_hip.so" if use_abi
+                  else "none (one rank)" if world == 1
+                  else f"torch.distributed.gather over {backend} + rt_deinterleave_stripes")
+    r = StripeRenderer(pipe, w, h, rank, world, comm=comm)
     stream = torch.cuda.current_stream()
     local_px = w * min(r.rows, h)
 
@@ -291,6 +318,9 @@ def main():
         dt, render_s, gather_s = (float(x) for x in t.tolist())
     frames_total = (args.warmup + args.steps) if dispatch else spf
     image_ok, image_what = image_check(cfg, image, frames_total, cam0, w, h)
+    # this rank's per-tile candidate lists of the timed camera (a tile with more than
+    # kCandMax = 19 candidates has none: its camera rays scan the whole scene, same pixels)
+    cand_stats = pipe.candidate_stats()
 
     # dispatch configs: the timed steps are ONE rt_update_frames call (one launch per
     # frame); 64-spp configs: one call per step, all alike
@@ -303,7 +333,8 @@ def main():
     kernel = info["kernel_name"]
     fpl = info["max_frames_per_launch"]
     bytes_launch = local_px * BYTES_PER_PIXEL_LAUNCH
-    pmc = load_pmc(cfg, kernel, fpl) if world == 1 else None
+    pmc, pmc_path = load_pmc(cfg, kernel, fpl) if world == 1 else (None, None)
+    wgt, wgt_path = load_weighted(cfg, kernel) if pmc else (None, None)
     roof = {"bound": "hbm", "achieved": round(bytes_launch / launch_s / 1e9, 1),
             "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(bytes_launch / launch_s / 1e9 / PEAK_HBM_GBS, 4),
@@ -323,9 +354,19 @@ def main():
                         "issue_cycles": insts * VALU_ISSUE_CYCLES,
                         "available_cycles": round(avail),
                         "frac": round(insts * VALU_ISSUE_CYCLES / avail, 4),
-                        "pmc": f"profiles/pmc_r02_{cfg}.json",
+                        "pmc": pmc_path,
                         "rule": "VALU wave-instructions x 2 cycles / (1024 SIMDs x 2.4 GHz x "
                                 "kernel_avg_us)"}
+        if wgt:
+            # each PMC instruction class priced at the measured issue cost of the kernel's
+            # own forms of that class (profiles/r0*_valu_rates.txt): the SIMD cycles the
+            # VALU work holds, against what 1024 SIMDs offer at the 2.4-GHz peak clock
+            wc = wgt["weighted_cycles"]
+            roof["valu"].update({
+                "weighted_cycles": wc, "weighted_frac": round(wc / avail, 4),
+                "weighted_frac_bounds": [round(b / avail, 4) for b in wgt["weighted_cycles_bounds"]],
+                "mean_cycles_per_valu": wgt["mean_cycles_per_valu"], "weighted": wgt_path})
+            roof["binding_frac"] = roof["valu"]["weighted_frac"]
 
     line = {
         "metric": BASELINE["metric"],
@@ -351,6 +392,8 @@ def main():
         # max over ranks; value's time includes both (and the barriers)
         "timed_breakdown_ms": {"steps": round(render_s * 1e3, 4),
                                "gather_and_deinterleave": round(gather_s * 1e3, 4)},
+        "gather": gather_how,
+        "candidate_lists": cand_stats,
     }
 
     # ---- side measurements (after the timed region and its image check) -------------
@@ -420,6 +463,9 @@ def main():
         if world == 1 and args.cpu_seconds > 0:
             line["cpu_baseline"] = cpu_baseline(cam0, spheres, w, h, args.cpu_seconds)
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        torch.cuda.synchronize()
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
     pipe.close()

@@ -19,6 +19,7 @@
 
 #include "rt_abi.h"
 #include "rt_device.h"
+#include "rt_internal.h"
 #include "rt_kernels.h"
 
 struct rt_ctx {
@@ -44,16 +45,15 @@ struct rt_ctx {
     } grid;
     // Per-tile candidate lists of camera rays (culled scan), valid for cand_key.
     float4* cand = nullptr;   // [tile][rtk::kCandStride] candidate blocks
-    // band order of one-frame launches (rtk::launch_band_order), for candidate generation
+    // workgroup order of one-frame launches (rtk::launch_wg_order), for candidate generation
     // band_gen; built when a generation is used a second time (a camera that moves every
     // frame never pays for it)
-    uint32_t* band_order = nullptr;
-    uint32_t band_cap = 0;
-    uint32_t* wg_buf = nullptr;      // wg_order (RT_BAND_ORDER=2): cost + order words
+    uint32_t* wg_buf = nullptr;      // cost + order words
     uint64_t wg_cap = 0;
     uint32_t wg_pix = 0;
     uint64_t band_gen = ~0ull, band_seen_gen = ~0ull;
     uint64_t cand_tiles = 0;        // allocated tiles
+    uint64_t cand_live = 0;         // tiles of the current lists
     std::vector<unsigned char> cand_key;
     uint64_t cand_gen = 0;          // bumped whenever the lists are rebuilt
     // Cost-ordered tiles (TraceParams::tile_order): per-tile durations recorded by the
@@ -87,8 +87,10 @@ struct rt_ctx {
 };
 
 namespace {
-
 thread_local std::string g_last_error = "";
+}  // namespace
+
+namespace rti {
 
 rt_status fail(rt_status s, const std::string& msg) {
     g_last_error = msg;
@@ -99,21 +101,25 @@ rt_status hip_fail(hipError_t e, const char* what) {
     return fail(RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Switches to the context's device for the duration of a call.
-struct DeviceGuard {
-    int prev = -1;
-    bool ok = true;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
-
 constexpr uint32_t kMaxDim = 1u << 16;         // 65536 x 65536 texels
+
+rt_status check_image(uint32_t w, uint32_t h) {
+    if (w == 0 || h == 0 || w > kMaxDim || h > kMaxDim)
+        return fail(RT_ERR_INVALID_SIZE, "image size out of range (1..65536 per side)");
+    return RT_OK;
+}
+
+int ctx_device(const rt_ctx* ctx) { return ctx->device; }
+
+}  // namespace rti
+
+namespace {
+
+using rti::check_image;
+using rti::DeviceGuard;
+using rti::fail;
+using rti::hip_fail;
+
 constexpr uint32_t kMaxSpheres = 1u << 20;
 constexpr uint32_t kScanPad = 68;  // >= chunk round-up + one chunk + a 64-lane block
 
@@ -174,14 +180,16 @@ bool camera_rays_bounded(const rt_ctx* ctx, const rtk::TraceParams& p) {
 
 // Kernel instance for a launch (rtk::kTrace*): without bounce rays (max_depth <= 1) the
 // culled mode needs only the candidate lists; the camera-ray-only instance also requires
-// camera_rays_bounded (its fast cores).
+// camera_rays_bounded (its fast cores).  Bounce rays (max_depth >= 2) run the bounce
+// instance, whose path schedule (per wave by default, compacted or frame pairs) is
+// rt_set_path_compaction's.
 int trace_kernel_for(const rt_ctx* ctx, const rtk::TraceParams& p) {
     if (ctx->scan_mode == RT_SCAN_EXHAUSTIVE) return rtk::kTraceExhaustive;
 #ifndef RT_FORCE_CULLED_KERNEL
     if (p.depth <= 1u && camera_rays_bounded(ctx, p)) return rtk::kTraceList;
 #endif
 #ifndef RT_NO_BOUNCE_KERNEL
-    // bounce rays: paths compacted across the workgroup after every bounce
+    // bounce rays: the bounce instance (path schedule: TraceParams::compact)
     if (p.depth >= 2u) return rtk::kTraceBounce;
 #endif
     return rtk::kTraceCulled;
@@ -199,8 +207,9 @@ int single_or(const rt_ctx* ctx, const rtk::TraceParams& p, int kernel) {
     return tiles <= rtk::kSingleOneMaxTiles ? rtk::kTraceSingleOne : rtk::kTraceSingle;
 }
 
-// Frames per rt_update_frames launch (see rt_update_frames).  Only the camera-ray-only
-// instance has the per-frame stores (rt_kernels.hip, kStoreEach).
+// Frames per rt_update_frames launch (see rt_update_frames): the camera-ray-only and the
+// bounce instances fuse frames (both keep the accumulator in registers and store the last
+// two frames' images); the others run one frame per launch.
 uint32_t frames_per_launch_for(const rt_ctx* ctx, const rtk::TraceParams& p) {
     const int k = trace_kernel_for(ctx, p);
     const bool fusable = k == rtk::kTraceList || k == rtk::kTraceBounce;
@@ -208,12 +217,6 @@ uint32_t frames_per_launch_for(const rt_ctx* ctx, const rtk::TraceParams& p) {
     if (ctx->frames_per_launch)
         return std::min<uint32_t>(ctx->frames_per_launch, rtk::kMaxFramesPerLaunch);
     return rtk::kHintFrames;
-}
-
-rt_status check_image(uint32_t w, uint32_t h) {
-    if (w == 0 || h == 0 || w > kMaxDim || h > kMaxDim)
-        return fail(RT_ERR_INVALID_SIZE, "image size out of range (1..65536 per side)");
-    return RT_OK;
 }
 
 // Uniform XZ grid of the small spheres (rt_kernels.hip scan_grid), built on every scene
@@ -450,6 +453,7 @@ void free_candidates(rt_ctx* ctx) {
     (void)hipFree(ctx->cand);
     ctx->cand = nullptr;
     ctx->cand_tiles = 0;
+    ctx->cand_live = 0;
     ctx->cand_key.clear();
 }
 
@@ -499,6 +503,7 @@ rt_status ensure_candidates(rt_ctx* ctx, rtk::TraceParams& p, hipStream_t stream
         if (e != hipSuccess) return hip_fail(e, "rt_candidates_kernel launch");
         ctx->cand_key.assign(kb, kb + sizeof(key));
         ctx->cand_gen++;
+        ctx->cand_live = tiles;
     }
     p.cand = ctx->cand;
     return RT_OK;
@@ -564,23 +569,14 @@ rt_status plan_tile_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
     return RT_OK;
 }
 
-// Dispatch order of one-frame launches (rt_single_kernel): the workgroups (or whole rows)
-// of the current candidate generation by decreasing list load, costliest first (scheduling
-// only; rtk::launch_wg_order, rtk::launch_band_order).  Built on the second launch of a
-// generation.
-rt_status plan_band_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t stream) {
-    p.band_order = nullptr;
+// Dispatch order of one-frame launches (rt_single_kernel): the workgroups of the current
+// candidate generation by decreasing candidate-list load, costliest first (scheduling only;
+// rtk::launch_wg_order).  Built on the second launch of a generation (a camera that moves
+// every frame never pays for it); rt_set_tile_order(OFF) keeps raster order.
+rt_status plan_wg_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t stream) {
     p.wg_order = nullptr;
-    // RT_BAND_ORDER (measurements): 0 = top to bottom, 1 = whole bands by load, 2 (default)
-    // = workgroups by load
-    static const int mode = [] {
-        const char* e = std::getenv("RT_BAND_ORDER");
-        return e ? (int)std::strtol(e, nullptr, 10) : 2;
-    }();
-    const bool off = mode == 0;
-    if (off || (kernel != rtk::kTraceSingle && kernel != rtk::kTraceSingleOne) || p.cand_k == 0 ||
-        p.local_bands < 2 || p.local_bands > rtk::kBandOrderMax ||
-        ctx->tile_order_mode == RT_TILE_ORDER_OFF)
+    if ((kernel != rtk::kTraceSingle && kernel != rtk::kTraceSingleOne) || p.cand_k == 0 ||
+        p.local_bands < 2 || ctx->tile_order_mode == RT_TILE_ORDER_OFF)
         return RT_OK;
     const uint64_t gen = ctx->cand_gen;
     if (ctx->band_gen != gen) {
@@ -588,51 +584,30 @@ rt_status plan_band_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
             ctx->band_seen_gen = gen;
             return RT_OK;
         }
-        if (mode == 1 && p.local_bands > ctx->band_cap) {
-            if (ctx->band_cap) {
-                hipError_t e = hipStreamSynchronize(stream);   // old order may be in use
-                if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-            }
-            (void)hipFree(ctx->band_order);
-            ctx->band_order = nullptr;
-            ctx->band_cap = 0;
-            hipError_t e = hipMalloc(&ctx->band_order, rtk::kBandOrderMax * sizeof(uint32_t));
-            if (e != hipSuccess) return hip_fail(e, "hipMalloc(band order)");
-            ctx->band_cap = rtk::kBandOrderMax;
-        }
-        if (mode == 1) {
-            hipError_t e = rtk::launch_band_order(p.cand, (p.width + 7u) >> 3, p.local_bands,
-                                                  ctx->band_order, stream);
-            if (e != hipSuccess) return hip_fail(e, "rt_band_order_kernel launch");
-        }
         ctx->band_gen = gen;
         ctx->wg_pix = 0;
     }
-    if (mode == 2) {
-        const uint32_t pix = kernel == rtk::kTraceSingle ? rtk::single_pix() : 1u;
-        const uint32_t per = rtk::single_wg_tiles(pix);
-        const uint64_t units = (uint64_t)((((p.width + 7u) >> 3) + per - 1u) / per) * p.local_bands;
-        if (units > ctx->wg_cap) {
-            hipError_t e = hipStreamSynchronize(stream);
-            if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-            (void)hipFree(ctx->wg_buf);
-            ctx->wg_buf = nullptr;
-            ctx->wg_cap = 0;
-            e = hipMalloc(&ctx->wg_buf, (2 * units + 1) * sizeof(uint32_t));
-            if (e != hipSuccess) return hip_fail(e, "hipMalloc(workgroup order)");
-            ctx->wg_cap = units;
-            ctx->wg_pix = 0;
-        }
-        if (ctx->wg_pix != pix) {
-            hipError_t e = rtk::launch_wg_order(p.cand, (p.width + 7u) >> 3, p.local_bands, pix,
-                                                ctx->wg_buf, ctx->wg_buf + units, stream);
-            if (e != hipSuccess) return hip_fail(e, "workgroup order launch");
-            ctx->wg_pix = pix;
-        }
-        p.wg_order = ctx->wg_buf + units;
-        return RT_OK;
+    const uint32_t pix = kernel == rtk::kTraceSingle ? rtk::single_pix() : 1u;
+    const uint32_t per = rtk::single_wg_tiles(pix);
+    const uint64_t units = (uint64_t)((((p.width + 7u) >> 3) + per - 1u) / per) * p.local_bands;
+    if (units > ctx->wg_cap) {
+        hipError_t e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+        (void)hipFree(ctx->wg_buf);
+        ctx->wg_buf = nullptr;
+        ctx->wg_cap = 0;
+        e = hipMalloc(&ctx->wg_buf, (2 * units + 1) * sizeof(uint32_t));
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(workgroup order)");
+        ctx->wg_cap = units;
+        ctx->wg_pix = 0;
     }
-    p.band_order = ctx->band_order;
+    if (ctx->wg_pix != pix) {
+        hipError_t e = rtk::launch_wg_order(p.cand, (p.width + 7u) >> 3, p.local_bands, pix,
+                                            ctx->wg_buf, ctx->wg_buf + units, stream);
+        if (e != hipSuccess) return hip_fail(e, "workgroup order launch");
+        ctx->wg_pix = pix;
+    }
+    p.wg_order = ctx->wg_buf + units;
     return RT_OK;
 }
 
@@ -871,7 +846,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         plan_hint(ctx, p, src, dst);
         const int kernel = single_or(ctx, p, trace_kernel_for(ctx, p));
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
-        if (rt_status s = plan_band_order(ctx, p, kernel, stream)) return s;
+        if (rt_status s = plan_wg_order(ctx, p, kernel, stream)) return s;
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         finish_tile_order(ctx, p);
@@ -907,6 +882,33 @@ rt_status rt_last_launch_info(const rt_ctx* ctx, rt_launch_info* out) {
     return RT_OK;
 }
 
+rt_status rt_candidate_stats(rt_ctx* ctx, uint64_t out[5]) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!out) return fail(RT_ERR_INVALID_ARGUMENT, "out is NULL");
+    for (int i = 0; i < 5; ++i) out[i] = 0;
+    out[4] = rtk::kCandMax;
+    if (!ctx->cand || ctx->cand_live == 0) return RT_OK;
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    // the count is the first word of each tile's kCandStride-float4 block
+    std::vector<uint32_t> cnt(ctx->cand_live);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess)
+        e = hipMemcpy2D(cnt.data(), sizeof(uint32_t), ctx->cand, rtk::kCandStride * sizeof(float4),
+                        sizeof(uint32_t), cnt.size(), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy2D(candidate counts)");
+    out[0] = cnt.size();
+    for (uint32_t c : cnt) {
+        if (c == rtk::kCandNone) {
+            out[1]++;
+        } else {
+            out[2] += c;
+            out[3] = std::max<uint64_t>(out[3], c);
+        }
+    }
+    return RT_OK;
+}
+
 rt_status rt_create(int device, rt_ctx** out_ctx) {
     if (!out_ctx) return fail(RT_ERR_INVALID_ARGUMENT, "out_ctx is NULL");
     *out_ctx = nullptr;
@@ -933,7 +935,6 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->tile_cost);
         (void)hipFree(ctx->tile_order);
         (void)hipFree(ctx->d_grid);
-        (void)hipFree(ctx->band_order);
         (void)hipFree(ctx->wg_buf);
         free_candidates(ctx);
     }
@@ -1057,12 +1058,12 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
                               seeds, stream, p))
         return s;
     float4* img[2] = {reinterpret_cast<float4*>(image_a), reinterpret_cast<float4*>(image_b)};
-    // Frames per launch.  Fusing removes the per-launch fill, tail and kernel boundary
-    // (≈ 6 µs of a 30-µs K3 frame); it pays where frames are short, i.e. for the
-    // camera-ray-only kernel (max_depth <= 1: up to kHintFrames frames, the hint's
-    // reach).  Bounce kernels' frames are long (K5: 1.6 ms) and their per-tile cost
-    // uneven: one frame per launch.  rt_set_frames_per_launch overrides the count for the
-    // camera-ray-only kernel (1 = one dispatch per frame, the reference's structure).
+    // Frames per launch (frames_per_launch_for).  Fusing removes the per-launch fill, tail
+    // and kernel boundary (≈ 6 µs of a 30-µs K3 frame): the camera-ray-only instances
+    // (max_depth <= 1) and the bounce instance (max_depth >= 2) run up to kHintFrames
+    // frames per launch, the hint's reach; rt_set_frames_per_launch caps both (1 = one
+    // dispatch per frame, the reference's structure).  The exhaustive and general culled
+    // instances run one frame per launch.
     const uint32_t per = frames_per_launch_for(ctx, p);
     int cur = 0;
     ctx->last = {0, 0, 0, -1};
@@ -1102,7 +1103,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         }
         kernel = single_or(ctx, p, kernel);
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
-        if (rt_status s = plan_band_order(ctx, p, kernel, stream)) return s;
+        if (rt_status s = plan_wg_order(ctx, p, kernel, stream)) return s;
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         finish_tile_order(ctx, p);

@@ -55,11 +55,8 @@ struct TraceParams {
     uint32_t lds_records;  // culled scan: records staged in LDS (0 = read from HBM/L2)
     uint32_t cand_k;       // per-tile candidate list capacity (0 = no lists)
     const float4* cand;    // [tile][kCandStride] candidate blocks (see kCandStride)
-    // one-frame launches (rt_single_kernel): local bands in decreasing candidate-list load
-    // (launch_band_order), null = top to bottom
-    const uint32_t* band_order;
-    // one-frame launches: workgroup u traces (band << 16 | column group) wg_order[u]
-    // (launch_wg_order), null = band_order / natural order
+    // one-frame launches (rt_single_kernel): workgroup u traces (band << 16 | column group)
+    // wg_order[u] (launch_wg_order), null = natural order
     const uint32_t* wg_order;
     // Uniform XZ grid over the small spheres for bounce rays (rt_kernels.hip scan_grid;
     // built by rt_abi.cpp build_grid): per cell the range of its items, each item a copy
@@ -177,14 +174,9 @@ hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream);
 // Builds the per-tile candidate blocks for p's camera/scene/stripes (p.cand_k entries at
 // most per tile).
 hipError_t launch_candidates(const TraceParams& p, float4* cand, hipStream_t stream);
-// band_order for one-frame launches: the local bands by decreasing load of their tiles'
-// candidate lists (sum over tiles of 4 + count for tiles with a list entry, 64 for tiles
-// without a list), ties in band order.  At most kBandOrderMax bands.
-constexpr uint32_t kBandOrderMax = 1024;
-hipError_t launch_band_order(const float4* cand, uint32_t tiles_x, uint32_t bands,
-                             uint32_t* band_order, hipStream_t stream);
 // wg_order for one-frame launches of `pix` tiles per wave: the workgroups by decreasing
-// candidate-list load (the same per-tile load), sorted by launch_tile_order's buckets;
+// candidate-list load (per tile 4 + count for a tile with a list, 64 for a tile without
+// one), sorted by launch_tile_order's buckets;
 // wg_cost is scratch of one word per workgroup.
 hipError_t launch_wg_order(const float4* cand, uint32_t tiles_x, uint32_t bands, uint32_t pix,
                            uint32_t* wg_cost, uint32_t* wg_order, hipStream_t stream);

@@ -88,6 +88,41 @@ __device__ __forceinline__ void wave_trace(int end) {
 #define WAVE_TRACE(e) ((void)0)
 #endif
 
+// ---- diagnostic phase stamps of the one-frame kernel (RT_SSTAMPS=1 builds only) ------
+// Per wave of rt_single_kernel: s_memtime when each phase's result is available (the asm
+// consumes the value, so the stamp waits for it): 0 entry, 1 workgroup order resolved,
+// 2 seed tables + candidate counts arrived, 3 camera rays built, 4 list walk done, 5 hit
+// shading + sky done, 6 accumulator consumed, 7 stores issued; 8 / 9 s_memrealtime at entry
+// / end (100 MHz), 10 HW_ID, 11 XCC_ID.  tools/stamps_single.py reads them
+// (rt_diag_single_stamps).
+#ifndef RT_SSTAMPS
+#define RT_SSTAMPS 0
+#endif
+#if RT_SSTAMPS
+constexpr uint32_t kSStampWaves = 1u << 17;
+__device__ unsigned long long g_sst[kSStampWaves][12];
+__device__ __forceinline__ uint32_t sst_wave() {
+    return (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+}
+__device__ __forceinline__ void sst_put(int k, unsigned long long t) {
+    const uint32_t gw = sst_wave();
+    if ((threadIdx.x & 63u) == 0u && gw < kSStampWaves) g_sst[gw][k] = t;
+}
+#define SST_V(k, dep)                                        \
+    do {                                                     \
+        asm volatile("" ::"v"(dep));                         \
+        sst_put((k), __builtin_amdgcn_s_memtime());          \
+    } while (0)
+#define SST_S(k, dep)                                        \
+    do {                                                     \
+        asm volatile("" ::"s"(dep));                         \
+        sst_put((k), __builtin_amdgcn_s_memtime());          \
+    } while (0)
+#else
+#define SST_V(k, dep) ((void)0)
+#define SST_S(k, dep) ((void)0)
+#endif
+
 // Constant address space (read-only for the whole launch; eligible for scalar loads).
 // (The host pass of hipcc also parses device code; there the qualifier is dropped.)
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -195,9 +230,10 @@ __device__ __forceinline__ int max_bits(const float (&dd)[K]) {
 #endif
 template <int kScan>
 constexpr int scan_chunk() { return is_list_kernel(kScan) ? RT_LIST_CHUNK : RT_SCAN_CHUNK; }
-// Per-frame stores of fused launches (TraceParams::store_each) exist in the camera-ray-only
-// instance alone: the bounce instances would spill registers for them (rt_abi.cpp runs
-// their rt_update_frames one frame per launch).
+// Per-frame stores of fused launches (TraceParams::store_each) in rt_trace_kernel exist in
+// the camera-ray-only instances alone (the culled instance would spill registers for them
+// and runs one frame per launch); the bounce instance (rt_bounce_kernel) has its own
+// two-last-frames stores and fuses frames too (rt_abi.cpp frames_per_launch_for).
 template <int kScan>
 constexpr bool kStoreEach = is_list_kernel(kScan);
 // Exact fast division / sqrt cores (rt_device.h) in the camera-ray-only instances, which
@@ -1242,7 +1278,6 @@ struct SingleParams {
     uint32_t n_hint;       // every pixel's count before the frame (0 on reset)
     uint32_t seed_b;       // B = u32(random_seed * 2^32) (wgsl:311, 353)
     uint32_t hy_off;       // hash(y * 51) table offset in the hx buffer
-    const uint32_t* band_order;   // local band of blockIdx.y (null: blockIdx.y)
     double rcp_hint;       // RN64(1 / (n_hint + 1))
     float4 rs;             // (rf(sb), random_unit_vector(sb)) of frame 0, bounce 0
     double disk_rcp[8];
@@ -1384,6 +1419,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
         get_ray<true>(cam, tc[s].x, tc[s].y, hxy[s], seed[s] * 25u + p.seed_b, o[s], d[s]);
 #endif
     }
+    SST_V(3, d[S - 1].x);
     const uint32_t lane = threadIdx.x & 63u;
     if (kSingleLds<S>) {
         // (this wave's own LDS slots: written and read by this wave only, in order)
@@ -1448,6 +1484,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                 tmax[s] = h.t;
             }
         }
+        SST_V(4, tmax[S - 1]);
         // hit records and the scatter (wgsl:205-218, 268-286)
         bool hit[S];
         bool any = false;
@@ -1504,6 +1541,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
         const v3 c = sky_w(cf[s], dsky[s]);                       // wgsl:293-296
         col[s] = black[s] ? mk(0.0f, 0.0f, 0.0f) : c;             // wgsl:277-279
     }
+    SST_V(5, col[S - 1].x);
 }
 
 template <int kPix>
@@ -1515,21 +1553,23 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
     static_assert(kPix >= 1 && kPix <= 4, "1 to 4 tiles per wave");
     constexpr uint32_t S = kPix;
     WAVE_TRACE(0);
+#if RT_SSTAMPS
+    sst_put(8, __builtin_amdgcn_s_memrealtime());
+    sst_put(0, __builtin_amdgcn_s_memtime());
+#endif
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t tiles_x = (a_width + 7u) >> 3;
-    // bands by decreasing candidate-list load (launch_band_order): the costliest rows are
-    // dispatched first and the cheap ones fill the tail (rows stay whole, so the
-    // accumulator traffic keeps its locality); or workgroups by decreasing load (wg_order)
+    // workgroups by decreasing candidate-list load (wg_order, launch_wg_order): the
+    // costliest are dispatched first and the cheap ones fill the tail
     uint32_t gx = blockIdx.x, lband = blockIdx.y;
     if (a_order) {   // (a leading, preloadable argument: one scalar load to the entry)
         const uint32_t e = __builtin_amdgcn_readfirstlane(
             a_order[blockIdx.y * gridDim.x + blockIdx.x]);
         gx = e & 0xFFFFu;
         lband = e >> 16;
-    } else if (p.band_order) {
-        lband = __builtin_amdgcn_readfirstlane(p.band_order[blockIdx.y]);
     }
+    SST_S(1, lband);
     const uint32_t tx0 = (gx * kSingleWg + wave) * S;
     const uint32_t band_first = a_bands & 0xFFFFu, band_step = (a_bands >> 16) & 0x7FFFu;
     TileCoord tc[S];
@@ -1573,6 +1613,8 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
         __syncthreads();
     }
     if (tx0 >= tiles_x) return;
+    SST_V(2, hxy[S - 1]);
+    SST_S(2, ncand[S - 1]);
 
     Cam cam;
     cam.center = mk(p.center[0], p.center[1], p.center[2]);
@@ -1651,6 +1693,7 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
                 n[s] += 1u;
             }
     }
+    SST_V(6, c[S - 1].x);
 #if RT_SKO & 16
     // every result stays live; the per-lane store happens only if a never-true runtime
     // condition holds (no image traffic, all compute kept)
@@ -1678,6 +1721,12 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
     for (uint32_t s = 0; s < S; ++s)
         if (tc[s].valid)                                          // wgsl:362-363
             p.out[tc[s].idx] = make_float4(c[s].x, c[s].y, c[s].z, (float)n[s]);
+#endif
+#if RT_SSTAMPS
+    sst_put(7, __builtin_amdgcn_s_memtime());
+    sst_put(9, __builtin_amdgcn_s_memrealtime());
+    sst_put(10, __builtin_amdgcn_s_getreg((31 << 11) | 4));    // HW_ID
+    sst_put(11, __builtin_amdgcn_s_getreg((31 << 11) | 20));   // XCC_ID
 #endif
     WAVE_TRACE(1);
 }
@@ -2061,39 +2110,8 @@ hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, ui
     return hipGetLastError();
 }
 
-// launch_band_order: one 1024-thread workgroup.  Each wave sums its bands' tile loads (lane
-// per tile column, a DPP reduction), then every thread ranks its bands against all others
-// (LDS broadcast reads): rank = bands with a larger load, or an equal load and a lower
-// index.  Scheduling only: which band a workgroup row traces, never what it computes.
-__global__ __launch_bounds__(1024) void rt_band_order_kernel(const float4* __restrict__ cand,
-                                                             uint32_t tiles_x, uint32_t bands,
-                                                             uint32_t* __restrict__ order) {
-    __shared__ uint32_t s_load[kBandOrderMax];
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    for (uint32_t b = wave; b < bands; b += 16u) {
-        uint32_t sum = 0u;
-        for (uint32_t tx = lane; tx < tiles_x; tx += 64u) {
-            const uint32_t c = load_cnt(cand, b * tiles_x + tx);
-            sum += c == kCandNone ? 64u : (c ? 4u + c : 0u);
-        }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
-        if (lane == 0u) s_load[b] = sum;
-    }
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < bands; b += 1024u) {
-        const uint32_t mine = s_load[b];
-        uint32_t rank = 0u;
-        for (uint32_t o = 0; o < bands; ++o) {
-            const uint32_t v = s_load[o];
-            rank += (v > mine || (v == mine && o < b)) ? 1u : 0u;
-        }
-        order[rank] = b;
-    }
-}
-
 // Per-workgroup candidate-list load of one-frame launches (wg_order's sort key): the sum of
-// its `per` tiles' loads, as rt_band_order_kernel weighs them.
+// its `per` tiles' loads (4 + count for a tile with a list, 64 for a tile without one).
 __global__ __launch_bounds__(256) void rt_wg_cost_kernel(const float4* __restrict__ cand,
                                                          uint32_t tiles_x, uint32_t cols,
                                                          uint32_t per, uint32_t units,
@@ -2451,7 +2469,6 @@ static void launch_single(const TraceParams& p, hipStream_t stream) {
     q.n_hint = p.hint_n[0];
     q.seed_b = p.seed_b[0];
     q.hy_off = (uint32_t)(p.hy - p.hx);
-    q.band_order = p.band_order;
     q.rcp_hint = p.hint_rcp[0];
     q.rs = p.hint_rs[0];
     for (int k = 0; k < 8; ++k) q.disk_rcp[k] = p.disk_rcp[k];
@@ -2497,14 +2514,6 @@ hipError_t launch_candidates(const TraceParams& p, float4* cand, hipStream_t str
                     (p.local_bands + kCandBY - 1u) / kCandBY);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
     hipLaunchKernelGGL(rt_candidates_kernel, grid, dim3(64), 0, stream, p, cand);
-    return hipGetLastError();
-}
-
-hipError_t launch_band_order(const float4* cand, uint32_t tiles_x, uint32_t bands,
-                             uint32_t* band_order, hipStream_t stream) {
-    if (bands == 0 || bands > kBandOrderMax) return hipSuccess;
-    hipLaunchKernelGGL(rt_band_order_kernel, dim3(1), dim3(1024), 0, stream, cand, tiles_x,
-                       bands, band_order);
     return hipGetLastError();
 }
 
@@ -2581,6 +2590,22 @@ extern "C" __attribute__((visibility("default"))) int rt_diag_stamps(unsigned lo
     for (int i = 0; i < 8; ++i) out[i] = 0;
     for (unsigned wv = 0; wv < waves; ++wv)
         for (int i = 1; i < 8; ++i) out[i] += host[wv][i];
+    return 0;
+}
+#endif
+
+#if RT_SSTAMPS
+// Diagnostic builds: copies the one-frame kernel's per-wave stamps (12 words each, see
+// RT_SSTAMPS) of the first n waves of the last launch to out[12 n] and clears them.
+extern "C" __attribute__((visibility("default"))) int rt_diag_single_stamps(
+    unsigned long long* out, unsigned n) {
+    if (n > rtk::kSStampWaves) n = rtk::kSStampWaves;
+    static unsigned long long t[rtk::kSStampWaves][12];
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    if (hipMemcpyFromSymbol(t, HIP_SYMBOL(rtk::g_sst), sizeof(t)) != hipSuccess) return 1;
+    std::memcpy(out, t, (size_t)n * 12 * sizeof(unsigned long long));
+    std::memset(t, 0, sizeof(t));
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rtk::g_sst), t, sizeof(t)) != hipSuccess) return 1;
     return 0;
 }
 #endif

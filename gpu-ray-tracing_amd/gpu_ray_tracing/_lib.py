@@ -40,7 +40,9 @@ STATUS_NAMES = {
     4: "RT_ERR_HIP",
     5: "RT_ERR_NO_MEMORY",
     6: "RT_ERR_INVALID_CONTEXT",
+    7: "RT_ERR_COMM",
 }
+RT_COMM_ID_BYTES = 128
 RT_STRIPE_ROWS = 8
 RT_SCAN_EXHAUSTIVE = 0
 RT_SCAN_CULLED = 1
@@ -120,6 +122,16 @@ _SIGS = {
     "rt_last_launch_info": (ctypes.c_int, [P, P]),
     "rt_set_path_compaction": (ctypes.c_int, [P, ctypes.c_int]),
     "rt_set_single_kernel": (ctypes.c_int, [P, ctypes.c_int]),
+    "rt_candidate_stats": (ctypes.c_int, [P, P]),
+    "rt_comm_unique_id": (ctypes.c_int, [P]),
+    "rt_comm_create": (ctypes.c_int, [P, P, U32, U32, ctypes.POINTER(P)]),
+    "rt_comm_create_all": (ctypes.c_int, [U32, P, P]),
+    "rt_comm_destroy": (ctypes.c_int, [P]),
+    "rt_comm_info": (ctypes.c_int, [P, ctypes.POINTER(U32), ctypes.POINTER(U32),
+                                    ctypes.POINTER(ctypes.c_int)]),
+    "rt_comm_group_start": (ctypes.c_int, []),
+    "rt_comm_group_end": (ctypes.c_int, []),
+    "rt_gather_stripes": (ctypes.c_int, [P, P, P, P, P, U32, U32, U32, P]),
 }
 
 

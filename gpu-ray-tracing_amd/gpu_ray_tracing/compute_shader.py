@@ -109,6 +109,17 @@ class ComputeShaderPipeline:
         d["kernel_name"] = _lib.lib().rt_kernel_name(d["kernel"]).decode()
         return d
 
+    def candidate_stats(self) -> dict:
+        """rt_candidate_stats: the camera rays' per-tile candidate lists built last."""
+        out = (ctypes.c_uint64 * 5)()
+        _lib.call("rt_candidate_stats", self._ctx, out)
+        t, none, entries, mx, cap = (int(v) for v in out)
+        listed = t - none
+        return {"tiles": t, "tiles_without_list": none,
+                "no_list_frac": round(none / t, 6) if t else 0.0,
+                "mean_entries": round(entries / listed, 3) if listed else 0.0,
+                "max_entries": mx, "capacity": cap}
+
     def selftest_fastmath(self, n_random: int = 1 << 26) -> list[int]:
         """rt_selftest_fastmath: [defocus, division, sqrt, root-selection mismatches,
         cases run]."""

@@ -5,14 +5,89 @@ pixel coordinate, so the image shards with no data-path exchange.  Bands of
 RT_STRIPE_ROWS rows are dealt round-robin (band b -> rank b % world), which balances the
 sky/ground cost between ranks.  Each rank renders its bands into a compact local buffer
 (rt_render_stripes); the only collective is ONE gather of the finished tiles to rank 0
-(RCCL over xGMI), followed by the de-interleave kernel on the root.
+(RCCL over xGMI), followed by the de-interleave kernel on the root.  The gather runs either
+behind the C ABI (StripeComm: rt_comm_* + rt_gather_stripes, ncclGather inside
+librt_hip.so — what a non-Python host binds) or through torch.distributed (gather_stripes).
 """
 from __future__ import annotations
+
+import ctypes
 
 import torch
 import torch.distributed as dist
 
-from .compute_shader import ComputeShaderPipeline, stripe_local_rows
+from . import _lib
+from .compute_shader import ComputeShaderPipeline, _check_image, stripe_local_rows
+
+
+class StripeComm:
+    """An RCCL communicator of librt_hip.so (rt_comm_create) on a pipeline's device: the
+    stripe gather behind the C ABI (rt_gather_stripes = one ncclGather + the root's
+    de-interleave)."""
+
+    def __init__(self, pipeline: ComputeShaderPipeline, uid: bytes, nranks: int, rank: int):
+        if len(uid) != _lib.RT_COMM_ID_BYTES:
+            raise ValueError(f"unique id must be {_lib.RT_COMM_ID_BYTES} bytes")
+        self.pipe = pipeline
+        buf = (ctypes.c_uint8 * _lib.RT_COMM_ID_BYTES).from_buffer_copy(uid)
+        comm = ctypes.c_void_p()
+        _lib.call("rt_comm_create", pipeline._ctx, buf, nranks, rank, ctypes.byref(comm))
+        self._comm = comm
+        self.rank, self.nranks, self.device = self.info()
+
+    @staticmethod
+    def unique_id() -> bytes:
+        """rt_comm_unique_id (ncclGetUniqueId): call on one rank, share with all."""
+        buf = (ctypes.c_uint8 * _lib.RT_COMM_ID_BYTES)()
+        _lib.call("rt_comm_unique_id", buf)
+        return bytes(buf)
+
+    @classmethod
+    def from_process_group(cls, pipeline: ComputeShaderPipeline, group=None, src: int = 0):
+        """Every rank of an initialised torch.distributed group calls this together: `src`
+        draws the unique id, it is broadcast over the group, and each rank creates its
+        communicator (rank and size as in the group)."""
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        box = [cls.unique_id() if rank == src else None]
+        dist.broadcast_object_list(box, src=src, group=group)
+        return cls(pipeline, box[0], world, rank)
+
+    def info(self) -> tuple[int, int, int]:
+        r, n, d = _lib.U32(0), _lib.U32(0), ctypes.c_int(-1)
+        _lib.call("rt_comm_info", self._comm, ctypes.byref(r), ctypes.byref(n), ctypes.byref(d))
+        return int(r.value), int(n.value), int(d.value)
+
+    def gather(self, local: torch.Tensor, width: int, height: int, root: int = 0,
+               gathered: torch.Tensor | None = None,
+               out: torch.Tensor | None = None) -> torch.Tensor | None:
+        """rt_gather_stripes on the current stream: the full image on `root` (into `out`
+        when given), None elsewhere."""
+        rows0 = stripe_local_rows(height, 0, self.nranks)
+        _check_image(local, width, rows0, "local")
+        gptr = outp = None
+        if self.rank == root:
+            if out is None:
+                out = torch.empty((height, width, 4), dtype=torch.float32, device=local.device)
+            _check_image(out, width, height, "out")
+            outp = ctypes.c_void_p(out.data_ptr())
+            if gathered is not None:
+                _check_image(gathered, width, rows0 * self.nranks, "gathered")
+                gptr = ctypes.c_void_p(gathered.data_ptr())
+        _lib.call("rt_gather_stripes", self.pipe._ctx, self._comm,
+                  ctypes.c_void_p(local.data_ptr()), gptr, outp, width, height, root,
+                  self.pipe._stream())
+        return out if self.rank == root else None
+
+    def close(self) -> None:
+        if getattr(self, "_comm", None) and self._comm.value:
+            _lib.call("rt_comm_destroy", self._comm)
+            self._comm = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def padded_rows(height: int, world: int) -> int:
@@ -51,9 +126,14 @@ class StripeRenderer:
     """One rank's share of a width x height progressive render."""
 
     def __init__(self, pipeline: ComputeShaderPipeline, width: int, height: int, rank: int,
-                 world: int):
+                 world: int, comm: StripeComm | None = None):
+        """comm: gather through the C ABI's RCCL communicator (rt_gather_stripes) instead
+        of torch.distributed."""
+        if comm is not None and (comm.rank, comm.nranks) != (rank, world):
+            raise ValueError("the communicator's rank/size differ from the renderer's")
         self.pipe, self.width, self.height = pipeline, width, height
         self.rank, self.world = rank, world
+        self.comm = comm
         self.rows = stripe_local_rows(height, rank, world)
         self.rows0 = padded_rows(height, world)
         # ping-pong local accumulators, padded to rows0 so the gather is uniform
@@ -97,6 +177,13 @@ class StripeRenderer:
 
     def finish(self, dst: int = 0, group=None) -> torch.Tensor | None:
         """Gather the finished tiles; returns the full image on `dst`, None elsewhere."""
+        if self.comm is not None:
+            if group is not None:
+                raise ValueError("a renderer with a communicator gathers over it, not a group")
+            pre = dst == 0 and self._gathered is not None
+            return self.comm.gather(self.local, self.width, self.height, dst,
+                                    gathered=self._gathered.reshape(-1, self.width, 4) if pre else None,
+                                    out=self._image if pre else None)
         if self.world == 1:
             return self.local[: self.height]
         pre = dst == 0 and self._gathered is not None

@@ -146,7 +146,8 @@ typedef enum rt_status {
     RT_ERR_INVALID_DEVICE = 3,   /* device ordinal does not exist */
     RT_ERR_HIP = 4,              /* a HIP runtime call failed (rt_last_error has text) */
     RT_ERR_NO_MEMORY = 5,
-    RT_ERR_INVALID_CONTEXT = 6
+    RT_ERR_INVALID_CONTEXT = 6,
+    RT_ERR_COMM = 7              /* an RCCL call failed (rt_last_error has RCCL's text) */
 } rt_status;
 
 /* One context per device; calls on one ctx are externally serialized.  A context keeps
@@ -193,6 +194,14 @@ typedef struct rt_launch_info {
     int32_t kernel;
 } rt_launch_info;
 RT_API rt_status rt_last_launch_info(const rt_ctx* ctx, rt_launch_info* out);
+/* Diagnostic: the per-tile candidate lists of camera rays the context built last (culled
+ * scan; rebuilt when the camera geometry, image, stripe map or scene change).  A tile lists
+ * every sphere its camera rays can hit, at most 19 (rt_kernels.h kCandMax); a tile whose
+ * cone admits more, or is degenerate, has no list and its camera rays scan the whole scene
+ * with the per-wave culling (same pixels, slower).  out[0] = tiles, out[1] = tiles without a
+ * list, out[2] = entries over the listed tiles, out[3] = the longest list, out[4] = the list
+ * capacity.  Synchronous (reads the counts back); all zero before any list was built. */
+RT_API rt_status rt_candidate_stats(rt_ctx* ctx, uint64_t out[5]);
 
 /* Context ---------------------------------------------------------------------------- */
 /* Create a context on HIP device `device`.  Replaces ComputeShaderPipeline::from_world
@@ -226,7 +235,10 @@ RT_API rt_status rt_init_image(rt_ctx* ctx, float* out_rgba, uint32_t width, uin
 
 /* `update` (wgsl:333-364; dispatched every frame, lib.rs:408-417): one progressive sample
  * per pixel.  in_rgba and out_rgba are device images (must not alias: the reference
- * ping-pongs two textures, lib.rs:218-227).  spheres/count/camera are host pointers. */
+ * ping-pongs two textures, lib.rs:218-227).  spheres/count/camera are host pointers.
+ * in_rgba must be a valid, fully mapped width x height image even when the camera resets
+ * the accumulator (camera_has_moved > 0.5): the kernels load it before they know the
+ * reset and then discard the values (the same holds for every call's input images). */
 RT_API rt_status rt_update(rt_ctx* ctx, const float* in_rgba, float* out_rgba, uint32_t width,
                     uint32_t height, const rt_scene_camera* camera,
                     const rt_sphere* spheres, uint32_t sphere_count, void* stream);
@@ -249,13 +261,16 @@ RT_API rt_status rt_render(rt_ctx* ctx, const float* in_rgba, float* out_rgba, u
  * for rt_render_stripes).  *out_newest receives 0 if image_a holds the result, 1 for
  * image_b.  Afterwards BOTH images hold exactly what `frames` chained rt_update calls leave
  * (the newest frame and the one before).  Frames run in launches of
- * rt_set_frames_per_launch frames (default: 64 at max_depth <= 1, else 1); within a
- * launch each wave carries its pixels' accumulator in registers from frame to frame and
- * writes the images of the launch's last two frames (the earlier ones would be overwritten
- * unread).  No per-frame host round trip. */
-/* Frames rt_update_frames runs per launch at max_depth <= 1: 0 = automatic (up to 64),
- * 1 = one `update` dispatch per frame, exactly the reference's dispatch structure, n = up
- * to n (at most 128).  Launches with bounce rays always run one frame each. */
+ * rt_set_frames_per_launch frames (default 64) in the culled scan mode — camera rays only
+ * (max_depth <= 1, the camera-ray-only instances) and bounce rays (max_depth >= 2, the
+ * bounce instance) alike; within a launch each wave carries its pixels' accumulator in
+ * registers from frame to frame and writes the images of the launch's last two frames (the
+ * earlier ones would be overwritten unread).  The exhaustive scan mode, and cameras or
+ * scenes outside the fast instances' proven domain at max_depth <= 1, run one frame per
+ * launch.  No per-frame host round trip. */
+/* Frames rt_update_frames runs per fused launch (see above): 0 = automatic (64), 1 = one
+ * `update` dispatch per frame, exactly the reference's dispatch structure, n = up to n (at
+ * most 128).  The cap applies to the camera-ray-only and the bounce launches. */
 RT_API rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launch);
 /* rt_update_frames at max_depth <= 1 traces with several waves per 8x8 tile, each taking
  * a different frame of each group of frames (the others hand their colours to wave 0,
@@ -329,6 +344,41 @@ RT_API uint32_t rt_stripe_local_rows(uint32_t height, uint32_t rank, uint32_t nr
 RT_API rt_status rt_deinterleave_stripes(rt_ctx* ctx, const float* gathered, float* out_rgba,
                                   uint32_t width, uint32_t height, uint32_t nranks,
                                   void* stream);
+
+/* The multi-GPU collective: ONE RCCL gather over xGMI of every rank's
+ * finished stripe bands to the root, then the de-interleave there.  The reference renders
+ * on one device (ComputeShaderNode::run, lib.rs:379-421, one dispatch per frame); these
+ * calls are what a host driving one context per GPU adds around rt_update_frames /
+ * rt_render_stripes.  A communicator spans nranks ranks, one GPU each:
+ *   - one process per GPU: rank 0 calls rt_comm_unique_id, sends the RT_COMM_ID_BYTES bytes
+ *     to every rank by any means, and every rank calls rt_comm_create with them
+ *     (ncclGetUniqueId + ncclCommInitRank, rccl.h:187, 220; collective: all ranks must call
+ *     it concurrently);
+ *   - one process driving several GPUs: rt_comm_create_all (ncclCommInitAll, rccl.h:236),
+ *     with rt_comm_group_start / rt_comm_group_end around the per-device gathers.
+ * RCCL's own error text is returned through rt_last_error with RT_ERR_COMM. */
+#define RT_COMM_ID_BYTES 128
+typedef struct rt_comm rt_comm;
+RT_API rt_status rt_comm_unique_id(uint8_t out_id[RT_COMM_ID_BYTES]);
+/* A communicator on ctx's device (the rank's GPU). */
+RT_API rt_status rt_comm_create(rt_ctx* ctx, const uint8_t id[RT_COMM_ID_BYTES], uint32_t nranks,
+                                uint32_t rank, rt_comm** out_comm);
+/* ndev communicators, out_comms[i] on device devices[i] with rank i. */
+RT_API rt_status rt_comm_create_all(uint32_t ndev, const int* devices, rt_comm** out_comms);
+RT_API rt_status rt_comm_destroy(rt_comm* comm);
+RT_API rt_status rt_comm_info(const rt_comm* comm, uint32_t* out_rank, uint32_t* out_nranks,
+                              int* out_device);
+RT_API rt_status rt_comm_group_start(void);
+RT_API rt_status rt_comm_group_end(void);
+/* Gathers the rank's compact local image `local` (width x rt_stripe_local_rows(height, 0,
+ * nranks) rows — every rank's buffer padded to the root's row count) into `gathered` on
+ * the root (nranks such buffers back to back, rank order; NULL = a buffer the communicator
+ * keeps) with one ncclGather (rccl.h:745) on `stream`, then de-interleaves it into the
+ * width x height image `out_rgba` on the root (rt_deinterleave_stripes).  Non-root ranks
+ * ignore `gathered` and `out_rgba`.  ctx must be on the communicator's device. */
+RT_API rt_status rt_gather_stripes(rt_ctx* ctx, rt_comm* comm, const float* local,
+                                   float* gathered, float* out_rgba, uint32_t width,
+                                   uint32_t height, uint32_t root, void* stream);
 
 /* Presentation (replaces the sprite of lib.rs:79-102, which shows the newest
  * Rgba32Float image on the window): quantizes the accumulator's mean colour to 8-bit RGBA

@@ -237,3 +237,98 @@ def test_stripe_renderer_hip_multiprocess(world, w, h, dst):
             if p.is_alive():
                 p.terminate()
                 p.join(timeout=10)
+
+
+def _abi_gather_check(pipe, comm, w, h, q=None):
+    """Render through a StripeRenderer that gathers with `comm` (rt_gather_stripes) and
+    compare the root's image with the oracle's."""
+    import gpu_ray_tracing as rt
+    from gpu_ray_tracing.distributed import StripeRenderer
+    from oracle import oracle as O
+    sc = rt.create_default_spheres(seed=7)
+    seeds = rt.frame_seeds(21, 4)
+    moved = rt.SceneCamera.from_settings(
+        rt.CameraSettings(max_depth=3, samples_per_pixel=500), w, h, float(seeds[0]))
+    still = moved.with_fields(camera_has_moved=0.0)
+    r = StripeRenderer(pipe, w, h, comm.rank, comm.nranks, comm=comm)
+    r.frame(moved, sc, seeds[:1])
+    r.frames(still, sc, seeds[1:4])
+    img = r.finish()
+    full, _ = O.render(np.zeros((h, w, 4), np.float32), moved.blob, sc.spheres, seeds[:1])
+    full, _ = O.render(full, still.blob, sc.spheres, seeds[1:4])
+    got = img.cpu().numpy()
+    return got.shape == (h, w, 4) and np.array_equal(got.view(np.uint32), full.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h", [(40, 32), (33, 21)])
+def test_gather_stripes_abi_single_rank(rt, w, h):
+    """The RCCL gather behind the C ABI on one GPU: a one-rank communicator from
+    rt_comm_unique_id + rt_comm_create, and one from rt_comm_create_all; StripeRenderer's
+    finish() runs rt_gather_stripes (ncclGather + the de-interleave kernel) and must return
+    the oracle's image bit for bit; a caller-provided gather buffer gives the same image."""
+    import ctypes
+    from gpu_ray_tracing.distributed import StripeComm
+    pipe = rt.ComputeShaderPipeline(0)
+    comm = StripeComm(pipe, StripeComm.unique_id(), 1, 0)
+    assert (comm.rank, comm.nranks, comm.device) == (0, 1, 0)
+    assert _abi_gather_check(pipe, comm, w, h)
+    # explicit gather buffer, and ncclCommInitAll over the one device
+    local = torch.rand((rt.stripe_local_rows(h, 0, 1), w, 4), device="cuda")
+    gathered = torch.empty_like(local)
+    img = comm.gather(local, w, h, gathered=gathered)
+    torch.cuda.synchronize()
+    assert torch.equal(img, local[:h]) and torch.equal(gathered, local)
+    comm.close()
+    L = rt._lib.lib()
+    arr = (ctypes.c_void_p * 1)()
+    rt._lib.call("rt_comm_create_all", 1, (ctypes.c_int * 1)(0), arr)
+    comm2 = StripeComm.__new__(StripeComm)
+    comm2.pipe, comm2._comm = pipe, ctypes.c_void_p(arr[0])
+    comm2.rank, comm2.nranks, comm2.device = comm2.info()
+    assert (comm2.rank, comm2.nranks) == (0, 1)
+    assert _abi_gather_check(pipe, comm2, w, h)
+    # error paths on the device: root out of range, missing output on the root
+    assert L.rt_gather_stripes(pipe._ctx, comm2._comm, ctypes.c_void_p(local.data_ptr()),
+                               None, None, w, h, 1, None) == 1
+    assert L.rt_gather_stripes(pipe._ctx, comm2._comm, ctypes.c_void_p(local.data_ptr()),
+                               None, None, w, h, 0, None) == 1
+    comm2.close()
+    pipe.close()
+
+
+def _nccl_group_worker(port, w, h, q):
+    sys.path[:0] = [str(PKG_DIR), str(ROOT)]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        import gpu_ray_tracing as rt
+        from gpu_ray_tracing.distributed import StripeComm
+        pipe = rt.ComputeShaderPipeline(0)
+        comm = StripeComm.from_process_group(pipe)
+        q.put(bool(_abi_gather_check(pipe, comm, w, h)))
+        torch.cuda.synchronize()
+        comm.close()
+        pipe.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_stripe_comm_from_nccl_process_group():
+    """bench.py's setup of the C-ABI gather: the unique id drawn on rank 0 and broadcast over
+    an RCCL (nccl backend) process group, then rt_comm_create beside torch's own
+    communicator (one rank: RCCL refuses two ranks on one device)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_group_worker, args=(_free_port(), 24, 16, q))
+    p.start()
+    try:
+        p.join(timeout=180)
+        assert p.exitcode == 0
+        assert q.get(timeout=5) is True
+    finally:
+        if p.is_alive():
+            p.terminate()
+            p.join(timeout=10)

@@ -187,7 +187,8 @@ def test_bench_dispatch_chain_matches_fixture(rt, cfg, single):
 
 def test_bench_k5_launches_match_golden(rt):
     """bench.py --config K5's timed structure on one GPU: rt_update_frames of 64 frames
-    (bounce instance, one launch per frame) at 3840x2160, depth 8, sampled pixels."""
+    (the bounce instance, all 64 fused in one launch) at 3840x2160, depth 8, sampled
+    pixels."""
     g = load_golden("k5.npz")
     w, h = int(g["width"]), int(g["height"])
     p = rt.ComputeShaderPipeline(0)
@@ -524,6 +525,11 @@ def test_candidate_list_overflow_falls_back(rt, depth):
         img = p.new_image(w, h)
         p.render(img, img, w, h, cam, sc, rt.frame_seeds(3, 2))
         out[mode] = host(img)
+        if mode == "culled":
+            st = p.candidate_stats()
+            # the cluster fills the middle tiles: more spheres than a list holds
+            assert st["tiles"] == 64 and st["tiles_without_list"] > 0
+            assert st["capacity"] == 19 and st["max_entries"] <= 19
         p.close()
     assert_same(out["culled"], out["exhaustive"])
 
@@ -578,15 +584,10 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, s
         assert_same(got_prev, want_prev)
 
 
-@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "auto"])
-@pytest.mark.parametrize("w,h,depth,frames,scene,nranks", [
-    (56, 40, 2, 5, "n120", 1), (67, 45, 8, 3, "default", 1), (64, 48, 3, 1, "n120", 1),
-    (50, 37, 8, 6, "default", 3), (40, 32, 0, 2, "n120", 1), (72, 48, 5, 4, "three", 2)])
-def test_bounce_launches_match_oracle(rt, oracle, paths, w, h, depth, frames, scene, nranks):
-    """The bounce instance (max_depth >= 2, frames fused per launch, 4-tile workgroups),
-    with live paths compacted across the workgroup after every bounce or kept per wave:
-    both ping-pong buffers equal the oracle's chained updates (the newest frame and the one
-    before), whole image and stripe ranks, ragged edges included."""
+BOUNCE_PATH_KERNEL = {"per_wave": 0, "compact": 1, "pair": 2, "auto": 0}
+
+
+def _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks, fpl):
     sc = {"n120": rt.synthetic_scene(120), "default": rt.create_default_spheres(seed=3),
           "three": rt.three_spheres()}[scene]
     seeds = rt.frame_seeds(33, frames)
@@ -598,6 +599,8 @@ def test_bounce_launches_match_oracle(rt, oracle, paths, w, h, depth, frames, sc
                                         yy.ravel(), cam.blob, sc.spheres, seeds[:frames - 1])
     p = rt.ComputeShaderPipeline(0)
     p.set_path_compaction(paths)
+    if fpl:
+        p.set_frames_per_launch(fpl)
     rows0 = rt.stripe_local_rows(h, 0, nranks)
     got_new = np.zeros((h, w, 4), np.float32)
     got_prev = np.zeros((h, w, 4), np.float32)
@@ -607,8 +610,9 @@ def test_bounce_launches_match_oracle(rt, oracle, paths, w, h, depth, frames, sc
             newest = p.update_frames(a, b, w, h, cam, sc, seeds, r, nranks)
             info = p.last_launch_info()
             if depth >= 2:
-                assert info["kernel_name"] == "rt_bounce_kernel<%d>" % {
-                    "per_wave": 0, "compact": 1, "pair": 2, "auto": 0}[paths]
+                assert info["kernel_name"] == "rt_bounce_kernel<%d>" % BOUNCE_PATH_KERNEL[paths]
+                if fpl and rt.stripe_local_rows(h, r, nranks):
+                    assert info["launches"] == -(-frames // fpl)
             img_new, img_prev = (host(a), host(b)) if newest == 0 else (host(b), host(a))
             for lr in range(rt.stripe_local_rows(h, r, nranks)):
                 y = (r + (lr // 8) * nranks) * 8 + lr % 8
@@ -619,6 +623,29 @@ def test_bounce_launches_match_oracle(rt, oracle, paths, w, h, depth, frames, sc
     assert_same(got_new, want_new.reshape(h, w, 4))
     if frames >= 2:
         assert_same(got_prev, want_prev.reshape(h, w, 4))
+
+
+@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "auto"])
+@pytest.mark.parametrize("w,h,depth,frames,scene,nranks", [
+    (56, 40, 2, 5, "n120", 1), (67, 45, 8, 3, "default", 1), (64, 48, 3, 1, "n120", 1),
+    (50, 37, 8, 6, "default", 3), (40, 32, 0, 2, "n120", 1), (72, 48, 5, 4, "three", 2)])
+def test_bounce_launches_match_oracle(rt, oracle, paths, w, h, depth, frames, scene, nranks):
+    """The bounce instance (max_depth >= 2, frames fused per launch, 4-tile workgroups),
+    with live paths compacted across the workgroup after every bounce or kept per wave:
+    both ping-pong buffers equal the oracle's chained updates (the newest frame and the one
+    before), whole image and stripe ranks, ragged edges included."""
+    _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks, 0)
+
+
+@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair"])
+@pytest.mark.parametrize("w,h,depth,frames,scene,nranks", [
+    (56, 40, 2, 5, "n120", 1), (50, 37, 8, 6, "default", 3), (72, 48, 5, 4, "three", 2)])
+def test_bounce_launches_in_tile_order(rt, oracle, paths, w, h, depth, frames, scene, nranks):
+    """Two frames per launch (rt_set_frames_per_launch(2)): the first launch records the
+    per-tile (compact mode: per-workgroup) costs, every later launch runs the measured
+    cost order (tile_order) — both ping-pong buffers still equal the oracle's chain, in
+    every path mode."""
+    _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks, 2)
 
 
 def test_accumulator_written_outside_the_library(rt, oracle, pipe):

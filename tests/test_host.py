@@ -21,7 +21,7 @@ def header_functions():
 
 def test_library_exports_every_declared_symbol(rt):
     declared = header_functions()
-    assert len(declared) == 32
+    assert len(declared) == 41
     nm = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True,
                         text=True, check=True).stdout
     exported = set(re.findall(r" T (rt_\w+)$", nm, flags=re.M))
@@ -156,6 +156,22 @@ def test_argument_errors_without_device(rt):
     assert L.rt_kernel_name(8).decode() == "rt_single_kernel<2>"
     assert L.rt_kernel_name(9).decode() == "rt_single_kernel<1>"
     assert L.rt_kernel_name(99).decode() == "rt_trace_kernel"
+    # the RCCL gather behind the ABI (rt_comm.cpp)
+    assert L.rt_comm_unique_id(None) == 1
+    assert L.rt_comm_create(None, None, 1, 0, None) == 6
+    assert L.rt_comm_create_all(0, None, None) == 1
+    assert L.rt_comm_destroy(None) == 1
+    assert L.rt_comm_info(None, None, None, None) == 1
+    assert L.rt_gather_stripes(None, None, None, None, None, 8, 8, 0, None) == 6
+    assert L.rt_candidate_stats(None, None) == 6
+
+
+def test_comm_unique_id_without_device(rt):
+    """rt_comm_unique_id (ncclGetUniqueId) needs no GPU: 128 bytes, fresh on every call."""
+    from gpu_ray_tracing.distributed import StripeComm
+    a, b = StripeComm.unique_id(), StripeComm.unique_id()
+    assert len(a) == len(b) == rt._lib.RT_COMM_ID_BYTES == 128
+    assert a != b
 
 
 def test_srgb_thresholds_match_restatement(rt):

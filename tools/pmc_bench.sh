@@ -1,7 +1,8 @@
 #!/bin/bash
 # PMC summaries of the timed trace kernel of `bench.py --config CFG` (the kernel instance and
 # frames per launch the bench line reports): FETCH_SIZE and WRITE_SIZE in separate passes
-# (MI355X_MICROARCH.md §HBM), then one SQ/GRBM group.  Writes gpurun_out/TAG/pmc_r02_CFG.json
+# (MI355X_MICROARCH.md §HBM), then SQ/GRBM groups and the VALU instruction classes (two
+# passes of 8 SQ counters, read by tools/valu_weighted.py).  Writes gpurun_out/TAG/pmc_r03_CFG.json
 # (copy to profiles/ to have bench.py report `traffic` and `roofline.valu` from it).
 # Usage: bash tools/pmc_bench.sh TAG "K3 K2 K4 K5"
 set -o pipefail
@@ -17,12 +18,15 @@ for c in $CFGS; do
   F=$(python3 -c "import json; print(json.loads(open('$O/pmc_bench_$c.json').read())['roofline']['frames_per_launch'])")
   i=0
   for CS in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
-            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY"; do
+            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY" \
+            "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT64" \
+            "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_ACTIVE_INST_VALU2 SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_WAVES"; do
     i=$((i+1))
-    timeout -k 10 300 rocprofv3 --pmc $CS --output-format csv -d $O/raw -o ${c}_p$i -- python3 bench.py $ARGS \
+    timeout -s KILL 120 rocprofv3 --pmc $CS --output-format csv -d $O/raw -o ${c}_p$i -- python3 bench.py $ARGS \
       > $O/pmc_${c}_p$i.log 2>&1 || { echo "pmc $c pass $i failed"; tail -5 $O/pmc_${c}_p$i.log; exit 1; }
   done
-  python3 tools/pmc_bench_summary.py $O/pmc_r02_$c.json "$K" "$F" $O/raw/${c}_p1_counter_collection.csv \
-    $O/raw/${c}_p2_counter_collection.csv $O/raw/${c}_p3_counter_collection.csv \
-    $O/raw/${c}_p4_counter_collection.csv || exit 1
+  U=$(python3 -c "import json; print(json.loads(open('$O/pmc_bench_$c.json').read())['roofline']['kernel_avg_us'])")
+  python3 tools/pmc_bench_summary.py $O/pmc_r03_$c.json "$K" "$F" $O/raw/${c}_p*_counter_collection.csv \
+    || exit 1
+  python3 -c "import json; d=json.load(open('$O/pmc_r03_$c.json')); d['kernel_avg_us']=$U; json.dump(d, open('$O/pmc_r03_$c.json','w'), indent=1)"
 done

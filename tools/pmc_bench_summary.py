@@ -1,4 +1,4 @@
-"""Reduce rocprofv3 --pmc CSVs of one bench config to profiles/pmc_r02_<cfg>.json (read by
+"""Reduce rocprofv3 --pmc CSVs of one bench config to profiles/pmc_r03_<cfg>.json (read by
 bench.py): per-launch medians over the dispatches of the timed kernel instance.
 HBM bytes per launch (MI355X_MICROARCH.md §HBM): FETCH_SIZE x2 (gfx950 reports half the
 bytes of wide coalesced reads) x 1024 + WRITE_SIZE x 1024 (both in KiB).
@@ -13,6 +13,8 @@ out, kernel, fpl, files = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4
 vals = collections.defaultdict(list)
 for f in files:
     per = collections.defaultdict(float)
+    if not f.endswith(".csv"):
+        continue
     for r in csv.DictReader(open(f)):
         if kernel + "(" not in r["Kernel_Name"]:
             continue

@@ -15,6 +15,7 @@ __device__ inline float tof(float v) { return v; }
 __device__ inline float tof(unsigned v) { return (float)v; }
 __device__ inline float tof(unsigned long long v) { return (float)v; }
 __device__ inline float tof(f2 v) { return v.x + v.y; }
+__device__ inline float tof(double v) { return (float)v; }
 
 #define REP8(S, A) S(A##0) S(A##1) S(A##2) S(A##3) S(A##4) S(A##5) S(A##6) S(A##7)
 
@@ -145,6 +146,51 @@ KER(k_cnd_sgpr, f1, F1, _)
 KER(k_cmp_lt, f1, F1, _)
 KER(k_cmp_class, f1, F1, _)
 
+// round 3: the remaining forms of rt_single_kernel's hot path (tools/valu_weighted.py)
+typedef double d1;
+#define D1(i) ((double)threadIdx.x * 0.5 + (double)(i))
+const double dx = 1.5;
+#define STEP_k_mul_f64(a) asm volatile("v_mul_f64 %0, %1, %0" : "+v"(a) : "v"(dx));
+KER(k_mul_f64, d1, D1, _)
+#define STEP_k_fma_f64(a) asm volatile("v_fma_f64 %0, %1, %1, %0" : "+v"(a) : "v"(dx));
+KER(k_fma_f64, d1, D1, _)
+#define STEP_k_cvt_f64_f32(a) { double t_; asm volatile("v_cvt_f64_f32 %0, %1" : "=v"(t_) : "v"(a)); asm volatile("" :: "v"(t_)); }
+KER(k_cvt_f64_f32, f1, F1, _)
+#define STEP_k_cvt_f32_f64(a) { float t_; asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(t_) : "v"(a)); asm volatile("" :: "v"(t_)); }
+KER(k_cvt_f32_f64, d1, D1, _)
+#define STEP_k_cvt_u32_f32(a) asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(a));
+KER(k_cvt_u32_f32, f1, F1, _)
+#define STEP_k_fmac(a) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(a) : "v"(x), "v"(y));
+KER(k_fmac, f1, F1, _)
+#define STEP_k_fmamk(a) asm volatile("v_fmamk_f32 %0, %0, 0x3f8ccccd, %1" : "+v"(a) : "v"(x));
+KER(k_fmamk, f1, F1, _)
+#define STEP_k_add_f32(a) asm volatile("v_add_f32 %0, %1, %0" : "+v"(a) : "v"(x));
+KER(k_add_f32, f1, F1, _)
+#define STEP_k_bitop3(a) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96" : "+v"(a) : "v"(ux));
+KER(k_bitop3, u1, U1, _)
+#define STEP_k_lshl_or(a) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(a) : "v"(ux));
+KER(k_lshl_or, u1, U1, _)
+#define STEP_k_min3_u32(a) asm volatile("v_min3_u32 %0, %0, %1, %1" : "+v"(a) : "v"(ux));
+KER(k_min3_u32, u1, U1, _)
+#define STEP_k_max_i32(a) asm volatile("v_max_i32 %0, %1, %0" : "+v"(a) : "v"(ux));
+KER(k_max_i32, u1, U1, _)
+#define STEP_k_bfe(a) asm volatile("v_bfe_u32 %0, %0, 3, 7" : "+v"(a));
+KER(k_bfe, u1, U1, _)
+#define STEP_k_lshl_add_u64(a) asm volatile("v_lshl_add_u64 %0, %0, 4, %0" : "+v"(a));
+KER(k_lshl_add_u64, l1, L1, _)
+#define STEP_k_mov_b64(a) asm volatile("v_mov_b64 %0, %1" : "=v"(a) : "v"(dx));
+KER(k_mov_b64, d1, D1, _)
+#define STEP_k_cmp_u32_e32(a) asm volatile("v_cmp_gt_u32_e32 vcc, %0, %1" :: "v"(a), "v"(ux) : "vcc");
+KER(k_cmp_u32_e32, u1, U1, _)
+#define STEP_k_cmp_f32_e32(a) asm volatile("v_cmp_gt_f32_e32 vcc, %0, %1" :: "v"(a), "v"(x) : "vcc");
+KER(k_cmp_f32_e32, f1, F1, _)
+#define STEP_k_cnd_vcc(a) asm volatile("s_mov_b64 vcc, %1\n\tv_cndmask_b32_e32 %0, %0, %2, vcc" : "+v"(a) : "s"(m64), "v"(x) : "vcc");
+KER(k_cnd_vcc, f1, F1, _)
+#define STEP_k_readfirstlane(a) { unsigned t_; asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(t_) : "v"(a)); asm volatile("" :: "s"(t_)); }
+KER(k_readfirstlane, u1, U1, _)
+#define STEP_k_mul_lo_mix(a) asm volatile("v_mul_lo_u32 %0, %1, %0\n\tv_add_u32 %0, %1, %0" : "+v"(a) : "v"(ux));
+KER(k_mul_lo_mix, u1, U1, _)
+
 template <typename F>
 int run(const char* name, F launch, float* d_out, unsigned long long* d_clk, int blocks) {
     hipEvent_t e0, e1;
@@ -185,5 +231,11 @@ int main() {
     RUN(k_cnd_sgpr); RUN(k_add_u32); RUN(k_lshr); RUN(k_and); RUN(k_mov); RUN(k_mul_f32); RUN(k_sub_f32);
     RUN(k_max_f32); RUN(k_fma_abs); RUN(k_fma_sgpr); RUN(k_fma_lit); RUN(k_cmp_lt); RUN(k_bfi); RUN(k_cmp_class);
     RUN(k_min3); RUN(k_rndne); RUN(k_cvt_i32);
+    RUN(k_mul_f64); RUN(k_fma_f64); RUN(k_cvt_f64_f32); RUN(k_cvt_f32_f64); RUN(k_cvt_u32_f32);
+    RUN(k_fmac); RUN(k_fmamk); RUN(k_add_f32); RUN(k_bitop3); RUN(k_lshl_or); RUN(k_min3_u32);
+    RUN(k_max_i32); RUN(k_bfe); RUN(k_lshl_add_u64); RUN(k_mov_b64); RUN(k_cmp_u32_e32);
+    RUN(k_cmp_f32_e32); RUN(k_cnd_vcc); RUN(k_readfirstlane);
+    // (two instructions per step: the pair's cost)
+    RUN(k_mul_lo_mix);
     return 0;
 }
