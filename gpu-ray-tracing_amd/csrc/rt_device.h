@@ -13,6 +13,11 @@
 
 #define RT_HD __host__ __device__ __forceinline__
 
+// sincos_c's quadrant swap as bit selects (1) or selects (0); identical bits
+#ifndef RT_SINCOS_BITS
+#define RT_SINCOS_BITS 0
+#endif
+
 namespace rtd {
 
 struct v3 {
@@ -75,9 +80,33 @@ RT_HD void sincos_c(float x, float& s, float& c) {
     const float sr = fmaf(r * r2, ps, r);
     const float pc = fmaf(fmaf(0x1.99eb9cp-16f, r2, -0x1.6c0c34p-10f), r2, 0x1.55554ap-5f);
     const float cr = fmaf(r2 * r2, pc, fmaf(-0.5f, r2, 1.0f));
+#if RT_SINCOS_BITS
+    // the odd-quadrant swap as bit selects under an all-ones mask: on gfx950 one v_bfe_i32
+    // and one v_bitop3 per select (no compare writing VCC, no hazard nops); the same bits
+    // as the selects below
+    float s0, c0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t sw = (uint32_t)__builtin_amdgcn_sbfe(k, 0, 1);   // 0 or all ones
+    uint32_t s0b, c0b;
+    // bitop3:0xCA = S0 ? S1 : S2 bitwise (truth table over 0xF0, 0xCC, 0xAA)
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(s0b) : "v"(sw), "v"(cr), "v"(sr));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(c0b) : "v"(sw), "v"(sr), "v"(cr));
+    s0 = __uint_as_float(s0b);
+    c0 = __uint_as_float(c0b);
+#else
+    const uint32_t sw = 0u - ((uint32_t)k & 1u);
+    uint32_t sb, cb;
+    memcpy(&sb, &sr, 4);
+    memcpy(&cb, &cr, 4);
+    const uint32_t s0b = (cb & sw) | (sb & ~sw), c0b = (sb & sw) | (cb & ~sw);
+    memcpy(&s0, &s0b, 4);
+    memcpy(&c0, &c0b, 4);
+#endif
+#else
     const bool swap = (k & 1) != 0;
     const float s0 = swap ? cr : sr;
     const float c0 = swap ? sr : cr;
+#endif
     // the quadrant's signs as sign-bit flips (the bits of -x; no compare + select)
     s = flip_sign(s0, ((uint32_t)k << 30) & 0x80000000u);
     c = flip_sign(c0, ((uint32_t)(k + 1) << 30) & 0x80000000u);

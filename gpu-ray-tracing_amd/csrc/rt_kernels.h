@@ -195,7 +195,7 @@ const char* single_kernel_name(uint32_t pix);
 // tile_order for launch_trace: the local tiles by decreasing recorded cost (quantised
 // log2 of tile_cost), so the slowest tiles start first and the cheap ones fill the tail.
 hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, uint32_t tiles,
-                             uint32_t tiles_x, hipStream_t stream);
+                             uint32_t tiles_x, hipStream_t stream, uint32_t snake = 0);
 // Exact fast-path self-test (rt_selftest_fastmath): cnt[5] device counters, zeroed.
 hipError_t launch_selftest(unsigned long long* cnt, uint64_t n_rand, hipStream_t stream);
 

@@ -665,11 +665,24 @@ __device__ __forceinline__ void init_disk_rcp(const TraceParams& p) {
         s_disk_rcp[threadIdx.x] = v;
     }
 }
-template <bool kTable>
+// The eight table entries in closed form: sqrtf(len2) = 1 - m 2^-24 with
+// m = (0x3F800001 - bits(len2)) >> 1 in {3, 3, 2, 2, 1, 1, 0, 0}, and
+// RN64(1 / (1 - m 2^-24)) = 1 + m 2^-24 + m^2 2^-48 exactly (the next term, m^3 2^-72, is
+// below half an ulp of 1): the f64 bits 0x3FF00000 : (m << 28 | m^2 << 4).  (rt_abi.cpp
+// fill_camera computes the table with the IEEE operations; the self-test compares the
+// register form with the IEEE division for all 2^32 seeds.)
+__device__ __forceinline__ double disk_rcp_reg(float len2) {
+    const uint32_t m = (0x3F800001u - __float_as_uint(len2)) >> 1;
+    const uint32_t lo = (m << 28) | ((m * m) << 4);
+    return __hiloint2double(0x3FF00000, (int)lo);
+}
+// kTable: 0 = sqrt_core / div_core, 1 = the LDS table (s_disk_rcp), 2 = disk_rcp_reg
+template <int kTable>
 __device__ __forceinline__ void disk_unit(float sa, float ca, float& ux, float& uy) {
     const float len2 = fmaf(sa, sa, ca * ca);
     if (kTable) {
-        const double y = s_disk_rcp[__float_as_uint(len2) - kDiskLen2Lo];
+        const double y = kTable == 2 ? disk_rcp_reg(len2)
+                                     : s_disk_rcp[__float_as_uint(len2) - kDiskLen2Lo];
         ux = (float)((double)ca * y);
         uy = (float)((double)sa * y);
     } else {
@@ -683,7 +696,7 @@ __device__ __forceinline__ void disk_unit(float sa, float ca, float& ux, float& 
 // get_ray (wgsl:305-325) with the pixel-invariant hash(hash(x*73) ^ hash(y*51)) part
 // precomputed per pixel: seed = hash(hxy ^ su), su = sample_index*25 + B (wave-uniform
 // when every pixel of the wave holds the same sample count).
-template <bool kTable>
+template <int kTable>
 __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, uint32_t hxy,
                                         uint32_t su, v3& o, v3& d) {
     const uint32_t seed = hash(hxy ^ su);
@@ -1330,6 +1343,13 @@ constexpr uint32_t kSingleWg = RT_SINGLE_WG;
 #ifndef RT_SINGLE_WT
 #define RT_SINGLE_WT 1
 #endif
+// The defocus disk's reciprocal in the one-frame kernel: 1 = the workgroup's LDS table
+// (filled by wave 0 from the launch parameters, one barrier), 2 = its closed form in
+// registers (disk_rcp_reg: no table, no barrier)
+#ifndef RT_SINGLE_DISK
+#define RT_SINGLE_DISK 1
+#endif
+constexpr int kSingleDisk = RT_SINGLE_DISK;
 
 
 // Shading of a camera ray's hit at depth 1 (ray_color's loop body at i = 0, wgsl:266-286):
@@ -1416,7 +1436,8 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
         d[s] = sub(fmas((float)tc[s].y + (float)(hxy[s] & 1u), cam.pdv,
                         fmas((float)tc[s].x, cam.pdu, cam.vul)), o[s]);
 #else
-        get_ray<true>(cam, tc[s].x, tc[s].y, hxy[s], seed[s] * 25u + p.seed_b, o[s], d[s]);
+        get_ray<kSingleDisk>(cam, tc[s].x, tc[s].y, hxy[s], seed[s] * 25u + p.seed_b, o[s],
+                             d[s]);
 #endif
     }
     SST_V(3, d[S - 1].x);
@@ -1602,7 +1623,7 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
     for (uint32_t s = 0; s < S; ++s)
         acc[s] = (RT_SKO & 1) ? make_float4(0.0f, 0.0f, 0.0f, (float)p.n_hint)
                               : a_in[tc[s].valid ? tc[s].idx : 0];                // wgsl:339
-    if (p.defocus_angle > 0.0f) {                                 // (disk_unit's table)
+    if (kSingleDisk == 1 && p.defocus_angle > 0.0f) {             // (disk_unit's table)
         if (threadIdx.x < 8u) {
             double v = 0.0;
 #pragma unroll
@@ -2037,9 +2058,20 @@ rt_bounce_kernel(const TraceParams p) {
 // contend inside a wave), one block-wide scan over the [bucket][wave] counts turns them
 // into offsets, costliest bucket first, and each tile is placed at its wave's next slot of
 // its bucket (order inside a bucket is arbitrary: tiles are independent).
+// snake > 0: the sorted list is dealt in runs of `snake`, every second run reversed (the
+// costliest of run 2 pairs with the cheapest of run 1 on the dispatcher's round-robin over
+// CUs), for launches of a few workgroups per CU.
+__device__ __forceinline__ uint32_t snake_pos(uint32_t pos, uint32_t n, uint32_t g) {
+    if (g == 0u) return pos;
+    const uint32_t c = pos / g, j = pos - c * g;
+    if ((c & 1u) == 0u) return pos;
+    const uint32_t len = min(g, n - c * g);
+    return c * g + (len - 1u - j);
+}
 __global__ __launch_bounds__(1024) void rt_tile_order_kernel(const uint32_t* __restrict__ cost,
                                                              uint32_t* __restrict__ order,
-                                                             uint32_t tiles, uint32_t tiles_x) {
+                                                             uint32_t tiles, uint32_t tiles_x,
+                                                             uint32_t snake) {
     constexpr uint32_t kBuckets = 128, kWaves = 16, kSlots = kBuckets * kWaves;
     __shared__ uint32_t hist[kSlots];          // [bucket][wave]
     __shared__ uint32_t scan[1024];
@@ -2096,20 +2128,24 @@ __global__ __launch_bounds__(1024) void rt_tile_order_kernel(const uint32_t* __r
             const uint32_t t = t0 + k * 1024u;
             if (t < tiles) {
                 const uint32_t pos = atomicAdd(&hist[bucket(c[k]) * kWaves + wave], 1u);
-                order[pos] = ((t / tiles_x) << 16) | (t % tiles_x);
+                order[snake_pos(pos, tiles, snake)] = ((t / tiles_x) << 16) | (t % tiles_x);
             }
         }
     }
 }
 
 hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, uint32_t tiles,
-                             uint32_t tiles_x, hipStream_t stream) {
+                             uint32_t tiles_x, hipStream_t stream, uint32_t snake) {
     if (tiles == 0) return hipSuccess;
     hipLaunchKernelGGL(rt_tile_order_kernel, dim3(1), dim3(1024), 0, stream, tile_cost,
-                       tile_order, tiles, tiles_x);
+                       tile_order, tiles, tiles_x, snake);
     return hipGetLastError();
 }
 
+// wg_order dealt in snake runs of this many workgroups (0 = straight costliest first)
+#ifndef RT_WG_SNAKE
+#define RT_WG_SNAKE 0
+#endif
 // Per-workgroup candidate-list load of one-frame launches (wg_order's sort key): the sum of
 // its `per` tiles' loads (4 + count for a tile with a list, 64 for a tile without one).
 __global__ __launch_bounds__(256) void rt_wg_cost_kernel(const float4* __restrict__ cand,
@@ -2361,13 +2397,16 @@ __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cn
         sincos_c(ang, sa, ca);
         const float len_ref = sqrtf(fmaf(sa, sa, ca * ca));
         const float ux_ref = ca / len_ref, uy_ref = sa / len_ref;
-        float ux, uy, tx, ty;
-        disk_unit<false>(sa, ca, ux, uy);
-        disk_unit<true>(sa, ca, tx, ty);
+        float ux, uy, tx, ty, gx, gy;
+        disk_unit<0>(sa, ca, ux, uy);
+        disk_unit<1>(sa, ca, tx, ty);
+        disk_unit<2>(sa, ca, gx, gy);
         bad0 += (__float_as_uint(ux) != __float_as_uint(ux_ref)) ||
                 (__float_as_uint(uy) != __float_as_uint(uy_ref)) ||
                 (__float_as_uint(tx) != __float_as_uint(ux_ref)) ||
-                (__float_as_uint(ty) != __float_as_uint(uy_ref));
+                (__float_as_uint(ty) != __float_as_uint(uy_ref)) ||
+                (__float_as_uint(gx) != __float_as_uint(ux_ref)) ||
+                (__float_as_uint(gy) != __float_as_uint(uy_ref));
         const float x = __uint_as_float((uint32_t)i);
         if ((uint32_t)i >= 0x0F800000u && (uint32_t)i < 0x7F800000u)   // [2^-96, +inf)
             bad2 += __float_as_uint(sqrt_core(x)) != __float_as_uint(sqrtf(x));
@@ -2530,7 +2569,7 @@ hipError_t launch_wg_order(const float4* cand, uint32_t tiles_x, uint32_t bands,
                        tiles_x, cols, per, units, wg_cost);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_tile_order(wg_cost, wg_order, units, cols, stream);
+    return launch_tile_order(wg_cost, wg_order, units, cols, stream, RT_WG_SNAKE);
 }
 
 hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream) {

@@ -517,7 +517,9 @@ def test_candidate_list_overflow_falls_back(rt, depth):
     s[0] = [0, -1000, 0, 1000, 0.5, 0.5, 0.5, -2]
     sc = rt.SphereCollection(s)
     w, h = 64, 64
-    cam = rt.SceneCamera.from_settings(rt.CameraSettings(field_of_view=3.0, max_depth=depth), w, h, 0.5)
+    # aimed at the cluster: the middle tiles' cones admit far more than kCandMax spheres
+    cam = rt.SceneCamera.from_settings(rt.CameraSettings(field_of_view=3.0, max_depth=depth,
+                                                         look_at=(0.0, 1.0, 0.0)), w, h, 0.5)
     out = {}
     for mode in ("culled", "exhaustive"):
         p = rt.ComputeShaderPipeline(0)

@@ -24,3 +24,12 @@ python -c "import json; d=json.load(open('$O/bench_driver.json')); print(d['valu
 bash tools/pmc_bench.sh $TAG "K3 K2" || exit 1
 RT_FPL=1 timeout -k 10 300 python tools/rank_sim.py K3 100 > $O/rank_k3_dispatch.jsonl 2>&1 || exit 1
 grep '^{' $O/rank_k3_dispatch.jsonl
+# A/B of the one-frame kernel variants (bench.py lines, interleaved) and their rank shares
+V=gpu-ray-tracing_amd/build/variants
+bash tools/gpu_ab_bench.sh $TAG/ab "K3 K2" 3 default $V/librt_hip_disk2.so $V/librt_hip_sinbits.so \
+  $V/librt_hip_snake256.so $V/librt_hip_wg8.so $V/librt_hip_combo.so $V/librt_hip_combowg8.so || exit 1
+for v in disk2 snake256 combo wg8; do
+  RT_HIP_LIB=$V/librt_hip_$v.so RT_FPL=1 timeout -k 10 300 python tools/rank_sim.py K3 100 \
+    > $O/rank_k3_dispatch_$v.jsonl 2>&1 || exit 1
+  echo $v; grep '^{' $O/rank_k3_dispatch_$v.jsonl
+done
