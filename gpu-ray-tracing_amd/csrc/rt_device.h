@@ -13,9 +13,11 @@
 
 #define RT_HD __host__ __device__ __forceinline__
 
-// sincos_c's quadrant swap as bit selects (1) or selects (0); identical bits
+// sincos_c's quadrant swap as bit selects (1, default) or selects (0); identical bits
+// (with the closed-form disk reciprocal, K2 15.74 against 16.0 us per update,
+// profiles/r03a_ab_single.log)
 #ifndef RT_SINCOS_BITS
-#define RT_SINCOS_BITS 0
+#define RT_SINCOS_BITS 1
 #endif
 
 namespace rtd {

@@ -273,6 +273,12 @@ __device__ __forceinline__ v3 acc_f64(v3 c, v3 num, double y) {
 }
 template <int kScan>
 constexpr bool fast_core(int bit) { return is_list_kernel(kScan) && (RT_FAST_CORES & bit) != 0; }
+// The defocus disk's reciprocal in the camera-ray-only trace instances: 1 = the workgroup's
+// LDS table (one barrier at wave start), 2 = the closed form in registers (disk_rcp_reg)
+#ifndef RT_TRACE_DISK
+#define RT_TRACE_DISK 1
+#endif
+constexpr int kTraceDisk = RT_TRACE_DISK;
 
 // Scan records are read through the constant address space: they do not change during a
 // launch, and only then may the compiler use scalar loads (s_load_dwordx8/16 into SGPRs)
@@ -458,14 +464,51 @@ __device__ __forceinline__ void consider_any(float disc, float h, float a, uint3
         }
     }
 }
-__device__ __forceinline__ Hit scan_grid(const TraceParams& p, v3 o, v3 d, bool live) {
+// The grid's launch parameters (TraceParams grid_*), as one value: built from the kernel
+// argument, or (rt_bounce_kernel, RT_BOUNCE_RELOAD) re-read from the kernarg segment at every
+// use so that they do not stay live in SGPRs across the frame loop.
+struct GridP {
+    const uint2* cells;
+    const float4* geom;
+    const uint32_t* items;
+    const uint32_t* big;
+    const float4* sgeom;     // TraceParams::geom (the big spheres' records)
+    uint32_t nx, nz, nbig;
+    float x0, z0, s, inv_s, ylo, yhi, cx, cy, cz, reach, m, e;
+};
+template <typename P>
+__device__ __forceinline__ GridP grid_params(const P& p) {
+    GridP g;
+    g.cells = p.grid_cells;
+    g.geom = p.grid_geom;
+    g.items = p.grid_items;
+    g.big = p.grid_big;
+    g.sgeom = p.geom;
+    g.nx = p.grid_nx;
+    g.nz = p.grid_nz;
+    g.nbig = p.grid_nbig;
+    g.x0 = p.grid_x0;
+    g.z0 = p.grid_z0;
+    g.s = p.grid_s;
+    g.inv_s = p.grid_inv_s;
+    g.ylo = p.grid_ylo;
+    g.yhi = p.grid_yhi;
+    g.cx = p.grid_cx;
+    g.cy = p.grid_cy;
+    g.cz = p.grid_cz;
+    g.reach = p.grid_reach;
+    g.m = p.grid_m;
+    g.e = p.grid_e;
+    return g;
+}
+__device__ __forceinline__ Hit scan_grid(const GridP& p, v3 o, v3 d, bool live) {
     const float a = dot(d, d);
     float tmax = 0x1.05ed2ep+118f;             // 3.4e35 (wgsl:266)
     int idx = -1;
     // spheres outside the grid (the ground, large ones): every live lane tests them
-    for (uint32_t b = 0; b < p.grid_nbig; ++b) {
-        const uint32_t i = p.grid_big[b];
-        const float4 g = p.geom[i];
+    for (uint32_t b = 0; b < p.nbig; ++b) {
+        const uint32_t i = p.big[b];
+        const float4 g = p.sgeom[i];
         float h;
         const float disc = discriminant(g, o, d, a, h);
         if (live) consider_any(disc, h, a, i, tmax, idx);
@@ -482,33 +525,33 @@ __device__ __forceinline__ Hit scan_grid(const TraceParams& p, v3 o, v3 d, bool 
             t1 = -1.0f;
         }
     };
-    const float xhi = p.grid_x0 + p.grid_s * (float)p.grid_nx;
-    const float zhi = p.grid_z0 + p.grid_s * (float)p.grid_nz;
-    clip(o.y, d.y, p.grid_ylo, p.grid_yhi);
-    clip(o.x, d.x, p.grid_x0, xhi);
-    clip(o.z, d.z, p.grid_z0, zhi);
+    const float xhi = p.x0 + p.s * (float)p.nx;
+    const float zhi = p.z0 + p.s * (float)p.nz;
+    clip(o.y, d.y, p.ylo, p.yhi);
+    clip(o.x, d.x, p.x0, xhi);
+    clip(o.z, d.z, p.z0, zhi);
     if (!(t0 <= t1)) return Hit{idx, tmax};
     // 2-D DDA over the cells from P(t0) to P(t1)
-    const int nx = (int)p.grid_nx, nz = (int)p.grid_nz;
-    int ix = (int)floorf((fmaf(t0, d.x, o.x) - p.grid_x0) * p.grid_inv_s);
-    int iz = (int)floorf((fmaf(t0, d.z, o.z) - p.grid_z0) * p.grid_inv_s);
+    const int nx = (int)p.nx, nz = (int)p.nz;
+    int ix = (int)floorf((fmaf(t0, d.x, o.x) - p.x0) * p.inv_s);
+    int iz = (int)floorf((fmaf(t0, d.z, o.z) - p.z0) * p.inv_s);
     ix = min(max(ix, 0), nx - 1);
     iz = min(max(iz, 0), nz - 1);
     const int sx = d.x > 0.0f ? 1 : -1, sz = d.z > 0.0f ? 1 : -1;
     const float inf = 0x1.05ed2ep+118f;
     float tx = d.x != 0.0f
-                   ? (p.grid_x0 + p.grid_s * (float)(ix + (sx > 0)) - o.x) / d.x : inf;
+                   ? (p.x0 + p.s * (float)(ix + (sx > 0)) - o.x) / d.x : inf;
     float tz = d.z != 0.0f
-                   ? (p.grid_z0 + p.grid_s * (float)(iz + (sz > 0)) - o.z) / d.z : inf;
-    const float dtx = d.x != 0.0f ? p.grid_s / fabsf(d.x) : inf;
-    const float dtz = d.z != 0.0f ? p.grid_s / fabsf(d.z) : inf;
-    const float slack = 2.0f * p.grid_e * rsqrtf(a) * 1.01f;
+                   ? (p.z0 + p.s * (float)(iz + (sz > 0)) - o.z) / d.z : inf;
+    const float dtx = d.x != 0.0f ? p.s / fabsf(d.x) : inf;
+    const float dtz = d.z != 0.0f ? p.s / fabsf(d.z) : inf;
+    const float slack = 2.0f * p.e * rsqrtf(a) * 1.01f;
     for (int step = 0; step < nx + nz + 2; ++step) {
-        const uint2 range = p.grid_cells[iz * nx + ix];
+        const uint2 range = p.cells[iz * nx + ix];
         for (uint32_t k = range.x; k < range.y; ++k) {
             float h;
-            const float disc = discriminant(p.grid_geom[k], o, d, a, h);
-            consider_any(disc, h, a, p.grid_items[k], tmax, idx);
+            const float disc = discriminant(p.geom[k], o, d, a, h);
+            consider_any(disc, h, a, p.items[k], tmax, idx);
         }
         // A cell entered beyond t1, or beyond the closest hit so far, holds no better hit;
         // slack: the walk's position error (grid_e, as t) and 1e-4 of t.
@@ -528,28 +571,29 @@ __device__ __forceinline__ Hit scan_grid(const TraceParams& p, v3 o, v3 d, bool 
 }
 
 // The wave may walk the grid: every live ray finite and within reach of the grid margin.
-__device__ __forceinline__ bool grid_usable(const TraceParams& p, v3 o, v3 d, bool live) {
-    if (p.grid_nx == 0u) return false;
-    const v3 oc = mk(o.x - p.grid_cx, o.y - p.grid_cy, o.z - p.grid_cz);
+__device__ __forceinline__ bool grid_usable(const GridP& p, v3 o, v3 d, bool live) {
+    if (p.nx == 0u) return false;
+    const v3 oc = mk(o.x - p.cx, o.y - p.cy, o.z - p.cz);
     const float dist = __builtin_amdgcn_sqrtf(dot(oc, oc));
     const float dd = dot(d, d);
     const bool ok = finite3(o) && finite3(d) && dd >= 0x1p-20f && dd <= 0x1p20f &&
-                    2.5e-3f * 1.01f * (dist + p.grid_reach) <= p.grid_m;
+                    2.5e-3f * 1.01f * (dist + p.reach) <= p.m;
     return __ballot(live && !ok) == 0ull;
 }
 
 template <bool kLds>
-__device__ __forceinline__ Hit scan_culled(const TraceParams& p, const float4* __restrict__ geom,
+__device__ __forceinline__ Hit scan_culled(const GridP& gp, const float4* __restrict__ geom,
                                            uint32_t count, v3 o, v3 d, bool live, bool bounce) {
     const float4* recs = kLds ? lds_recs : geom;
     // Bounce rays walk the grid whenever the wave may (measured faster than the cone
     // culling even for coherent specular waves); camera rays of tiles without a candidate
     // list keep the cone, whose rays share a narrow beam.
 #ifndef RT_NO_GRID
-    if (bounce && count >= kCullMinSpheres && grid_usable(p, o, d, live))
-        return scan_grid(p, o, d, live);
+    if (bounce && count >= kCullMinSpheres && grid_usable(gp, o, d, live))
+        return scan_grid(gp, o, d, live);
 #endif
     (void)bounce;
+    (void)gp;
     Cone k;
     if (count < kCullMinSpheres || !wave_cone(o, d, live, k))
         return scan_exhaustive<RT_SCAN_CHUNK>(geom, count, o, d);
@@ -635,6 +679,18 @@ struct Cam {
     v3 center, vul, pdu, pdv, ddu, ddv;
     float defocus_angle;
 };
+template <typename P>
+__device__ __forceinline__ Cam cam_params(const P& p) {
+    Cam cam;
+    cam.center = mk(p.center[0], p.center[1], p.center[2]);
+    cam.vul = mk(p.vul[0], p.vul[1], p.vul[2]);
+    cam.pdu = mk(p.pdu[0], p.pdu[1], p.pdu[2]);
+    cam.pdv = mk(p.pdv[0], p.pdv[1], p.pdv[2]);
+    cam.ddu = mk(p.ddu[0], p.ddu[1], p.ddu[2]);
+    cam.ddv = mk(p.ddv[0], p.ddv[1], p.ddv[2]);
+    cam.defocus_angle = p.defocus_angle;
+    return cam;
+}
 
 // The defocus disk's normalize((cos, sin)) (wgsl:327-331).  Over all 2^32 values of
 // hash(seed + 1), len2 = sa^2 + ca^2 takes only the eight f32 values of
@@ -775,8 +831,8 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
             (kScan != kTraceCulled || listed)
                 ? scan_exhaustive<scan_chunk<kScan>(), fast_core<kScan>(1), kScan != kTraceList>(
                       listed ? blk + kCandRecOff : p.geom, listed ? ncand : p.count, o, d)
-            : p.lds_records ? scan_culled<true>(p, p.geom, p.count, o, d, live, i > 0)
-                            : scan_culled<false>(p, p.geom, p.count, o, d, live, i > 0);
+            : p.lds_records ? scan_culled<true>(grid_params(p), p.geom, p.count, o, d, live, i > 0)
+                            : scan_culled<false>(grid_params(p), p.geom, p.count, o, d, live, i > 0);
 #endif
         if (kScan != kTraceCulled) STAMP(2);                      // (culled: inside the scan)
         const float4* hs = listed ? blk + kCandSphOff : p.sph;
@@ -920,7 +976,8 @@ __device__ __forceinline__ v3 sample(const TraceParams& p, const Cam& cam, uint3
     o = cam.center;
     d = sub(fmas((float)tc.y, cam.pdv, fmas((float)tc.x, cam.pdu, cam.vul)), o);
 #else
-    get_ray<fast_core<kScan>(16)>(cam, tc.x, tc.y, hxy, seed * 25u + B, o, d);   // wgsl:311
+    get_ray<fast_core<kScan>(16) ? kTraceDisk : 0>(cam, tc.x, tc.y, hxy, seed * 25u + B, o,
+                                                  d);                          // wgsl:311
 #endif
     STAMP(1);
     const v3 col = ray_color<kScan>(p, tile, ncand, depth, o, d, seed + 1u, live, uni, f);
@@ -1224,7 +1281,7 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
         }
         __syncthreads();
     }
-    if (fast_core<kScan>(16)) {                                   // (disk_unit)
+    if (fast_core<kScan>(16) && kTraceDisk == 1) {               // (disk_unit's table)
         init_disk_rcp(p);
         __syncthreads();
     }
@@ -1345,9 +1402,11 @@ constexpr uint32_t kSingleWg = RT_SINGLE_WG;
 #endif
 // The defocus disk's reciprocal in the one-frame kernel: 1 = the workgroup's LDS table
 // (filled by wave 0 from the launch parameters, one barrier), 2 = its closed form in
-// registers (disk_rcp_reg: no table, no barrier)
+// registers (disk_rcp_reg: no table, no barrier).  2 (default): K3 23.30 -> 22.46 us, K2
+// 17.13 -> 16.0 us per update, 8-rank K3 share 6.26 -> 5.52 us (profiles/r03a_ab_single.log):
+// the barrier made every wave of a workgroup wait for wave 0's kernarg read at wave start.
 #ifndef RT_SINGLE_DISK
-#define RT_SINGLE_DISK 1
+#define RT_SINGLE_DISK 2
 #endif
 constexpr int kSingleDisk = RT_SINGLE_DISK;
 
@@ -1849,6 +1908,19 @@ __device__ __forceinline__ uint32_t compact_slot(bool live, uint32_t wave, uint3
 #ifndef RT_BOUNCE_MIN_WAVES
 #define RT_BOUNCE_MIN_WAVES 6
 #endif
+// RT_BOUNCE_RELOAD: the camera (per frame) and the grid parameters (per bounce scan) are
+// re-read from the kernarg segment through a pointer the compiler cannot see through
+// (scalar-cache hits), instead of staying live in SGPRs for the whole launch.
+#ifndef RT_BOUNCE_RELOAD
+#define RT_BOUNCE_RELOAD 0
+#endif
+__device__ __forceinline__ const kconst TraceParams* karg_bounce_params() {
+    // rt_bounce_kernel's only argument: the TraceParams block at kernarg offset 0
+    const kconst TraceParams* q =
+        (const kconst TraceParams*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(q));
+    return q;
+}
 // Modes: kBounceWave — one-wave workgroups (one tile each: the finest unit for the
 // cost-ordered schedule) whose paths stay in their lanes, colours in registers, no
 // barriers; kBounceCompact — four-wave workgroups exchanging paths through LDS (above);
@@ -1897,14 +1969,9 @@ rt_bounce_kernel(const TraceParams p) {
     const uint32_t ncand = (p.cand_k && wave_in) ? load_cnt(p.cand, tile) : kCandNone;
     const float4* blk = p.cand + (size_t)tile * kCandStride;
     const uint32_t hxy = p.hx[min(tc.x, p.width - 1u)] ^ p.hy[min(tc.y, p.height - 1u)];
-    Cam cam;
-    cam.center = mk(p.center[0], p.center[1], p.center[2]);
-    cam.vul = mk(p.vul[0], p.vul[1], p.vul[2]);
-    cam.pdu = mk(p.pdu[0], p.pdu[1], p.pdu[2]);
-    cam.pdv = mk(p.pdv[0], p.pdv[1], p.pdv[2]);
-    cam.ddu = mk(p.ddu[0], p.ddu[1], p.ddu[2]);
-    cam.ddv = mk(p.ddv[0], p.ddv[1], p.ddv[2]);
-    cam.defocus_angle = p.defocus_angle;
+#if !RT_BOUNCE_RELOAD
+    const Cam cam = cam_params(p);
+#endif
     const uint32_t spp = p.spp, depth = p.depth;        // wgsl:343, 264
     // the pixel's accumulator (wgsl:339-341; a frame-0 reset discards it)
     v3 c = mk(0.0f, 0.0f, 0.0f);
@@ -1933,6 +2000,9 @@ rt_bounce_kernel(const TraceParams p) {
         if (kCompact) s_bounce.res[me] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         // bounce 0: this wave's own camera rays (wgsl:305-325), its tile's scan
         v3 o, d, cf = mk(1.0f, 1.0f, 1.0f);
+#if RT_BOUNCE_RELOAD
+        const Cam cam = cam_params(*karg_bounce_params());
+#endif
         get_ray<false>(cam, tc.x, tc.y, hxy, seed * 25u + B, o, d);
         uint32_t pseed = seed + 1u;                               // ray_color's seed
         bool live = sampling;
@@ -1947,10 +2017,15 @@ rt_bounce_kernel(const TraceParams p) {
             const float4* hs = p.sph;
             if (__ballot(live) != 0ull) {
                 const bool listed = i == 0u && ncand != kCandNone;
+#if RT_BOUNCE_RELOAD
+                const GridP gp = grid_params(*karg_bounce_params());
+#else
+                const GridP gp = grid_params(p);
+#endif
                 hit = listed ? scan_exhaustive<RT_SCAN_CHUNK, false, true>(blk + kCandRecOff,
                                                                           ncand, o, d)
-                      : p.lds_records ? scan_culled<true>(p, p.geom, p.count, o, d, live, i > 0)
-                                      : scan_culled<false>(p, p.geom, p.count, o, d, live, i > 0);
+                      : p.lds_records ? scan_culled<true>(gp, p.geom, p.count, o, d, live, i > 0)
+                                      : scan_culled<false>(gp, p.geom, p.count, o, d, live, i > 0);
                 if (listed) hs = blk + kCandSphOff;
             }
             bool done = false, keep = false;
