@@ -71,16 +71,19 @@ RT_HD float flip_sign(float x, uint32_t m) {
 }
 
 // Canonical sin/cos: Cody-Waite by pi/2 in three parts, Cephes minimax.
-RT_HD void sincos_c(float x, float& s, float& c) {
+// k1s / k1c: the leading coefficients of the two polynomials, -0x1.9943f2p-13f and
+// 0x1.99eb9cp-16f, passed in so that a kernel can keep them in registers (sincos_c below
+// passes the literals; the arithmetic is the same either way).
+RT_HD void sincos_k(float x, float& s, float& c, float k1s, float k1c) {
     const float q = rintf(x * 0x1.45f306p-1f);
     const int k = (q == q) ? (int)q : 0;
     float r = fmaf(q, -0x1.921fb6p+0f, x);
     r = fmaf(q, 0x1.777a5cp-25f, r);
     r = fmaf(q, 0x1p-49f, r);
     const float r2 = r * r;
-    const float ps = fmaf(fmaf(-0x1.9943f2p-13f, r2, 0x1.11073cp-7f), r2, -0x1.555546p-3f);
+    const float ps = fmaf(fmaf(k1s, r2, 0x1.11073cp-7f), r2, -0x1.555546p-3f);
     const float sr = fmaf(r * r2, ps, r);
-    const float pc = fmaf(fmaf(0x1.99eb9cp-16f, r2, -0x1.6c0c34p-10f), r2, 0x1.55554ap-5f);
+    const float pc = fmaf(fmaf(k1c, r2, -0x1.6c0c34p-10f), r2, 0x1.55554ap-5f);
     const float cr = fmaf(r2 * r2, pc, fmaf(-0.5f, r2, 1.0f));
 #if RT_SINCOS_BITS
     // the odd-quadrant swap as bit selects under an all-ones mask: on gfx950 one v_bfe_i32
@@ -112,6 +115,10 @@ RT_HD void sincos_c(float x, float& s, float& c) {
     // the quadrant's signs as sign-bit flips (the bits of -x; no compare + select)
     s = flip_sign(s0, ((uint32_t)k << 30) & 0x80000000u);
     c = flip_sign(c0, ((uint32_t)(k + 1) << 30) & 0x80000000u);
+}
+
+RT_HD void sincos_c(float x, float& s, float& c) {
+    sincos_k(x, s, c, -0x1.9943f2p-13f, 0x1.99eb9cp-16f);
 }
 
 // wgsl:234-243; rf_seed = rf(seed)

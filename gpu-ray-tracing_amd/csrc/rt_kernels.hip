@@ -123,6 +123,13 @@ __device__ __forceinline__ void sst_put(int k, unsigned long long t) {
 #define SST_S(k, dep) ((void)0)
 #endif
 
+// Wave ballot of a per-lane condition.  HIP's __ballot(int) takes the predicate as an int,
+// and the bool -> int -> bool round trip costs a v_cndmask + v_cmp per ballot on gfx950;
+// the builtin takes the condition's lane mask as it is.
+__device__ __forceinline__ unsigned long long rt_ballot(bool x) {
+    return __builtin_amdgcn_ballot_w64(x);
+}
+
 // Constant address space (read-only for the whole launch; eligible for scalar loads).
 // (The host pass of hipcc also parses device code; there the qualifier is dropped.)
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -399,8 +406,8 @@ __device__ __forceinline__ bool wave_cone(v3 o, v3 d, bool live, Cone& k) {
     const float dd = dot(d, d);
     const v3 q = add(o, d);
     const bool bad = live && !(finite3(o) && finite3(q) && dd > 0.0f && __builtin_isfinite(dd));
-    const unsigned long long lm = __ballot(live);
-    if (lm == 0ull || __ballot(bad)) return false;
+    const unsigned long long lm = rt_ballot(live);
+    if (lm == 0ull || rt_ballot(bad)) return false;
     // Axis and apex come from the first live lane (v_readlane: no cross-lane reduction);
     // the half-angle, the apex radius and max |d| are then exact max-reductions.
     const int L = (int)__builtin_ctzll(lm);
@@ -578,7 +585,7 @@ __device__ __forceinline__ bool grid_usable(const GridP& p, v3 o, v3 d, bool liv
     const float dd = dot(d, d);
     const bool ok = finite3(o) && finite3(d) && dd >= 0x1p-20f && dd <= 0x1p20f &&
                     2.5e-3f * 1.01f * (dist + p.reach) <= p.m;
-    return __ballot(live && !ok) == 0ull;
+    return rt_ballot(live && !ok) == 0ull;
 }
 
 template <bool kLds>
@@ -608,7 +615,7 @@ __device__ __forceinline__ Hit scan_culled(const GridP& gp, const float4* __rest
     for (uint32_t base = 0; base < count; base += 64u) {
         const float4 g = recs[base + lane];
         const bool keep = (base + lane < count) && !cone_misses(k, g);
-        unsigned long long mask = __ballot(keep);
+        unsigned long long mask = rt_ballot(keep);
         while (mask) {                                    // survivors, in index order
             const int j = __builtin_ctzll(mask);
             mask &= mask - 1ull;
@@ -678,6 +685,7 @@ __device__ __forceinline__ bool footprint_cone(const TraceParams& p, float x0, f
 struct Cam {
     v3 center, vul, pdu, pdv, ddu, ddv;
     float defocus_angle;
+    float k1s = -0x1.9943f2p-13f, k1c = 0x1.99eb9cp-16f;   // sincos_k's leading coefficients
 };
 template <typename P>
 __device__ __forceinline__ Cam cam_params(const P& p) {
@@ -767,7 +775,7 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
     if (cam.defocus_angle > 0.0f) {                     // defocus_disk_sample wgsl:327-331
         const float ang = (float)hash(seed + 1u) * 0x1.921fb4p-30f;  // 2*3.1415926 * rf
         float sa, ca, ux, uy;
-        sincos_c(ang, sa, ca);
+        sincos_k(ang, sa, ca, cam.k1s, cam.k1c);
         disk_unit<kTable>(sa, ca, ux, uy);
         o = fmas(uy, cam.ddv, fmas(ux, cam.ddu, cam.center));
     } else {
@@ -792,7 +800,7 @@ __device__ __forceinline__ v3 normalize_w(v3 v) {
         const float dd = dot(v, v);
         const bool in = __float_as_uint(dd) - kBits2m20 < kBits2p40 - kBits2m20 &&
                         min(min(abs_bits(v.x), abs_bits(v.y)), abs_bits(v.z)) >= kBits2m100;
-        if (__ballot(!in) == 0ull) {
+        if (rt_ballot(!in) == 0ull) {
             const float len = sqrt_core(dd);
             const float y = rcp_refined(len);
             return mk(div_core(v.x, len, y), div_core(v.y, len, y), div_core(v.z, len, y));
@@ -816,7 +824,7 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
     v3 cf = mk(1.0f, 1.0f, 1.0f);
     bool black = false;
     for (uint32_t i = 0; i < depth; ++i) {
-        if (__ballot(live) == 0ull) break;
+        if (rt_ballot(live) == 0ull) break;
         // Camera rays of a tile with a candidate list (ncand != kCandNone) test only the
         // listed spheres: their records are in index order and padded like the full list,
         // so the same chunk loop applies; hit.idx then indexes the tile's copy of the
@@ -871,7 +879,7 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
         const v3 rel = sub(hp, C);
         v3 outward;
         if (fast_core<kScan>(2) &&
-            __ballot(min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z)) <
+            rt_ballot(min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z)) <
                      kBits2m100) == 0ull) {
             const float y = rcp_refined(pr.w);
             outward = mk(div_core(rel.x, pr.w, y), div_core(rel.y, pr.w, y),
@@ -922,7 +930,7 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
     uy = d.y * (dd > -1.0f ? 1.0f : 0.5f);
 #else
     if (fast_core<kScan>(4) &&
-        __ballot(__float_as_uint(dd) - kBits2m20 >= kBits2p40 - kBits2m20) == 0ull) {
+        rt_ballot(__float_as_uint(dd) - kBits2m20 >= kBits2p40 - kBits2m20) == 0ull) {
         const float len = sqrt_core(dd);
         uy = div_core(d.y, len, rcp_refined(len));
     } else {
@@ -1015,8 +1023,8 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
         for (;;) {
             const bool live = pending && ng < spp;                // wgsl:352
             v3 col = mk(0.0f, 0.0f, 0.0f);
-            if (__ballot(live) != 0ull) {
-                const bool uni = hinted && __ballot(live && ng != p.hint_n[f]) == 0ull;
+            if (rt_ballot(live) != 0ull) {
+                const bool uni = hinted && rt_ballot(live && ng != p.hint_n[f]) == 0ull;
                 col = sample<kScan>(p, cam, tile, ncand, tc, hxy, ng, B, f, live, uni);
             }
             bool wrong = false;
@@ -1032,7 +1040,7 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
                        c.z + (col.z - c.z) / k);
                 n += 1u;
             }
-            if (__ballot(wrong) == 0ull) break;
+            if (rt_ballot(wrong) == 0ull) break;
             pending = wrong;                                      // retrace these pixels
             ng = n;
         }
@@ -1076,7 +1084,7 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
         v3 col = mk(0.0f, 0.0f, 0.0f);
         if (fw < p.frames) {
             const uint32_t ng = p.hint_n[fw];   // every pixel's count before frame fw
-            if (ng < spp && __ballot(tc.valid) != 0ull)           // wgsl:352
+            if (ng < spp && rt_ballot(tc.valid) != 0ull)           // wgsl:352
                 col = sample<kScan>(p, cam, tile, ncand, tc, hxy, ng, p.seed_b[fw], fw,
                                     tc.valid, fw < p.hint_frames);
         }
@@ -1103,7 +1111,7 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
                     const v3 num = sub(col, c);
                     // num / f32(nb + 1) (wgsl:356) as RN32(num * RN64(1 / k)) (acc_f64)
                     if (RT_ACC_F64 && nb < (1u << 24) &&
-                        __ballot(tc.valid && !acc_f64_ok(num)) == 0ull) {
+                        rt_ballot(tc.valid && !acc_f64_ok(num)) == 0ull) {
                         c = acc_f64(c, num, p.hint_rcp[fj]);
                     } else {
                         const float k = (float)(nb + 1u);         // wgsl:356
@@ -1301,7 +1309,7 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
         // every frame's image is stored inside; on a count mismatch (every wave sees the
         // same pixels, hence takes the same decision) wave 0 runs the single-wave loop and
         // the others have nothing to do
-        if (p.reset_first || __ballot(tc.valid && f2u(acc.w) != p.hint_n[0]) == 0ull) {
+        if (p.reset_first || rt_ballot(tc.valid && f2u(acc.w) != p.hint_n[0]) == 0ull) {
             trace_pair<kScan>(p, cam, tile, ncand, tc, hxy, acc, wave);
             record_cost<kScan>(p, tile, wave, lane);
             WAVE_TRACE(1);
@@ -1343,12 +1351,15 @@ struct SingleParams {
     float4* out;
     const float4* geom;    // full scan records (tiles without a candidate list)
     const float4* sph;     // full sphere records
-    uint32_t count, depth, spp, reset;
+    uint32_t count, depth, spp;
     uint32_t hinted;       // hint_n / hint_rcp / hint_rs of frame 0 are valid
     uint32_t n_hint;       // every pixel's count before the frame (0 on reset)
     uint32_t seed_b;       // B = u32(random_seed * 2^32) (wgsl:311, 353)
     uint32_t hy_off;       // hash(y * 51) table offset in the hx buffer
     double rcp_hint;       // RN64(1 / (n_hint + 1))
+    // RT_SINGLE_NCHK: n_hint < 2^24 (n_exact), the bits of f32(n_hint) and of f32(the count
+    // after the frame): a pixel holding exactly f32(n_hint) holds the hinted count
+    uint32_t n_exact, ng_bits, n_after_bits;
     float4 rs;             // (rf(sb), random_unit_vector(sb)) of frame 0, bounce 0
     double disk_rcp[8];
     float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3];
@@ -1362,8 +1373,11 @@ struct SingleParams {
 #endif
 constexpr uint32_t kSinglePix = RT_SINGLE_PIX;
 static_assert(kSinglePix >= 1 && kSinglePix <= 4, "1 to 4 tiles per wave");
+// Waves per SIMD the one-frame kernel's register plan targets.  The compiler fills the
+// SGPR budget the bound allows: at 5 it reached 98 SGPRs (6 resident waves per SIMD on
+// gfx950: MI355X_MICROARCH.md, Residency), at 7 it stays at <= 96 (7 waves) without spills.
 #ifndef RT_SINGLE_MIN_WAVES
-#define RT_SINGLE_MIN_WAVES 5
+#define RT_SINGLE_MIN_WAVES 7
 #endif
 #ifndef RT_SINGLE_ACC_F64
 #define RT_SINGLE_ACC_F64 1
@@ -1400,6 +1414,14 @@ constexpr uint32_t kSingleWg = RT_SINGLE_WG;
 #ifndef RT_SINGLE_WT
 #define RT_SINGLE_WT 1
 #endif
+// wave-invariant constants of the camera ray kept in VGPRs (1) or left to the compiler (0)
+#ifndef RT_SINGLE_VCONST
+#define RT_SINGLE_VCONST 0
+#endif
+// the hinted count checked as the f32 bits of the stored count (1) or through f2u (0)
+#ifndef RT_SINGLE_NCHK
+#define RT_SINGLE_NCHK 0
+#endif
 // The defocus disk's reciprocal in the one-frame kernel: 1 = the workgroup's LDS table
 // (filled by wave 0 from the launch parameters, one barrier), 2 = its closed form in
 // registers (disk_rcp_reg: no table, no barrier).  2 (default): K3 23.30 -> 22.46 us, K2
@@ -1420,7 +1442,7 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
     const v3 hp = fmas(t, d, o);
     const v3 rel = sub(hp, mk(pr.x, pr.y, pr.z));
     v3 outward;                                                   // wgsl:209
-    if (__ballot(hit && min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z)) <
+    if (rt_ballot(hit && min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z)) <
                             kBits2m100) == 0ull) {
         const float y = rcp_refined(pr.w);
         outward = mk(div_core(rel.x, pr.w, y), div_core(rel.y, pr.w, y),
@@ -1437,7 +1459,7 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
     att = mk(mat.x, mat.y, mat.z);
     black = false;
     const bool other = hit && !(mat.w < -1.0f);
-    if (__ballot(other) != 0ull && other) {
+    if (rt_ballot(other) != 0ull && other) {
         if (mat.w <= 1.0f) {                                      // metal wgsl:95-100
             const v3 refl = fmas(mat.w, ruv, normalize_w<true>(reflect(d, n)));
             black = !(dot(refl, n) > 0.0f);                       // wgsl:277-279
@@ -1459,7 +1481,7 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
 __device__ __forceinline__ v3 sky_w(v3 cf, v3 d) {
     const float dd = dot(d, d);
     float uy;
-    if (__ballot(__float_as_uint(dd) - kBits2m20 >= kBits2p40 - kBits2m20) == 0ull) {
+    if (rt_ballot(__float_as_uint(dd) - kBits2m20 >= kBits2p40 - kBits2m20) == 0ull) {
         const float len = sqrt_core(dd);
         uy = div_core(d.y, len, rcp_refined(len));
     } else {
@@ -1577,7 +1599,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s)
                 if (hit[s]) cf[s] = mk(tmax[s], 0.5f, 0.5f);
-        } else if (__ballot(any) != 0ull) {
+        } else if (rt_ballot(any) != 0ull) {
             float4 pr[S], mat[S];
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
@@ -1593,7 +1615,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
             }
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
-                if (RT_SINGLE_GATE && __ballot(hit[s]) == 0ull) continue;   // (sky tiles)
+                if (RT_SINGLE_GATE && rt_ballot(hit[s]) == 0ull) continue;   // (sky tiles)
                 float r_sb;
                 v3 ruv;
                 if (kUniRs) {
@@ -1624,12 +1646,15 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
     SST_V(5, col[S - 1].x);
 }
 
-template <int kPix>
-__global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
+// kReset: the frame resets the accumulator (camera_has_moved > 0.5, wgsl:345-350) — a
+// separate kernel (rt_single_reset_kernel), so that the steady-state kernel carries no
+// per-pixel selects between the loaded and the zero accumulator, and the reset kernel no
+// accumulator load at all.
+template <int kPix, bool kReset>
+__device__ __forceinline__ void single_body(
     const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
-    const uint32_t* __restrict__ a_order,
-    const SingleParams p) {
+    const uint32_t* __restrict__ a_order, const SingleParams& p) {
     static_assert(kPix >= 1 && kPix <= 4, "1 to 4 tiles per wave");
     constexpr uint32_t S = kPix;
     WAVE_TRACE(0);
@@ -1681,6 +1706,7 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s)
         acc[s] = (RT_SKO & 1) ? make_float4(0.0f, 0.0f, 0.0f, (float)p.n_hint)
+                 : kReset     ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)   // (discarded: no load)
                               : a_in[tc[s].valid ? tc[s].idx : 0];                // wgsl:339
     if (kSingleDisk == 1 && p.defocus_angle > 0.0f) {             // (disk_unit's table)
         if (threadIdx.x < 8u) {
@@ -1704,6 +1730,14 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
     cam.ddu = mk(p.ddu[0], p.ddu[1], p.ddu[2]);
     cam.ddv = mk(p.ddv[0], p.ddv[1], p.ddv[2]);
     cam.defocus_angle = p.defocus_angle;
+#if RT_SINGLE_VCONST
+    // wave-invariant operands that would otherwise be re-materialised per use (gfx950 VALU
+    // instructions take one SGPR or literal): the sincos coefficients the v_fmaak forms
+    // need in a register, and the lens centre of fma(u, ddu, centre) — one v_mov each per
+    // wave instead of per pixel
+    asm volatile("" : "+v"(cam.k1s), "+v"(cam.k1c));
+    asm volatile("" : "+v"(cam.center.x), "+v"(cam.center.y), "+v"(cam.center.z));
+#endif
     const uint32_t spp = p.spp;                                   // wgsl:343
 
     v3 c[S];
@@ -1728,14 +1762,25 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
         any_pending = false;
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s) {
-            c[s] = p.reset ? mk(0.0f, 0.0f, 0.0f) : mk(acc[s].x, acc[s].y, acc[s].z);
-            n[s] = p.reset ? 0u : f2u(acc[s].w);                  // wgsl:339-350
+            c[s] = kReset ? mk(0.0f, 0.0f, 0.0f) : mk(acc[s].x, acc[s].y, acc[s].z);
+#if RT_SINGLE_NCHK
+            // f2u(acc.w) == ng (wgsl:341) holds for acc.w == f32(ng) (exact below 2^24); any
+            // other stored count — also one that truncates to ng — is traced again below
+            // with f2u(acc.w), which gives the same bits: one compare instead of the
+            // conversion with its saturation selects
+            n[s] = ng;
+            pending[s] = tc[s].valid && !kReset &&
+                         (p.n_exact ? __float_as_uint(acc[s].w) != p.ng_bits
+                                    : f2u(acc[s].w) != ng);
+#else
+            n[s] = kReset ? 0u : f2u(acc[s].w);                   // wgsl:339-350
             pending[s] = tc[s].valid && n[s] != ng;               // a foreign count
+#endif
             any_pending = any_pending || pending[s];
             if (ng < spp) {                                       // wgsl:352-357
                 const v3 num = sub(col[s], c[s]);
                 if (RT_SINGLE_ACC_F64 && ng < (1u << 24) &&
-                    __ballot(tc[s].valid && !acc_f64_ok(num)) == 0ull) {
+                    rt_ballot(tc[s].valid && !acc_f64_ok(num)) == 0ull) {
                     c[s] = acc_f64(c[s], num, p.rcp_hint);
                 } else {
                     const float k = (float)(ng + 1u);             // wgsl:356
@@ -1748,7 +1793,8 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s) pending[s] = tc[s].valid;
     }
-    if (__ballot(any_pending) != 0ull) {
+    const bool wave_pending = rt_ballot(any_pending) != 0ull;
+    if (wave_pending) {
         // pixels whose count is not the hinted one (or no hint): traced with their own
         // count and per-pixel random numbers
         uint32_t seed[S];
@@ -1757,8 +1803,8 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s) {
             if (pending[s]) {
-                c[s] = p.reset ? mk(0.0f, 0.0f, 0.0f) : mk(acc[s].x, acc[s].y, acc[s].z);
-                n[s] = p.reset ? 0u : f2u(acc[s].w);
+                c[s] = kReset ? mk(0.0f, 0.0f, 0.0f) : mk(acc[s].x, acc[s].y, acc[s].z);
+                n[s] = kReset ? 0u : f2u(acc[s].w);
             }
             live[s] = pending[s] && n[s] < spp;                   // wgsl:352
             seed[s] = 1u + n[s] + p.seed_b;                       // wgsl:353
@@ -1791,8 +1837,13 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
     for (uint32_t s = 0; s < S; ++s)
         if (tc[s].valid) {                                        // wgsl:362-363
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            // (every pixel of a wave without a foreign count holds the hinted count after
+            // the frame: f32 of it from the host)
+            const uint32_t nb = (RT_SINGLE_NCHK && p.hinted && !wave_pending)
+                                    ? p.n_after_bits
+                                    : __float_as_uint((float)n[s]);
             const u32x4 v = {__float_as_uint(c[s].x), __float_as_uint(c[s].y),
-                             __float_as_uint(c[s].z), __float_as_uint((float)n[s])};
+                             __float_as_uint(c[s].z), nb};
             __builtin_amdgcn_raw_buffer_store_b128(
                 v, rsrc, (int)(((lane >> 3) * a_width + tc[s].x) * 16u), 0, 16);
         }
@@ -1809,6 +1860,21 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
     sst_put(11, __builtin_amdgcn_s_getreg((31 << 11) | 20));   // XCC_ID
 #endif
     WAVE_TRACE(1);
+}
+
+template <int kPix>
+__global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
+    const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
+    const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
+    const uint32_t* __restrict__ a_order, const SingleParams p) {
+    single_body<kPix, false>(a_cand, a_hx, a_in, a_width, a_height, a_bands, a_order, p);
+}
+template <int kPix>
+__global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single_reset_kernel(
+    const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
+    const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
+    const uint32_t* __restrict__ a_order, const SingleParams p) {
+    single_body<kPix, true>(a_cand, a_hx, a_in, a_width, a_height, a_bands, a_order, p);
 }
 
 // ---- Bounce paths with workgroup-wide compaction (kTraceBounce) -----------------------
@@ -1890,7 +1956,7 @@ __device__ __forceinline__ v3 sky(v3 cf, v3 d) {
 // Workgroup-wide prefix of `live` over the kBounceWaves waves: returns this lane's slot
 // (valid when live) and the total.  Two barriers (counts written, counts read).
 __device__ __forceinline__ uint32_t compact_slot(bool live, uint32_t wave, uint32_t& total) {
-    const unsigned long long m = __ballot(live);
+    const unsigned long long m = rt_ballot(live);
     if ((threadIdx.x & 63u) == 0u) s_bounce.cnt[wave] = (uint32_t)__builtin_popcountll(m);
     __syncthreads();
     uint32_t before = 0, sum = 0;
@@ -2015,7 +2081,7 @@ rt_bounce_kernel(const TraceParams p) {
             // this wave's paths of bounce i (slot = lane for i == 0)
             Hit hit{-1, 0.0f};
             const float4* hs = p.sph;
-            if (__ballot(live) != 0ull) {
+            if (rt_ballot(live) != 0ull) {
                 const bool listed = i == 0u && ncand != kCandNone;
 #if RT_BOUNCE_RELOAD
                 const GridP gp = grid_params(*karg_bounce_params());
@@ -2062,7 +2128,7 @@ rt_bounce_kernel(const TraceParams p) {
             }
             if (!kCompact) {                                      // paths stay in their lane
                 live = keep;
-                if (__ballot(keep) == 0ull) break;
+                if (rt_ballot(keep) == 0ull) break;
                 continue;
             }
             // compact the surviving paths into the first slots (uniform trip count)
@@ -2308,7 +2374,7 @@ __global__ __launch_bounds__(64) void rt_candidates_kernel(const TraceParams p,
         for (uint32_t b = 0; b < kCandGroup; ++b) {             // block-cone survivors
             const uint32_t i = gbase + b * 64u + lane;
             const bool keep = i < count && (!in_blk || !cone_misses(kb, gv[b]));
-            const unsigned long long mask = __ballot(keep);
+            const unsigned long long mask = rt_ballot(keep);
             if (keep) {
                 const uint32_t pos = m + __builtin_amdgcn_mbcnt_hi(
                     (uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -2578,12 +2644,19 @@ static void launch_single(const TraceParams& p, hipStream_t stream) {
     q.count = p.count;
     q.depth = p.depth;
     q.spp = p.spp;
-    q.reset = p.reset_first;
     q.hinted = p.hint_frames != 0u;
     q.n_hint = p.hint_n[0];
     q.seed_b = p.seed_b[0];
     q.hy_off = (uint32_t)(p.hy - p.hx);
     q.rcp_hint = p.hint_rcp[0];
+    {
+        const uint32_t ng = q.n_hint;
+        const uint32_t after = ng < q.spp ? ng + 1u : ng;           // wgsl:352-357
+        const float fng = (float)ng, faft = (float)after;
+        std::memcpy(&q.ng_bits, &fng, 4);
+        std::memcpy(&q.n_after_bits, &faft, 4);
+        q.n_exact = ng < (1u << 24) ? 1u : 0u;
+    }
     q.rs = p.hint_rs[0];
     for (int k = 0; k < 8; ++k) q.disk_rcp[k] = p.disk_rcp[k];
     for (int i = 0; i < 3; ++i) {
@@ -2595,9 +2668,14 @@ static void launch_single(const TraceParams& p, hipStream_t stream) {
         q.ddv[i] = p.ddv[i];
     }
     q.defocus_angle = p.defocus_angle;
-    hipLaunchKernelGGL(rt_single_kernel<kPix>, grid, dim3(64 * kSingleWg), 0, stream, p.cand,
-                       p.hx, p.in, p.width, p.height, pack_bands(p.band_first, p.band_step, false),
-                       p.wg_order, q);
+    if (p.reset_first)
+        hipLaunchKernelGGL(rt_single_reset_kernel<kPix>, grid, dim3(64 * kSingleWg), 0, stream,
+                           p.cand, p.hx, p.in, p.width, p.height,
+                           pack_bands(p.band_first, p.band_step, false), p.wg_order, q);
+    else
+        hipLaunchKernelGGL(rt_single_kernel<kPix>, grid, dim3(64 * kSingleWg), 0, stream,
+                           p.cand, p.hx, p.in, p.width, p.height,
+                           pack_bands(p.band_first, p.band_step, false), p.wg_order, q);
 }
 
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
