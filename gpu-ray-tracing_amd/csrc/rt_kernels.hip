@@ -737,7 +737,8 @@ __device__ __forceinline__ void init_disk_rcp(const TraceParams& p) {
 // register form with the IEEE division for all 2^32 seeds.)
 __device__ __forceinline__ double disk_rcp_reg(float len2) {
     const uint32_t m = (0x3F800001u - __float_as_uint(len2)) >> 1;
-    const uint32_t lo = (m << 28) | ((m * m) << 4);
+    // (m <= 3 on the domain: a 24-bit multiply, v_mul_u32_u24, instead of v_mul_lo_u32)
+    const uint32_t lo = (m << 28) | (__umul24(m, m) << 4);
     return __hiloint2double(0x3FF00000, (int)lo);
 }
 // kTable: 0 = sqrt_core / div_core, 1 = the LDS table (s_disk_rcp), 2 = disk_rcp_reg
@@ -1431,6 +1432,14 @@ constexpr uint32_t kSingleWg = RT_SINGLE_WG;
 #define RT_SINGLE_DISK 2
 #endif
 constexpr int kSingleDisk = RT_SINGLE_DISK;
+// hash(x*73) ^ hash(y*51) (wgsl:309-310) of the one-frame kernel: from the per-column /
+// per-row tables (two dependent loads behind the order entry) or computed in the wave —
+// one hash per lane (lanes [0, 8*kPix) the wave's columns, the next 8 its rows), handed to
+// the pixels with ds_bpermute — so the camera rays need no memory at all.  Bit k set =
+// computed in the kPix = k + 1 instance.
+#ifndef RT_SINGLE_HASH
+#define RT_SINGLE_HASH 0
+#endif
 
 
 // Shading of a camera ray's hit at depth 1 (ray_color's loop body at i = 0, wgsl:266-286):
@@ -1683,10 +1692,19 @@ __device__ __forceinline__ void single_body(
     float4 acc[S], bv[S];
     __shared__ float4 s_blk[kSingleWg * kPix * kCandStride];
     float4* lblk = s_blk + wave * S * kCandStride;
-    const uint32_t hy = a_hx[p.hy_off + min(band_first * RT_STRIPE_ROWS +
-                                                lband * band_step * RT_STRIPE_ROWS +
-                                                (lane >> 3),
-                                            a_height - 1u)];
+    constexpr bool kHash = (RT_SINGLE_HASH >> (kPix - 1)) & 1;
+    uint32_t hy = 0u, hv = 0u;
+    if (kHash) {
+        // (all 64 lanes active here: ds_bpermute reads every lane)
+        const uint32_t row = (band_first + lband * band_step) * RT_STRIPE_ROWS + lane - 8u * S;
+        const bool col = lane < 8u * S;                           // (selects, no branch)
+        hv = hash((col ? tx0 * 8u + lane : row) * (col ? 73u : 51u));    // wgsl:309-310
+        hy = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((8u * S + (lane >> 3)) * 4u), (int)hv);
+    } else {
+        hy = a_hx[p.hy_off + min(band_first * RT_STRIPE_ROWS +
+                                     lband * band_step * RT_STRIPE_ROWS + (lane >> 3),
+                                 a_height - 1u)];
+    }
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
         const uint32_t tx = tx0 + s;
@@ -1695,7 +1713,11 @@ __device__ __forceinline__ void single_body(
         tc[s] = tile_coord(a_width, a_height, band_first, band_step, tx, lband, lane);
         blk[s] = a_cand + (size_t)tile * kCandStride;
         ncand[s] = in ? load_cnt(a_cand, tile) : 0u;
-        hxy[s] = a_hx[min(tc[s].x, a_width - 1u)] ^ hy;           // wgsl:309-310
+        const uint32_t hx =
+            kHash ? (uint32_t)__builtin_amdgcn_ds_bpermute((int)((8u * s + (lane & 7u)) * 4u),
+                                                           (int)hv)
+                  : a_hx[min(tc[s].x, a_width - 1u)];
+        hxy[s] = hx ^ hy;                                         // wgsl:309-310
     }
     // (issued after the seed-table loads: vmcnt waits in issue order, and the camera rays
     // need the seeds long before the scan and the accumulation need these)

@@ -17,6 +17,3 @@ for v in default nv nvm8; do
   env $E RT_FPL=1 timeout -k 10 300 python tools/rank_sim.py K3 100 > $O/rank_k3_dispatch_$v.jsonl 2>&1 || exit 1
   echo k3 $v; grep '^{' $O/rank_k3_dispatch_$v.jsonl
 done
-RT_HIP_LIB=$V/librt_hip_sst.so timeout -k 10 200 python tools/stamps_single.py K3 1,8,135 \
-  > $O/stamps_K3.jsonl 2>&1 || { echo "stamps failed"; tail $O/stamps_K3.jsonl; exit 1; }
-grep '^{' $O/stamps_K3.jsonl | cut -c1-300
