@@ -91,6 +91,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--config", default="K3", choices=sorted(CONFIGS))
+    ap.add_argument("--queues", type=int, default=int(os.environ.get("RT_QUEUES", "0")),
+                    help="concurrent parts per one-frame update (rt_set_update_queues; "
+                         "0 = the library's choice)")
     ap.add_argument("--scan", default="culled", choices=["culled", "exhaustive"],
                     help="sphere-list scan: exact culling (default) or the reference's "
                          "exhaustive linear walk; images are bit-identical")
@@ -270,6 +273,7 @@ def main():
     pipe.set_spheres(spheres)
     if dispatch:
         pipe.set_frames_per_launch(1)          # one `update` launch per frame
+    pipe.set_update_queues(args.queues)
     # the job's one gather: RCCL behind the C ABI (rt_comm_create + rt_gather_stripes)
     use_abi = world > 1 and backend == "nccl" and os.environ.get("RT_GATHER", "abi") == "abi"
     comm = StripeComm.from_process_group(pipe) if use_abi else None
@@ -339,7 +343,10 @@ def main():
     # frame); 64-spp configs: one call per step, all alike
     total_launches = info["launches"] * (1 if dispatch else args.steps)
     launches_per_step = total_launches / args.steps
-    launch_s = ev0.elapsed_time(ev1) / 1e3 / max(1, total_launches)
+    # a one-frame update may run as `queues` concurrent launches (parts of the image on
+    # their own streams): the roofline's unit is then the update, all its parts together
+    queues = max(1, info.get("queues", 1))
+    launch_s = ev0.elapsed_time(ev1) / 1e3 / max(1, total_launches // queues)
     value = w * h * spf * args.steps / dt / 1e6
 
     # roofline of the timed trace kernel
@@ -354,6 +361,7 @@ def main():
             "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
             "kernel": kernel, "kernel_avg_us": round(launch_s * 1e6, 2),
             "frames_per_launch": fpl, "launches_per_step": launches_per_step,
+            "queues": queues,
             "algorithmic_bytes_per_launch": bytes_launch,
             "binding": "valu",
             # the same bytes against the measured streaming floor of the pattern (no tracing)

@@ -51,6 +51,8 @@ struct rt_ctx {
     uint32_t* wg_buf = nullptr;      // cost + order words
     uint64_t wg_cap = 0;
     uint32_t wg_pix = 0;
+    uint32_t wg_parts = 0;           // sub-lists the order was dealt into
+    uint64_t wg_builds = 0;          // order launches so far (a new order needs a new fork)
     uint64_t band_gen = ~0ull, band_seen_gen = ~0ull;
     uint64_t cand_tiles = 0;        // allocated tiles
     uint64_t cand_live = 0;         // tiles of the current lists
@@ -80,10 +82,16 @@ struct rt_ctx {
     };
     std::vector<CountRecord> counts;
     uint32_t frames_per_launch = 0;  // rt_update_frames fusion cap (0 = automatic)
-    rt_launch_info last = {0, 0, 0, -1};  // the last call's launches (rt_last_launch_info)
+    rt_launch_info last = {0, 0, 0, -1, 0};  // the last call's launches (rt_last_launch_info)
     int path_compaction = RT_PATHS_AUTO;
     int frame_pairs = RT_FRAME_PAIRS_AUTO;
     int single_kernel = RT_SINGLE_AUTO;
+    // Concurrent parts of one-frame updates (rt_set_update_queues): part 0 on the caller's
+    // stream, part k on aux[k - 1], forked and joined through events.
+    uint32_t update_queues = 0;      // 0 = automatic
+    hipStream_t aux[RT_MAX_UPDATE_QUEUES - 1] = {};
+    hipEvent_t fork_ev = nullptr;
+    hipEvent_t join_ev[RT_MAX_UPDATE_QUEUES - 1] = {};
 };
 
 namespace {
@@ -574,6 +582,7 @@ rt_status plan_tile_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
 // rtk::launch_wg_order).  Built on the second launch of a generation (a camera that moves
 // every frame never pays for it); rt_set_tile_order(OFF) keeps raster order.
 rt_status plan_wg_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t stream) {
+    const uint32_t parts = p.parts > 1u ? p.parts : 1u;
     p.wg_order = nullptr;
     if ((kernel != rtk::kTraceSingle && kernel != rtk::kTraceSingleOne) || p.cand_k == 0 ||
         p.local_bands < 2 || ctx->tile_order_mode == RT_TILE_ORDER_OFF)
@@ -586,6 +595,7 @@ rt_status plan_wg_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_
         }
         ctx->band_gen = gen;
         ctx->wg_pix = 0;
+        ctx->wg_parts = 0;
     }
     const uint32_t pix = kernel == rtk::kTraceSingle ? rtk::single_pix() : 1u;
     const uint32_t per = rtk::single_wg_tiles(pix);
@@ -601,11 +611,13 @@ rt_status plan_wg_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_
         ctx->wg_cap = units;
         ctx->wg_pix = 0;
     }
-    if (ctx->wg_pix != pix) {
+    if (ctx->wg_pix != pix || ctx->wg_parts != parts) {
         hipError_t e = rtk::launch_wg_order(p.cand, (p.width + 7u) >> 3, p.local_bands, pix,
-                                            ctx->wg_buf, ctx->wg_buf + units, stream);
+                                            ctx->wg_buf, ctx->wg_buf + units, stream, parts);
         if (e != hipSuccess) return hip_fail(e, "workgroup order launch");
         ctx->wg_pix = pix;
+        ctx->wg_parts = parts;
+        ctx->wg_builds++;
     }
     p.wg_order = ctx->wg_buf + units;
     return RT_OK;
@@ -811,8 +823,54 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
     return RT_OK;
 }
 
-void note_launch(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t frames) {
-    ctx->last.launches++;
+// Concurrent parts of a one-frame update (rt_set_update_queues).  AUTO: one launch.
+uint32_t update_parts(const rt_ctx* ctx, const rtk::TraceParams& p, int kernel) {
+    if ((kernel != rtk::kTraceSingle && kernel != rtk::kTraceSingleOne) || p.frames != 1u)
+        return 1u;
+    const uint32_t q = ctx->update_queues ? ctx->update_queues : 1u;
+    return std::max(1u, std::min(q, p.local_bands));
+}
+
+// The context's extra streams and fork/join events (created on first use, on ctx->device).
+rt_status ensure_aux_streams(rt_ctx* ctx, uint32_t n) {
+    if (!ctx->fork_ev) {
+        hipError_t e = hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming);
+        if (e != hipSuccess) return hip_fail(e, "hipEventCreateWithFlags");
+    }
+    for (uint32_t k = 0; k < n; ++k) {
+        if (!ctx->aux[k]) {
+            hipError_t e = hipStreamCreateWithFlags(&ctx->aux[k], hipStreamNonBlocking);
+            if (e != hipSuccess) return hip_fail(e, "hipStreamCreateWithFlags");
+        }
+        if (!ctx->join_ev[k]) {
+            hipError_t e = hipEventCreateWithFlags(&ctx->join_ev[k], hipEventDisableTiming);
+            if (e != hipSuccess) return hip_fail(e, "hipEventCreateWithFlags");
+        }
+    }
+    return RT_OK;
+}
+
+// aux[0..n) wait for everything issued on `stream` so far
+rt_status fork_aux(rt_ctx* ctx, uint32_t n, hipStream_t stream) {
+    hipError_t e = hipEventRecord(ctx->fork_ev, stream);
+    for (uint32_t k = 0; e == hipSuccess && k < n; ++k) e = hipStreamWaitEvent(ctx->aux[k], ctx->fork_ev, 0);
+    return e == hipSuccess ? RT_OK : hip_fail(e, "fork (hipEventRecord / hipStreamWaitEvent)");
+}
+
+// `stream` waits for everything issued on aux[0..n) so far
+rt_status join_aux(rt_ctx* ctx, uint32_t n, hipStream_t stream) {
+    hipError_t e = hipSuccess;
+    for (uint32_t k = 0; e == hipSuccess && k < n; ++k) {
+        e = hipEventRecord(ctx->join_ev[k], ctx->aux[k]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, ctx->join_ev[k], 0);
+    }
+    return e == hipSuccess ? RT_OK : hip_fail(e, "join (hipEventRecord / hipStreamWaitEvent)");
+}
+
+void note_launch(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t frames,
+                 uint32_t parts = 1u) {
+    ctx->last.launches += parts;
+    ctx->last.queues = parts;
     ctx->last.frames += frames;
     ctx->last.max_frames_per_launch = std::max(ctx->last.max_frames_per_launch, frames);
     ctx->last.kernel = kernel != rtk::kTraceBounce ? kernel : RT_KERNEL_BOUNCE + (int)p.compact;
@@ -835,7 +893,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         return s;
     const float4* src = reinterpret_cast<const float4*>(in);
     float4* dst = reinterpret_cast<float4*>(out);
-    ctx->last = {0, 0, 0, -1};
+    ctx->last = {0, 0, 0, -1, 0};
     for (uint32_t f0 = 0; f0 < frames; f0 += rtk::kMaxFramesPerLaunch) {
         const uint32_t nf = std::min<uint32_t>(frames - f0, rtk::kMaxFramesPerLaunch);
         p.in = src;
@@ -937,6 +995,11 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->d_grid);
         (void)hipFree(ctx->wg_buf);
         free_candidates(ctx);
+        for (uint32_t k = 0; k + 1 < RT_MAX_UPDATE_QUEUES; ++k) {
+            if (ctx->aux[k]) (void)hipStreamDestroy(ctx->aux[k]);
+            if (ctx->join_ev[k]) (void)hipEventDestroy(ctx->join_ev[k]);
+        }
+        if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
     }
     delete ctx;
     return RT_OK;
@@ -980,6 +1043,14 @@ rt_status rt_set_single_kernel(rt_ctx* ctx, int mode) {
         mode != RT_SINGLE_ONE)
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown single-kernel mode");
     ctx->single_kernel = mode;
+    return RT_OK;
+}
+
+rt_status rt_set_update_queues(rt_ctx* ctx, uint32_t queues) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (queues > RT_MAX_UPDATE_QUEUES)
+        return fail(RT_ERR_INVALID_ARGUMENT, "queues above RT_MAX_UPDATE_QUEUES");
+    ctx->update_queues = queues;
     return RT_OK;
 }
 
@@ -1066,7 +1137,9 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
     // instances run one frame per launch.
     const uint32_t per = frames_per_launch_for(ctx, p);
     int cur = 0;
-    ctx->last = {0, 0, 0, -1};
+    ctx->last = {0, 0, 0, -1, 0};
+    uint32_t aux_live = 0;      // aux streams with work of this call not yet joined
+    bool forked = false;        // aux streams ordered after the last work on `stream`
     for (uint32_t f0 = 0; f0 < frames; f0 += per) {
         const uint32_t nf = std::min<uint32_t>(per, frames - f0);
         p.in = img[cur];
@@ -1102,12 +1175,37 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
             kernel = quad ? rtk::kTraceListQuad : rtk::kTraceListPair;
         }
         kernel = single_or(ctx, p, kernel);
+        const uint32_t parts = update_parts(ctx, p, kernel);
+        p.parts = parts;
+        p.part = 0;
+        if (parts == 1u && aux_live) {          // back to one launch: wait for the parts
+            if (rt_status s = join_aux(ctx, aux_live, stream)) return s;
+            aux_live = 0;
+            forked = false;
+        }
+        const uint64_t builds = ctx->wg_builds;
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         if (rt_status s = plan_wg_order(ctx, p, kernel, stream)) return s;
-        hipError_t e = rtk::launch_trace(p, kernel, stream);
-        if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
+        if (parts > 1u) {
+            // every part's next frame reads only the pixels its own previous frame wrote;
+            // what `stream` prepared (lists, order, the input image) is forked to the others
+            if (rt_status s = ensure_aux_streams(ctx, parts - 1u)) return s;
+            if (!forked || ctx->wg_builds != builds) {
+                if (rt_status s = fork_aux(ctx, parts - 1u, stream)) return s;
+                forked = true;
+            }
+            for (uint32_t k = 0; k < parts; ++k) {
+                p.part = k;
+                hipError_t e = rtk::launch_trace(p, kernel, k ? ctx->aux[k - 1] : stream);
+                if (e != hipSuccess) return hip_fail(e, "rt_single_kernel launch");
+            }
+            aux_live = std::max(aux_live, parts - 1u);
+        } else {
+            hipError_t e = rtk::launch_trace(p, kernel, stream);
+            if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
+        }
         finish_tile_order(ctx, p);
-        note_launch(ctx, p, kernel, nf);
+        note_launch(ctx, p, kernel, nf, parts);
         // frame f of the launch wrote img[(cur + 1 + f) % 2]
         const int newest = (nf & 1u) ? 1 - cur : cur;
         if (known) {
@@ -1119,6 +1217,8 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         }
         cur = newest;
     }
+    if (aux_live)   // the call's work ends on the caller's stream
+        if (rt_status s = join_aux(ctx, aux_live, stream)) return s;
     if (out_newest) *out_newest = cur;
     return RT_OK;
 }

@@ -58,6 +58,11 @@ struct TraceParams {
     // one-frame launches (rt_single_kernel): workgroup u traces (band << 16 | column group)
     // wg_order[u] (launch_wg_order), null = natural order
     const uint32_t* wg_order;
+    // one-frame launches: this launch is part `part` of `parts` concurrent parts of the
+    // update (rt_set_update_queues), each on its own stream: the wg_order list's sub-list
+    // `part` (launch_wg_order with `parts`), or without an order every parts-th local band
+    // from band `part`.  parts <= 1: the whole update.
+    uint32_t part, parts;
     // Uniform XZ grid over the small spheres for bounce rays (rt_kernels.hip scan_grid;
     // built by rt_abi.cpp build_grid): per cell the range of its items, each item a copy
     // of the sphere's scan record and its index (every small sphere is registered in the
@@ -178,8 +183,15 @@ hipError_t launch_candidates(const TraceParams& p, float4* cand, hipStream_t str
 // candidate-list load (per tile 4 + count for a tile with a list, 64 for a tile without
 // one), sorted by launch_tile_order's buckets;
 // wg_cost is scratch of one word per workgroup.
+// parts > 1: dealt round-robin into `parts` contiguous sub-lists (part_range).
 hipError_t launch_wg_order(const float4* cand, uint32_t tiles_x, uint32_t bands, uint32_t pix,
-                           uint32_t* wg_cost, uint32_t* wg_order, hipStream_t stream);
+                           uint32_t* wg_cost, uint32_t* wg_order, hipStream_t stream,
+                           uint32_t parts);
+// [first, first + len) of sub-list k of n entries dealt round-robin into `parts` sub-lists
+inline void part_range(uint32_t n, uint32_t parts, uint32_t k, uint32_t& first, uint32_t& len) {
+    first = k * (n / parts) + (k < n % parts ? k : n % parts);
+    len = n / parts + (k < n % parts ? 1u : 0u);
+}
 uint32_t single_wg_tiles(uint32_t pix);
 uint32_t single_pix();   // tiles per wave of kTraceSingle
 hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t width,
@@ -195,7 +207,8 @@ const char* single_kernel_name(uint32_t pix);
 // tile_order for launch_trace: the local tiles by decreasing recorded cost (quantised
 // log2 of tile_cost), so the slowest tiles start first and the cheap ones fill the tail.
 hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, uint32_t tiles,
-                             uint32_t tiles_x, hipStream_t stream, uint32_t snake = 0);
+                             uint32_t tiles_x, hipStream_t stream, uint32_t snake = 0,
+                             uint32_t parts = 1);
 // Exact fast-path self-test (rt_selftest_fastmath): cnt[5] device counters, zeroed.
 hipError_t launch_selftest(unsigned long long* cnt, uint64_t n_rand, hipStream_t stream);
 

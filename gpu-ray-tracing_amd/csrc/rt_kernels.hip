@@ -1361,6 +1361,9 @@ struct SingleParams {
     // RT_SINGLE_NCHK: n_hint < 2^24 (n_exact), the bits of f32(n_hint) and of f32(the count
     // after the frame): a pixel holding exactly f32(n_hint) holds the hinted count
     uint32_t n_exact, ng_bits, n_after_bits;
+    // local bands of a launch in raster order (no a_order): lband = first + blockIdx.y *
+    // step, first | step << 16 — one of the update's concurrent parts (launch_single)
+    uint32_t lbands;
     float4 rs;             // (rf(sb), random_unit_vector(sb)) of frame 0, bounce 0
     double disk_rcp[8];
     float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3];
@@ -1676,7 +1679,7 @@ __device__ __forceinline__ void single_body(
     const uint32_t tiles_x = (a_width + 7u) >> 3;
     // workgroups by decreasing candidate-list load (wg_order, launch_wg_order): the
     // costliest are dispatched first and the cheap ones fill the tail
-    uint32_t gx = blockIdx.x, lband = blockIdx.y;
+    uint32_t gx = blockIdx.x, lband = (p.lbands & 0xFFFFu) + blockIdx.y * (p.lbands >> 16);
     if (a_order) {   // (a leading, preloadable argument: one scalar load to the entry)
         const uint32_t e = __builtin_amdgcn_readfirstlane(
             a_order[blockIdx.y * gridDim.x + blockIdx.x]);
@@ -2224,6 +2227,14 @@ rt_bounce_kernel(const TraceParams p) {
 // snake > 0: the sorted list is dealt in runs of `snake`, every second run reversed (the
 // costliest of run 2 pairs with the cheapest of run 1 on the dispatcher's round-robin over
 // CUs), for launches of a few workgroups per CU.
+// parts > 1: the sorted list is dealt round-robin into `parts` contiguous sub-lists (entry
+// pos to part pos % parts), one per concurrent part of a one-frame update (launch_single):
+// every part gets the same mix of costly and cheap workgroups, costliest first.
+__device__ __forceinline__ uint32_t part_pos(uint32_t pos, uint32_t n, uint32_t parts) {
+    if (parts <= 1u) return pos;
+    const uint32_t k = pos % parts, j = pos / parts;
+    return k * (n / parts) + min(k, n % parts) + j;
+}
 __device__ __forceinline__ uint32_t snake_pos(uint32_t pos, uint32_t n, uint32_t g) {
     if (g == 0u) return pos;
     const uint32_t c = pos / g, j = pos - c * g;
@@ -2234,7 +2245,7 @@ __device__ __forceinline__ uint32_t snake_pos(uint32_t pos, uint32_t n, uint32_t
 __global__ __launch_bounds__(1024) void rt_tile_order_kernel(const uint32_t* __restrict__ cost,
                                                              uint32_t* __restrict__ order,
                                                              uint32_t tiles, uint32_t tiles_x,
-                                                             uint32_t snake) {
+                                                             uint32_t snake, uint32_t parts) {
     constexpr uint32_t kBuckets = 128, kWaves = 16, kSlots = kBuckets * kWaves;
     __shared__ uint32_t hist[kSlots];          // [bucket][wave]
     __shared__ uint32_t scan[1024];
@@ -2291,17 +2302,19 @@ __global__ __launch_bounds__(1024) void rt_tile_order_kernel(const uint32_t* __r
             const uint32_t t = t0 + k * 1024u;
             if (t < tiles) {
                 const uint32_t pos = atomicAdd(&hist[bucket(c[k]) * kWaves + wave], 1u);
-                order[snake_pos(pos, tiles, snake)] = ((t / tiles_x) << 16) | (t % tiles_x);
+                order[part_pos(snake_pos(pos, tiles, snake), tiles, parts)] =
+                    ((t / tiles_x) << 16) | (t % tiles_x);
             }
         }
     }
 }
 
 hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, uint32_t tiles,
-                             uint32_t tiles_x, hipStream_t stream, uint32_t snake) {
+                             uint32_t tiles_x, hipStream_t stream, uint32_t snake,
+                             uint32_t parts) {
     if (tiles == 0) return hipSuccess;
     hipLaunchKernelGGL(rt_tile_order_kernel, dim3(1), dim3(1024), 0, stream, tile_cost,
-                       tile_order, tiles, tiles_x, snake);
+                       tile_order, tiles, tiles_x, snake, parts);
     return hipGetLastError();
 }
 
@@ -2656,10 +2669,27 @@ template <int kPix>
 static void launch_single(const TraceParams& p, hipStream_t stream) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     const uint32_t per = kSingleWg * kPix;
-    const dim3 grid((tiles_x + per - 1u) / per, p.local_bands);
+    const uint32_t cols = (tiles_x + per - 1u) / per;
+    const uint32_t parts = p.parts > 1u ? p.parts : 1u, part = parts > 1u ? p.part : 0u;
+    // this part's workgroups: its sub-list of the order, or every parts-th local band
+    dim3 grid(cols, p.local_bands);
+    const uint32_t* order = p.wg_order;
+    uint32_t lbands = 1u << 16;
+    if (parts > 1u) {
+        if (order) {
+            uint32_t first = 0, len = 0;
+            part_range(cols * p.local_bands, parts, part, first, len);
+            grid = dim3(len, 1);
+            order += first;
+        } else {
+            grid.y = p.local_bands > part ? (p.local_bands - part + parts - 1u) / parts : 0u;
+            lbands = part | (parts << 16);
+        }
+    }
     if (grid.x == 0 || grid.y == 0) return;
     SingleParams q;
     std::memset(&q, 0, sizeof(q));
+    q.lbands = lbands;
     q.out = p.out;
     q.geom = p.geom;
     q.sph = p.sph;
@@ -2693,11 +2723,11 @@ static void launch_single(const TraceParams& p, hipStream_t stream) {
     if (p.reset_first)
         hipLaunchKernelGGL(rt_single_reset_kernel<kPix>, grid, dim3(64 * kSingleWg), 0, stream,
                            p.cand, p.hx, p.in, p.width, p.height,
-                           pack_bands(p.band_first, p.band_step, false), p.wg_order, q);
+                           pack_bands(p.band_first, p.band_step, false), order, q);
     else
         hipLaunchKernelGGL(rt_single_kernel<kPix>, grid, dim3(64 * kSingleWg), 0, stream,
                            p.cand, p.hx, p.in, p.width, p.height,
-                           pack_bands(p.band_first, p.band_step, false), p.wg_order, q);
+                           pack_bands(p.band_first, p.band_step, false), order, q);
 }
 
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
@@ -2735,7 +2765,8 @@ uint32_t single_wg_tiles(uint32_t pix) { return kSingleWg * pix; }
 uint32_t single_pix() { return kSinglePix; }
 
 hipError_t launch_wg_order(const float4* cand, uint32_t tiles_x, uint32_t bands, uint32_t pix,
-                           uint32_t* wg_cost, uint32_t* wg_order, hipStream_t stream) {
+                           uint32_t* wg_cost, uint32_t* wg_order, hipStream_t stream,
+                           uint32_t parts) {
     const uint32_t per = kSingleWg * pix;
     const uint32_t cols = (tiles_x + per - 1u) / per;
     const uint32_t units = cols * bands;
@@ -2744,7 +2775,7 @@ hipError_t launch_wg_order(const float4* cand, uint32_t tiles_x, uint32_t bands,
                        tiles_x, cols, per, units, wg_cost);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_tile_order(wg_cost, wg_order, units, cols, stream, RT_WG_SNAKE);
+    return launch_tile_order(wg_cost, wg_order, units, cols, stream, RT_WG_SNAKE, parts);
 }
 
 hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream) {

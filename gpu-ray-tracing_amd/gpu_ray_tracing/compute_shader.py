@@ -79,6 +79,11 @@ class ComputeShaderPipeline:
         per-tile durations) or "off" (raster order)."""
         _lib.call("rt_set_tile_order", self._ctx, {"auto": 0, "off": 1}[mode])
 
+    def set_update_queues(self, queues: int) -> None:
+        """rt_set_update_queues: one-frame updates of update_frames as `queues` concurrent
+        parts on their own streams (0 = automatic, 1 = one launch per update)."""
+        _lib.call("rt_set_update_queues", self._ctx, int(queues))
+
     def set_path_compaction(self, mode: str) -> None:
         """rt_set_path_compaction for bounce launches: "auto" (default), "per_wave",
         "compact" (paths repacked across four waves after every bounce) or "pair" (two waves

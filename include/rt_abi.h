@@ -158,7 +158,7 @@ typedef struct rt_ctx rt_ctx;
 
 /* Version / introspection ------------------------------------------------------------ */
 RT_API uint32_t rt_abi_version(void); /* RT_ABI_VERSION */
-#define RT_ABI_VERSION 1u
+#define RT_ABI_VERSION 2u
 /* Text of the last error on this thread (never NULL). */
 RT_API const char* rt_last_error(void);
 /* Trace-kernel instances (rt_launch_info.kernel) and their names as rocprofv3 lists them
@@ -185,13 +185,15 @@ RT_API const char* rt_last_error(void);
  * "rt_single_kernel<p>"), "rt_trace_kernel" for an unknown id. */
 RT_API const char* rt_kernel_name(int which);
 /* What the last rt_update / rt_render / rt_render_stripes / rt_update_frames call on this
- * context launched: trace launches, frames traced, the most frames one launch carried and
- * the instance of its last launch (RT_KERNEL_*, -1 before any launch). */
+ * context launched: trace launches, frames traced, the most frames one launch carried, the
+ * instance of its last launch (RT_KERNEL_*, -1 before any launch) and the concurrent parts
+ * (streams) its last frame ran as (rt_set_update_queues; each part is one launch). */
 typedef struct rt_launch_info {
     uint32_t launches;
     uint32_t frames;
     uint32_t max_frames_per_launch;
     int32_t kernel;
+    uint32_t queues;
 } rt_launch_info;
 RT_API rt_status rt_last_launch_info(const rt_ctx* ctx, rt_launch_info* out);
 /* Diagnostic: the per-tile candidate lists of camera rays the context built last (culled
@@ -294,6 +296,16 @@ RT_API rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode);
 #define RT_TILE_ORDER_AUTO 0
 #define RT_TILE_ORDER_OFF 1
 RT_API rt_status rt_set_tile_order(rt_ctx* ctx, int mode);
+/* One-frame updates of rt_update_frames (rt_set_frames_per_launch(1), the one-frame
+ * instances) as `queues` concurrent parts, each a launch on its own stream: the caller's
+ * stream runs part 0, context-owned streams the others, forked from and joined back into
+ * the caller's stream by events inside the call (the call's work stays ordered on the
+ * caller's stream).  Each part takes every queues-th workgroup of the cost order (or every
+ * queues-th band), so a part's next frame depends only on its own previous frame: one
+ * part's kernel boundary and tail overlap the other parts' work.  0 = automatic, 1 = one
+ * launch per update, at most RT_MAX_UPDATE_QUEUES.  Pixel results are identical. */
+#define RT_MAX_UPDATE_QUEUES 4u
+RT_API rt_status rt_set_update_queues(rt_ctx* ctx, uint32_t queues);
 /* Bounce paths (max_depth >= 2): RT_PATHS_PER_WAVE keeps every path in the wave of its
  * pixel (one tile per workgroup); RT_PATHS_PAIR runs two waves per tile on alternate
  * frames, the second handing its colours to the first through LDS (shorter chains for

@@ -185,6 +185,48 @@ def test_bench_dispatch_chain_matches_fixture(rt, cfg, single):
         p.close()
 
 
+@pytest.mark.parametrize("order", ["auto", "off"])
+@pytest.mark.parametrize("single", ["auto", "one"])
+def test_update_queues_match_one_launch(rt, single, order):
+    """rt_set_update_queues: one-frame updates as 2-4 concurrent parts on their own streams
+    (each part every queues-th workgroup of the cost order, or every queues-th band when
+    the order is off) leave both ping-pong images bit-identical to one launch per update —
+    whole image and a rank share, across the reset frame, the order's first build and a
+    second call — and match the oracle's sampled pixels (tests/golden/bench_k3.npz)."""
+    g = load_golden("bench_k3.npz")
+    w, h = int(g["width"]), int(g["height"])
+    cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
+    cam_t = cam.with_fields(camera_has_moved=0.0)
+    p = rt.ComputeShaderPipeline(0)
+    p.set_frames_per_launch(1)
+    p.set_single_kernel(single)
+    p.set_tile_order(order)
+    try:
+        for rank, nranks in ((0, 1), (3, 8)):
+            rows = rt.stripe_local_rows(h, rank, nranks)
+            ref = None
+            for q in (1, 2, 3, 4):
+                p.set_update_queues(q)
+                a, b = p.new_image(w, rows), p.new_image(w, rows)
+                n0 = p.update_frames(a, b, w, h, cam, sc, g["seeds"][:5], rank, nranks)
+                if n0 == 1:
+                    a, b = b, a
+                newest = p.update_frames(a, b, w, h, cam_t, sc, g["seeds"][5:25], rank, nranks)
+                info = p.last_launch_info()
+                assert info["queues"] == q and info["launches"] == 20 * q, (q, info)
+                imgs = (host(b if newest == 1 else a), host(a if newest == 1 else b))
+                if ref is None:
+                    ref = imgs
+                    if nranks == 1:
+                        k = list(g["frame_counts"]).index(25)
+                        assert_same(imgs[0][g["py"], g["px"]], g["pixels"][k])
+                else:
+                    for x, y in zip(imgs, ref):
+                        assert_same(x, y)
+    finally:
+        p.close()
+
+
 def test_bench_k5_launches_match_golden(rt):
     """bench.py --config K5's timed structure on one GPU: rt_update_frames of 64 frames
     (the bounce instance, all 64 fused in one launch) at 3840x2160, depth 8, sampled

@@ -10,7 +10,7 @@ TAG=$1; CFGS=$2
 cd $GRAFT_REPO_ROOT; O=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
 for c in $CFGS; do
-  ARGS="--config $c --side 0 --cpu-seconds 0"
+  ARGS="--config $c --side 0 --cpu-seconds 0 --queues 1"
   [ "$c" = "K5" ] && ARGS="$ARGS --steps 1 --warmup 1"
   timeout -k 10 300 python3 bench.py $ARGS > $O/pmc_bench_$c.json 2> $O/pmc_bench_$c.err \
     || { echo "bench $c failed"; tail -3 $O/pmc_bench_$c.err; exit 1; }
