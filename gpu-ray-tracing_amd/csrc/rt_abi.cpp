@@ -823,11 +823,20 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
     return RT_OK;
 }
 
-// Concurrent parts of a one-frame update (rt_set_update_queues).  AUTO: one launch.
+// Concurrent parts of a one-frame update (rt_set_update_queues).  AUTO by the launch's
+// tiles (profiles/r03e_ab_queues.log, r03e_rank_sim_k3_q*.jsonl; µs per K3 update at 1 / 2
+// / 3 / 4 parts: whole image 22.7 / 19.6 / 19.6 / 19.0, K2 15.9 / 13.6 / 13.5 / 13.5; a
+// 2-rank share 12.5 / 11.4 / 11.5; 4-rank 7.8 / 7.5 / 9.7; 8-rank 5.9 / 7.9 / 10.9): each
+// part costs the host one more launch, which small shares cannot hide.
+constexpr uint64_t kQueues4MinTiles = 20000, kQueues2MinTiles = 12000;
 uint32_t update_parts(const rt_ctx* ctx, const rtk::TraceParams& p, int kernel) {
     if ((kernel != rtk::kTraceSingle && kernel != rtk::kTraceSingleOne) || p.frames != 1u)
         return 1u;
-    const uint32_t q = ctx->update_queues ? ctx->update_queues : 1u;
+    uint32_t q = ctx->update_queues;
+    if (q == 0) {
+        const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
+        q = tiles >= kQueues4MinTiles ? 4u : tiles >= kQueues2MinTiles ? 2u : 1u;
+    }
     return std::max(1u, std::min(q, p.local_bands));
 }
 

@@ -1,0 +1,64 @@
+// Host cost of issuing kernels (diagnostic): an empty kernel with a small and with a
+// 320-byte argument block, launched N times back to back on one stream and round-robin over
+// 2 / 4 streams; prints the host time per launch (the issuing loop alone) and the GPU time
+// per launch (until all have run).  Build: hipcc --offload-arch=gfx950 -O2 tools/launch_rate.hip
+// -o tools/launch_rate
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+
+struct Big {
+    float v[80];
+};
+
+__global__ void k_small(float* out, uint32_t n) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && n == 0xFFFFFFFFu) out[0] = 1.0f;
+}
+__global__ void k_big(float* out, const Big b) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && b.v[79] == -1.0f) out[0] = 1.0f;
+}
+
+#define CHECK(x)                                                                \
+    do {                                                                        \
+        hipError_t e_ = (x);                                                    \
+        if (e_ != hipSuccess) {                                                 \
+            std::printf("%s failed: %s\n", #x, hipGetErrorString(e_));          \
+            return 1;                                                           \
+        }                                                                       \
+    } while (0)
+
+int main() {
+    float* out = nullptr;
+    CHECK(hipMalloc(&out, 4));
+    hipStream_t s[4];
+    for (auto& x : s) CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    Big b{};
+    const int n = 4000;
+    for (int big = 0; big < 2; ++big)
+        for (int ns : {1, 2, 4}) {
+            for (int rep = 0; rep < 2; ++rep) {   // (first repetition warms up)
+                CHECK(hipDeviceSynchronize());
+                const auto t0 = std::chrono::steady_clock::now();
+                for (int i = 0; i < n; ++i) {
+                    hipStream_t st = s[i % ns];
+                    if (big)
+                        hipLaunchKernelGGL(k_big, dim3(1024), dim3(256), 0, st, out, b);
+                    else
+                        hipLaunchKernelGGL(k_small, dim3(1024), dim3(256), 0, st, out, (uint32_t)i);
+                }
+                const auto t1 = std::chrono::steady_clock::now();
+                CHECK(hipDeviceSynchronize());
+                const auto t2 = std::chrono::steady_clock::now();
+                if (rep)
+                    std::printf("{\"args\": \"%s\", \"streams\": %d, \"host_us_per_launch\": %.3f, "
+                                "\"gpu_us_per_launch\": %.3f}\n",
+                                big ? "320 B" : "12 B", ns,
+                                std::chrono::duration<double, std::micro>(t1 - t0).count() / n,
+                                std::chrono::duration<double, std::micro>(t2 - t0).count() / n);
+            }
+        }
+    for (auto& x : s) CHECK(hipStreamDestroy(x));
+    CHECK(hipFree(out));
+    return 0;
+}

@@ -4,6 +4,7 @@ of `bench.py --gpus N` computes per step, to predict strong-scaling efficiency w
 8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] [RT_QUEUES=q] [RT_PATHS=auto|per_wave|pair|compact] python tools/rank_sim.py [K3|K2|K5] [steps]"""
 import json
 import sys
+import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -45,14 +46,18 @@ def main(cfg="K3", steps=50):
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
+        t0 = time.perf_counter()
         r.frames(cam_t, sc, seeds[69:69 + steps])
+        host_us = (time.perf_counter() - t0) * 1e6 / steps      # the issuing call's own time
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / steps
         base = base or us
         print(json.dumps({"cfg": cfg, "world": world, "rank0_rows": r.rows,
                           "us_per_step": round(us, 2), "ideal_us": round(base / world, 2),
-                          "predicted_efficiency": round(base / world / us, 3)}), flush=True)
+                          "predicted_efficiency": round(base / world / us, 3),
+                          "host_issue_us_per_step": round(host_us, 2),
+                          "queues": pipe.last_launch_info().get("queues")}), flush=True)
     pipe.close()
 
 
