@@ -58,6 +58,33 @@ int main() {
                                 std::chrono::duration<double, std::micro>(t2 - t0).count() / n);
             }
         }
+    // a captured graph of `per` launches (the 320-byte kernel) replayed: host cost of one
+    // hipGraphLaunch per `per` kernels
+    for (int per : {20, 100}) {
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        CHECK(hipStreamBeginCapture(s[0], hipStreamCaptureModeThreadLocal));
+        for (int i = 0; i < per; ++i)
+            hipLaunchKernelGGL(k_big, dim3(1024), dim3(256), 0, s[0], out, b);
+        CHECK(hipStreamEndCapture(s[0], &g));
+        CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        const int reps = n / per;
+        for (int rep = 0; rep < 2; ++rep) {
+            CHECK(hipDeviceSynchronize());
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int i = 0; i < reps; ++i) CHECK(hipGraphLaunch(ge, s[0]));
+            const auto t1 = std::chrono::steady_clock::now();
+            CHECK(hipDeviceSynchronize());
+            const auto t2 = std::chrono::steady_clock::now();
+            if (rep)
+                std::printf("{\"graph_kernels\": %d, \"host_us_per_kernel\": %.3f, "
+                            "\"gpu_us_per_kernel\": %.3f}\n", per,
+                            std::chrono::duration<double, std::micro>(t1 - t0).count() / (reps * per),
+                            std::chrono::duration<double, std::micro>(t2 - t0).count() / (reps * per));
+        }
+        CHECK(hipGraphExecDestroy(ge));
+        CHECK(hipGraphDestroy(g));
+    }
     for (auto& x : s) CHECK(hipStreamDestroy(x));
     CHECK(hipFree(out));
     return 0;
