@@ -827,8 +827,11 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
 // tiles (profiles/r03e_ab_queues.log, r03e_rank_sim_k3_q*.jsonl; µs per K3 update at 1 / 2
 // / 3 / 4 parts: whole image 22.7 / 19.6 / 19.6 / 19.0, K2 15.9 / 13.6 / 13.5 / 13.5; a
 // 2-rank share 12.5 / 11.4 / 11.5; 4-rank 7.8 / 7.5 / 9.7; 8-rank 5.9 / 7.9 / 10.9): each
-// part costs the host one more launch, which small shares cannot hide.
-constexpr uint64_t kQueues4MinTiles = 20000, kQueues2MinTiles = 12000;
+// part costs the host one more launch (2.7-4.4 µs each on the boxes measured,
+// profiles/r03g_launch_rate.jsonl, r03h_launch_rate.jsonl), which small shares cannot hide,
+// and a slow host turns 4 parts into a host-bound chain (the driver's 20-step command:
+// 72-77 G rays/s at 4 parts, 87-90 at 2, 81-85 at 1, profiles/r03h_bench_driver_q*.json).
+constexpr uint64_t kQueues4MinTiles = ~0ull, kQueues2MinTiles = 12000;
 uint32_t update_parts(const rt_ctx* ctx, const rtk::TraceParams& p, int kernel) {
     if ((kernel != rtk::kTraceSingle && kernel != rtk::kTraceSingleOne) || p.frames != 1u)
         return 1u;

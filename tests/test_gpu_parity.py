@@ -175,9 +175,9 @@ def test_bench_dispatch_chain_matches_fixture(rt, cfg, single):
         newest = p.update_frames(a, b, w, h, cam.with_fields(camera_has_moved=0.0), sc,
                                  g["seeds"][5:25])
         info = p.last_launch_info()
-        # (the library's choice of concurrent parts per update: 4 at this size)
+        # (the library's choice of concurrent parts per update: 2 at this size)
         assert info["launches"] == 20 * info["queues"] and info["max_frames_per_launch"] == 1
-        assert info["queues"] == (4 if single == "auto" else 1 if single == "off" else 4)
+        assert info["queues"] == (1 if single == "off" else 2)
         assert info["kernel_name"] == {"off": "rt_trace_kernel<2>", "one": "rt_single_kernel<1>",
                                        "auto": "rt_single_kernel<2>"}[single]
         img = host(b if newest == 1 else a)

@@ -8,6 +8,8 @@ TAG=${1:-r03f}
 cd $GRAFT_REPO_ROOT; O=gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
 V=gpu-ray-tracing_amd/build/variants
+timeout -k 10 120 ./tools/launch_rate > $O/launch_rate.jsonl 2>&1 || { echo launch_rate failed; cat $O/launch_rate.jsonl; exit 1; }
+cat $O/launch_rate.jsonl
 for v in breload8 hash3; do
   RT_HIP_LIB=$V/librt_hip_$v.so timeout -k 10 400 python -u -m pytest tests -m gpu -x -q \
     --timeout 200 --timeout-method thread > $O/pytest_gpu_$v.log 2>&1

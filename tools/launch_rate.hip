@@ -85,6 +85,69 @@ int main() {
         CHECK(hipGraphExecDestroy(ge));
         CHECK(hipGraphDestroy(g));
     }
+    // instantiation of a captured graph of `per` kernels, and updating every kernel node's
+    // arguments of the instantiated graph (hipGraphExecKernelNodeSetParams)
+    for (int per : {8, 32, 128}) {
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        CHECK(hipStreamBeginCapture(s[0], hipStreamCaptureModeThreadLocal));
+        for (int i = 0; i < per; ++i)
+            hipLaunchKernelGGL(k_big, dim3(1024), dim3(256), 0, s[0], out, b);
+        CHECK(hipStreamEndCapture(s[0], &g));
+        const auto t0 = std::chrono::steady_clock::now();
+        CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        const auto t1 = std::chrono::steady_clock::now();
+        size_t nn = 0;
+        CHECK(hipGraphGetNodes(g, nullptr, &nn));
+        hipGraphNode_t nodes[128];
+        CHECK(hipGraphGetNodes(g, nodes, &nn));
+        float* argp = out;
+        Big bb = b;
+        void* args[] = {&argp, &bb};
+        hipKernelNodeParams kp{};
+        CHECK(hipGraphKernelNodeGetParams(nodes[0], &kp));
+        kp.kernelParams = args;
+        const auto t2 = std::chrono::steady_clock::now();
+        for (size_t i = 0; i < nn; ++i) {
+            bb.v[0] = (float)i;
+            CHECK(hipGraphExecKernelNodeSetParams(ge, nodes[i], &kp));
+        }
+        const auto t3 = std::chrono::steady_clock::now();
+        CHECK(hipGraphLaunch(ge, s[0]));
+        CHECK(hipDeviceSynchronize());
+        std::printf("{\"graph_kernels\": %d, \"instantiate_us\": %.1f, "
+                    "\"set_params_us_per_node\": %.3f}\n", per,
+                    std::chrono::duration<double, std::micro>(t1 - t0).count(),
+                    std::chrono::duration<double, std::micro>(t3 - t2).count() / nn);
+        CHECK(hipGraphExecDestroy(ge));
+        CHECK(hipGraphDestroy(g));
+    }
+    // a small host-to-device copy on the stream: pageable and pinned source
+    {
+        float* dtab = nullptr;
+        CHECK(hipMalloc(&dtab, 8192));
+        static float pageable[2048];
+        float* pinned = nullptr;
+        CHECK(hipHostMalloc(&pinned, 8192, 0));
+        for (int pin = 0; pin < 2; ++pin)
+            for (int bytes : {1024, 8192}) {
+                CHECK(hipDeviceSynchronize());
+                const int reps = 500;
+                const auto t0 = std::chrono::steady_clock::now();
+                for (int i = 0; i < reps; ++i)
+                    CHECK(hipMemcpyAsync(dtab, pin ? pinned : pageable, bytes,
+                                         hipMemcpyHostToDevice, s[0]));
+                const auto t1 = std::chrono::steady_clock::now();
+                CHECK(hipDeviceSynchronize());
+                const auto t2 = std::chrono::steady_clock::now();
+                std::printf("{\"h2d_bytes\": %d, \"pinned\": %d, \"host_us\": %.3f, "
+                            "\"gpu_us\": %.3f}\n", bytes, pin,
+                            std::chrono::duration<double, std::micro>(t1 - t0).count() / reps,
+                            std::chrono::duration<double, std::micro>(t2 - t0).count() / reps);
+            }
+        CHECK(hipHostFree(pinned));
+        CHECK(hipFree(dtab));
+    }
     for (auto& x : s) CHECK(hipStreamDestroy(x));
     CHECK(hipFree(out));
     return 0;
