@@ -94,9 +94,6 @@ def parse():
     ap.add_argument("--queues", type=int, default=int(os.environ.get("RT_QUEUES", "0")),
                     help="concurrent parts per one-frame update (rt_set_update_queues; "
                          "0 = the library's choice)")
-    ap.add_argument("--graphs", default=os.environ.get("RT_GRAPHS", "auto"),
-                    choices=["auto", "off"],
-                    help="runs of one-frame updates replayed as HIP graphs (rt_set_update_graphs)")
     ap.add_argument("--scan", default="culled", choices=["culled", "exhaustive"],
                     help="sphere-list scan: exact culling (default) or the reference's "
                          "exhaustive linear walk; images are bit-identical")
@@ -277,7 +274,6 @@ def main():
     if dispatch:
         pipe.set_frames_per_launch(1)          # one `update` launch per frame
     pipe.set_update_queues(args.queues)
-    pipe.set_update_graphs(args.graphs)
     # the job's one gather: RCCL behind the C ABI (rt_comm_create + rt_gather_stripes)
     use_abi = world > 1 and backend == "nccl" and os.environ.get("RT_GATHER", "abi") == "abi"
     comm = StripeComm.from_process_group(pipe) if use_abi else None
@@ -366,8 +362,6 @@ def main():
             "kernel": kernel, "kernel_avg_us": round(launch_s * 1e6, 2),
             "frames_per_launch": fpl, "launches_per_step": launches_per_step,
             "queues": queues,
-            # timed frames replayed as update graphs (windows of four one-frame updates)
-            "graph_frames": info.get("graph_frames", 0) * (1 if dispatch else args.steps),
             "algorithmic_bytes_per_launch": bytes_launch,
             "binding": "valu",
             # the same bytes against the measured streaming floor of the pattern (no tracing)

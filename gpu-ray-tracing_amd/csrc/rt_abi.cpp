@@ -9,7 +9,6 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
-#include <cstddef>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -83,29 +82,13 @@ struct rt_ctx {
     };
     std::vector<CountRecord> counts;
     uint32_t frames_per_launch = 0;  // rt_update_frames fusion cap (0 = automatic)
-    rt_launch_info last = {0, 0, 0, -1, 0, 0};  // the last call's launches (rt_last_launch_info)
+    rt_launch_info last = {0, 0, 0, -1, 0};  // the last call's launches (rt_last_launch_info)
     int path_compaction = RT_PATHS_AUTO;
     int frame_pairs = RT_FRAME_PAIRS_AUTO;
     int single_kernel = RT_SINGLE_AUTO;
     // Concurrent parts of one-frame updates (rt_set_update_queues): part 0 on the caller's
     // stream, part k on aux[k - 1], forked and joined through events.
     uint32_t update_queues = 0;      // 0 = automatic
-    // per-frame records of update graphs (rtk::SingleFrameTab; also the record address
-    // direct one-frame launches pass, unread)
-    rtk::SingleFrameTab* d_ftab = nullptr;
-    // Update graphs (rt_set_update_graphs): runs of one-frame updates replayed as
-    // instantiated HIP graphs of kGraphWindow frames; the records of a call's frames go to
-    // d_ftab in one copy from the pinned h_ftab (ftab_ev: that copy has read it).
-    int update_graphs = RT_UPDATE_GRAPHS_AUTO;
-    rtk::SingleFrameTab* h_ftab = nullptr;
-    hipEvent_t ftab_ev = nullptr;
-    struct GraphEntry {
-        std::vector<unsigned char> key;
-        hipGraphExec_t exec;
-        uint64_t used;
-    };
-    std::vector<GraphEntry> graphs;
-    uint64_t graph_clock = 0;
     hipStream_t aux[RT_MAX_UPDATE_QUEUES - 1] = {};
     hipEvent_t fork_ev = nullptr;
     hipEvent_t join_ev[RT_MAX_UPDATE_QUEUES - 1] = {};
@@ -732,17 +715,6 @@ uint32_t fill_hint(rtk::TraceParams& p, uint32_t n_in) {
     return n;
 }
 
-// The hint of a one-frame launch (p.frames == 1): known = every pixel of p.in holds one
-// count the context knows (or the frame resets it); n_last = the count after the frame.
-void plan_frame_hint(rt_ctx* ctx, rtk::TraceParams& p, bool& known, uint32_t& n_last) {
-    uint32_t n_in = 0;
-    known = p.reset_first || lookup_count(ctx, p.in, p, n_in);
-    if (known)
-        n_last = fill_hint(p, p.reset_first ? 0u : n_in);
-    else
-        p.hint_frames = 0;
-}
-
 // Sets the hint of one launch from what the context knows about `in` and records the
 // count of `out` afterwards (or forgets it when unknown).
 void plan_hint(rt_ctx* ctx, rtk::TraceParams& p, const void* in, const void* out) {
@@ -807,13 +779,6 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
                 : ctx->path_compaction == RT_PATHS_PAIR  ? 2u
                                                          : 0u;
     if (rt_status s = ensure_hash_tables(ctx, w, h, stream)) return s;
-    if (!ctx->d_ftab) {
-        hipError_t e = hipMalloc(&ctx->d_ftab, sizeof(rtk::SingleFrameTab));
-        if (e != hipSuccess) return hip_fail(e, "hipMalloc(frame table)");
-        e = hipMemsetAsync(ctx->d_ftab, 0, sizeof(rtk::SingleFrameTab), stream);
-        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(frame table)");
-    }
-    p.frame_rec = &ctx->d_ftab->cur[0];
     p.hx = ctx->d_hx;
     p.hy = ctx->d_hx + rtk::hy_offset(w);
     if (ctx->scan_mode == RT_SCAN_CULLED) {
@@ -914,189 +879,8 @@ rt_status join_aux(rt_ctx* ctx, uint32_t n, hipStream_t stream) {
     return e == hipSuccess ? RT_OK : hip_fail(e, "join (hipEventRecord / hipStreamWaitEvent)");
 }
 
-// ---- update graphs ----------------------------------------------------------------------
-// A run of one-frame updates costs the host one launch per part per frame (2.7-5.9 µs each
-// on the boxes measured, profiles/r03*_launch_rate.jsonl), more than a rank share's frame
-// takes on the GPU.  rt_update_frames therefore replays runs of kGraphWindow frames as an
-// instantiated graph: a stage node (rtk::stage_node: the window's records to the table's
-// fixed slots) and per part a chain of kGraphWindow one-frame launches (each reads its
-// frame's record from its slot; arguments fixed at instantiation), one hipGraphLaunch per
-// window (0.07-0.45 µs of host time per kernel).  Graphs are cached by their launches'
-// arguments (images, order, parts, camera, scene, ...), both ping-pong parities at once.
-constexpr uint32_t kGraphWindow = 4;
-static_assert(kGraphWindow <= rtk::kGraphMaxWindow && kGraphWindow % 2 == 0,
-              "windows start on the same image parity");
-constexpr size_t kGraphCache = 8;
-
-// The launches of one window graph over images (in0 -> out0 for its even frames): their
-// kernel-node parameters and the cache key (every node's function, grid and arguments).
-struct WindowNodes {
-    std::vector<rtk::SingleNodeArgs> args;   // (kernelParams point into these)
-    std::vector<hipKernelNodeParams> nodes;
-    std::vector<uint32_t> part;              // the part of each frame node
-    std::vector<unsigned char> key;
-};
-void window_nodes(rt_ctx* ctx, rtk::TraceParams p, int kernel, uint32_t parts, float4* in0,
-                  float4* out0, WindowNodes& wn) {
-    const size_t n = (size_t)parts * kGraphWindow + 1;
-    wn.args.assign(n, rtk::SingleNodeArgs{});
-    for (rtk::SingleNodeArgs& a : wn.args) std::memset(&a, 0, sizeof(a));
-    wn.nodes.clear();
-    wn.part.clear();
-    wn.key.clear();
-    auto add_key = [&](const void* v, size_t bytes) {
-        const unsigned char* b = static_cast<const unsigned char*>(v);
-        wn.key.insert(wn.key.end(), b, b + bytes);
-    };
-    hipKernelNodeParams np;
-    rtk::stage_node(ctx->d_ftab, kGraphWindow, wn.args[0], np);
-    wn.nodes.push_back(np);
-    wn.part.push_back(~0u);
-    p.frames = 1;
-    p.reset_first = 0;
-    p.parts = parts;
-    for (uint32_t k = 0; k < parts; ++k)
-        for (uint32_t j = 0; j < kGraphWindow; ++j) {
-            p.part = k;
-            p.in = (j & 1u) ? out0 : in0;
-            p.out = (j & 1u) ? in0 : out0;
-            rtk::SingleNodeArgs& a = wn.args[wn.nodes.size()];
-            if (!rtk::single_node(p, kernel, &ctx->d_ftab->cur[j], a, np)) continue;
-            wn.nodes.push_back(np);
-            wn.part.push_back(k);
-        }
-    for (size_t i = 0; i < wn.nodes.size(); ++i) {
-        const hipKernelNodeParams& q = wn.nodes[i];
-        add_key(&q.func, sizeof(q.func));
-        add_key(&q.gridDim, sizeof(q.gridDim));
-        add_key(&q.blockDim, sizeof(q.blockDim));
-        add_key(&wn.args[i], offsetof(rtk::SingleNodeArgs, ptrs));
-    }
-}
-
-// The instantiated graph of wn: the stage node, then per part a chain of its frames.
-rt_status instantiate_window(const WindowNodes& wn, hipGraphExec_t* exec) {
-    hipGraph_t g = nullptr;
-    hipError_t e = hipGraphCreate(&g, 0);
-    if (e != hipSuccess) return hip_fail(e, "hipGraphCreate");
-    hipGraphNode_t stage = nullptr;
-    e = hipGraphAddKernelNode(&stage, g, nullptr, 0, &wn.nodes[0]);
-    std::vector<hipGraphNode_t> last(RT_MAX_UPDATE_QUEUES, stage);
-    for (size_t i = 1; e == hipSuccess && i < wn.nodes.size(); ++i) {
-        hipGraphNode_t node = nullptr;
-        e = hipGraphAddKernelNode(&node, g, &last[wn.part[i]], 1, &wn.nodes[i]);
-        last[wn.part[i]] = node;
-    }
-    if (e == hipSuccess) e = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    return e == hipSuccess ? RT_OK : hip_fail(e, "update graph (hipGraphAddKernelNode / Instantiate)");
-}
-
-// The cached graph for (p, kernel, parts, in0 -> out0), instantiated on first use together
-// with the other parity's (out0 -> in0: a later call may start on the other image).
-rt_status window_graph(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t parts,
-                       float4* in0, float4* out0, hipGraphExec_t* out) {
-    WindowNodes wn;
-    window_nodes(ctx, p, kernel, parts, in0, out0, wn);
-    for (rt_ctx::GraphEntry& g : ctx->graphs)
-        if (g.key == wn.key) {
-            g.used = ++ctx->graph_clock;
-            *out = g.exec;
-            return RT_OK;
-        }
-    for (int parity = 0; parity < 2; ++parity) {
-        WindowNodes other;
-        const WindowNodes& w = parity ? other : wn;
-        if (parity) window_nodes(ctx, p, kernel, parts, out0, in0, other);
-        hipGraphExec_t exec = nullptr;
-        if (rt_status s = instantiate_window(w, &exec)) return s;
-        if (ctx->graphs.size() >= kGraphCache) {    // evict the least recently used
-            size_t lru = 0;
-            for (size_t i = 1; i < ctx->graphs.size(); ++i)
-                if (ctx->graphs[i].used < ctx->graphs[lru].used) lru = i;
-            (void)hipGraphExecDestroy(ctx->graphs[lru].exec);
-            ctx->graphs.erase(ctx->graphs.begin() + (long)lru);
-        }
-        ctx->graphs.push_back({w.key, exec, ++ctx->graph_clock});
-        if (!parity) *out = exec;
-    }
-    return RT_OK;
-}
-
 void note_launch(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t frames,
-                 uint32_t parts = 1u);
-void plan_frame_hint(rt_ctx* ctx, rtk::TraceParams& p, bool& known, uint32_t& n_last);
-
-// Frames [f0, f0 + n) of rt_update_frames (n a multiple of kGraphWindow, no reset among
-// them) as window graphs, when their launches are one-frame launches (*handled = false:
-// not applicable, nothing done).  cur: the image index frame f0 reads, updated.
-rt_status graph_frames(rt_ctx* ctx, rtk::TraceParams& p, float4* const img[2], int& cur,
-                       uint32_t f0, uint32_t n, const float* seeds, hipStream_t stream,
-                       uint32_t& aux_live, bool& forked, bool* handled) {
-    *handled = false;
-    p.frames = 1;
-    p.store_each = 0;
-    p.reset_first = 0;
-    const int kernel = single_or(ctx, p, trace_kernel_for(ctx, p));
-    if (kernel != rtk::kTraceSingle && kernel != rtk::kTraceSingleOne) return RT_OK;
-    const uint32_t parts = update_parts(ctx, p, kernel);
-    p.parts = parts;
-    p.part = 0;
-    if (aux_live) {   // (earlier direct parts on the context's streams: the graph orders
-                      //  after the caller's stream only)
-        if (rt_status s = join_aux(ctx, aux_live, stream)) return s;
-        aux_live = 0;
-    }
-    forked = false;
-    if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
-    if (rt_status s = plan_wg_order(ctx, p, kernel, stream)) return s;
-    if (!ctx->h_ftab) {
-        hipError_t e = hipHostMalloc(&ctx->h_ftab, sizeof(rtk::SingleFrameTab), 0);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ftab_ev, hipEventDisableTiming);
-        if (e != hipSuccess) return hip_fail(e, "hipHostMalloc / hipEventCreate (frame table)");
-    } else {
-        // the previous call's copy has read the pinned records
-        hipError_t e = hipEventSynchronize(ctx->ftab_ev);
-        if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize(frame table)");
-    }
-    float4* const in0 = img[cur];
-    float4* const out0 = img[1 - cur];
-    // the frames' records and the host's count bookkeeping, frame by frame as the direct
-    // launches do it
-    rtk::SingleFrameTab* h = ctx->h_ftab;
-    h->next = 0;
-    for (uint32_t j = 0; j < n; ++j) {
-        p.in = img[cur];
-        p.out = img[1 - cur];
-        p.seed_b[0] = host_f2u(seeds[f0 + j] * 4294967296.0f);
-        bool known = false;
-        uint32_t n_last = 0;
-        plan_frame_hint(ctx, p, known, n_last);
-        h->rec[j] = rtk::single_frame(p, 0);
-        note_launch(ctx, p, kernel, 1u, parts);
-        if (known)
-            record_count(ctx, img[1 - cur], p, n_last);
-        else
-            forget_count(ctx, img[1 - cur]);
-        cur = 1 - cur;
-    }
-    ctx->last.graph_frames += n;
-    const size_t bytes = offsetof(rtk::SingleFrameTab, rec) + (size_t)n * sizeof(rtk::SingleFrame);
-    hipError_t e = hipMemcpyAsync(ctx->d_ftab, h, bytes, hipMemcpyHostToDevice, stream);
-    if (e == hipSuccess) e = hipEventRecord(ctx->ftab_ev, stream);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(frame table)");
-    hipGraphExec_t exec = nullptr;
-    if (rt_status s = window_graph(ctx, p, kernel, parts, in0, out0, &exec)) return s;
-    for (uint32_t w = 0; w < n / kGraphWindow; ++w) {
-        e = hipGraphLaunch(exec, stream);
-        if (e != hipSuccess) return hip_fail(e, "hipGraphLaunch(update graph)");
-    }
-    *handled = true;
-    return RT_OK;
-}
-
-void note_launch(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t frames,
-                 uint32_t parts) {
+                 uint32_t parts = 1u) {
     ctx->last.launches += parts;
     ctx->last.queues = parts;
     ctx->last.frames += frames;
@@ -1121,7 +905,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         return s;
     const float4* src = reinterpret_cast<const float4*>(in);
     float4* dst = reinterpret_cast<float4*>(out);
-    ctx->last = {0, 0, 0, -1, 0, 0};
+    ctx->last = {0, 0, 0, -1, 0};
     for (uint32_t f0 = 0; f0 < frames; f0 += rtk::kMaxFramesPerLaunch) {
         const uint32_t nf = std::min<uint32_t>(frames - f0, rtk::kMaxFramesPerLaunch);
         p.in = src;
@@ -1222,10 +1006,6 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->tile_order);
         (void)hipFree(ctx->d_grid);
         (void)hipFree(ctx->wg_buf);
-        (void)hipFree(ctx->d_ftab);
-        for (rt_ctx::GraphEntry& g : ctx->graphs) (void)hipGraphExecDestroy(g.exec);
-        if (ctx->h_ftab) (void)hipHostFree(ctx->h_ftab);
-        if (ctx->ftab_ev) (void)hipEventDestroy(ctx->ftab_ev);
         free_candidates(ctx);
         for (uint32_t k = 0; k + 1 < RT_MAX_UPDATE_QUEUES; ++k) {
             if (ctx->aux[k]) (void)hipStreamDestroy(ctx->aux[k]);
@@ -1283,14 +1063,6 @@ rt_status rt_set_update_queues(rt_ctx* ctx, uint32_t queues) {
     if (queues > RT_MAX_UPDATE_QUEUES)
         return fail(RT_ERR_INVALID_ARGUMENT, "queues above RT_MAX_UPDATE_QUEUES");
     ctx->update_queues = queues;
-    return RT_OK;
-}
-
-rt_status rt_set_update_graphs(rt_ctx* ctx, int mode) {
-    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
-    if (mode != RT_UPDATE_GRAPHS_AUTO && mode != RT_UPDATE_GRAPHS_OFF)
-        return fail(RT_ERR_INVALID_ARGUMENT, "unknown update-graph mode");
-    ctx->update_graphs = mode;
     return RT_OK;
 }
 
@@ -1377,23 +1149,10 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
     // instances run one frame per launch.
     const uint32_t per = frames_per_launch_for(ctx, p);
     int cur = 0;
-    ctx->last = {0, 0, 0, -1, 0, 0};
+    ctx->last = {0, 0, 0, -1, 0};
     uint32_t aux_live = 0;      // aux streams with work of this call not yet joined
     bool forked = false;        // aux streams ordered after the last work on `stream`
     for (uint32_t f0 = 0; f0 < frames; f0 += per) {
-        // runs of one-frame updates: window graphs (update graphs, above)
-        if (per == 1u && ctx->update_graphs != RT_UPDATE_GRAPHS_OFF &&
-            !(f0 == 0 && cam->camera_has_moved > 0.5f) && frames - f0 >= kGraphWindow) {
-            const uint32_t n = (frames - f0) / kGraphWindow * kGraphWindow;
-            bool handled = false;
-            if (rt_status s = graph_frames(ctx, p, img, cur, f0, n, seeds, stream, aux_live,
-                                           forked, &handled))
-                return s;
-            if (handled) {
-                f0 += n - per;   // (the loop adds per)
-                continue;
-            }
-        }
         const uint32_t nf = std::min<uint32_t>(per, frames - f0);
         p.in = img[cur];
         p.out = img[1 - cur];

@@ -36,34 +36,6 @@ static_assert(kCandSphOff + 2u * kCandMax <= kCandStride, "sphere records fit");
 constexpr uint32_t kHintFrames = RT_HINT_FRAMES;
 constexpr uint32_t kHintEntries = RT_HINT_FRAMES;
 
-// Per-frame values of a one-frame update (rt_single_kernel): in its launch parameters, or
-// for the launches of an update graph in a device table (SingleFrameTab), since a graph's
-// kernel arguments are fixed when it is instantiated.
-struct SingleFrame {
-    uint32_t hinted;       // every pixel is expected to hold n_hint (TraceParams hint_*)
-    uint32_t n_hint;       // every pixel's count before the frame (0 on reset)
-    uint32_t seed_b;       // B = u32(random_seed * 2^32) (wgsl:311, 353)
-    // RT_SINGLE_NCHK: n_hint < 2^24 (n_exact), the bits of f32(n_hint) and of f32(the count
-    // after the frame): a pixel holding exactly f32(n_hint) holds the hinted count
-    uint32_t n_exact, ng_bits, n_after_bits;
-    uint32_t pad0, pad1;
-    double rcp_hint;       // RN64(1 / (n_hint + 1))
-    double pad2;
-    float4 rs;             // (rf(sb), random_unit_vector(sb)) of the frame, bounce 0
-};
-static_assert(sizeof(SingleFrame) == 64, "one 64-B record per frame");
-// The device table of update graphs (rt_abi.cpp): the host writes one call's records to
-// rec[] and next = 0; each graph launch's first node (stage_node) copies its window's
-// records rec[next, next + W) to cur[0, W) and advances next, and the graph's launch of
-// window frame j reads cur[j] (a fixed address: graph arguments are fixed).
-constexpr uint32_t kGraphMaxWindow = 8;
-struct SingleFrameTab {
-    uint32_t next;
-    uint32_t pad[15];
-    SingleFrame cur[kGraphMaxWindow];
-    SingleFrame rec[kMaxFramesPerLaunch];
-};
-
 // Everything the `update` kernel needs, passed by value (kernarg -> SGPRs).
 struct TraceParams {
     const float4* in;    // local image (compact stripes), row pitch = width
@@ -91,9 +63,6 @@ struct TraceParams {
     // `part` (launch_wg_order with `parts`), or without an order every parts-th local band
     // from band `part`.  parts <= 1: the whole update.
     uint32_t part, parts;
-    // a valid device address of one SingleFrame (the context's update-graph table): direct
-    // one-frame launches pass it as their record pointer, unread
-    const SingleFrame* frame_rec;
     // Uniform XZ grid over the small spheres for bounce rays (rt_kernels.hip scan_grid;
     // built by rt_abi.cpp build_grid): per cell the range of its items, each item a copy
     // of the sphere's scan record and its index (every small sphere is registered in the
@@ -206,28 +175,6 @@ constexpr uint32_t pack_bands(uint32_t first, uint32_t step, bool ordered) {
     return first | ((step < 0x7FFFu ? step : 0x7FFFu) << 16) | (ordered ? 1u << 31 : 0u);
 }
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream);
-// One-frame launches (kTraceSingle / kTraceSingleOne) as graph kernel nodes: the node of
-// part p.part of p.parts of a frame whose record is at `fr` (an update graph's staged
-// record; p.in / p.out: that frame's images).  `args` keeps the argument values the node's
-// kernelParams point to until the node is added.  Returns false when the part has no
-// workgroups (no node).
-struct SingleNodeArgs {
-    const float4* cand;
-    const SingleFrame* fr;
-    SingleFrameTab* tab;
-    const float4* in;
-    uint32_t width, height, bands;
-    const uint32_t* order;
-    alignas(16) unsigned char params[512];     // SingleParams
-    void* ptrs[8];
-};
-bool single_node(const TraceParams& p, int kernel, const SingleFrame* fr, SingleNodeArgs& args,
-                 hipKernelNodeParams& node);
-// an update graph's first node: stages `frames` records of tab (see SingleFrameTab)
-void stage_node(SingleFrameTab* tab, uint32_t frames, SingleNodeArgs& args,
-                hipKernelNodeParams& node);
-// SingleFrame of frame f of p (its hint, seed and the counts' bits)
-SingleFrame single_frame(const TraceParams& p, uint32_t f);
 hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream);
 // Builds the per-tile candidate blocks for p's camera/scene/stripes (p.cand_k entries at
 // most per tile).

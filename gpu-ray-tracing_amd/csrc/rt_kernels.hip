@@ -1352,14 +1352,19 @@ struct SingleParams {
     float4* out;
     const float4* geom;    // full scan records (tiles without a candidate list)
     const float4* sph;     // full sphere records
-    const uint32_t* hx;    // hash(x * 73), then hash(y * 51) from hy_off (wgsl:309-310)
     uint32_t count, depth, spp;
+    uint32_t hinted;       // hint_n / hint_rcp / hint_rs of frame 0 are valid
+    uint32_t n_hint;       // every pixel's count before the frame (0 on reset)
+    uint32_t seed_b;       // B = u32(random_seed * 2^32) (wgsl:311, 353)
     uint32_t hy_off;       // hash(y * 51) table offset in the hx buffer
+    double rcp_hint;       // RN64(1 / (n_hint + 1))
+    // RT_SINGLE_NCHK: n_hint < 2^24 (n_exact), the bits of f32(n_hint) and of f32(the count
+    // after the frame): a pixel holding exactly f32(n_hint) holds the hinted count
+    uint32_t n_exact, ng_bits, n_after_bits;
     // local bands of a launch in raster order (no a_order): lband = first + blockIdx.y *
     // step, first | step << 16 — one of the update's concurrent parts (launch_single)
     uint32_t lbands;
-    uint32_t graph;        // a launch of an update graph: the frame's values at a_fr
-    SingleFrame f0;        // otherwise these
+    float4 rs;             // (rf(sb), random_unit_vector(sb)) of frame 0, bounce 0
     double disk_rcp[8];
     float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3];
     float defocus_angle;
@@ -1375,9 +1380,6 @@ static_assert(kSinglePix >= 1 && kSinglePix <= 4, "1 to 4 tiles per wave");
 // Waves per SIMD the one-frame kernel's register plan targets.  The compiler fills the
 // SGPR budget the bound allows: at 5 it reached 98 SGPRs (6 resident waves per SIMD on
 // gfx950: MI355X_MICROARCH.md, Residency), at 7 it stays at <= 96 (7 waves) without spills.
-#ifndef RT_SINGLE_MIN_WAVES_ONE   // the one-tile instance (small launches): 8 (<= 80 SGPRs)
-#define RT_SINGLE_MIN_WAVES_ONE 8
-#endif
 #ifndef RT_SINGLE_MIN_WAVES
 #define RT_SINGLE_MIN_WAVES 7
 #endif
@@ -1509,8 +1511,7 @@ __device__ __forceinline__ v3 sky_w(v3 cf, v3 d) {
 template <uint32_t S>
 constexpr bool kSingleLds = RT_SINGLE_LDS == 2 || (RT_SINGLE_LDS == 1 && S == 1);
 template <uint32_t S, bool kUniRs>
-__device__ __forceinline__ void single_sample(const SingleParams& p, const SingleFrame& fr,
-                                              const Cam& cam,
+__device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& cam,
                                               const TileCoord (&tc)[S],
                                               const uint32_t (&hxy)[S],
                                               const uint32_t (&seed)[S],
@@ -1528,7 +1529,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Singl
         d[s] = sub(fmas((float)tc[s].y + (float)(hxy[s] & 1u), cam.pdv,
                         fmas((float)tc[s].x, cam.pdu, cam.vul)), o[s]);
 #else
-        get_ray<kSingleDisk>(cam, tc[s].x, tc[s].y, hxy[s], seed[s] * 25u + fr.seed_b, o[s],
+        get_ray<kSingleDisk>(cam, tc[s].x, tc[s].y, hxy[s], seed[s] * 25u + p.seed_b, o[s],
                              d[s]);
 #endif
     }
@@ -1630,8 +1631,8 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Singl
                 float r_sb;
                 v3 ruv;
                 if (kUniRs) {
-                    r_sb = fr.rs.x;
-                    ruv = mk(fr.rs.y, fr.rs.z, fr.rs.w);
+                    r_sb = p.rs.x;
+                    ruv = mk(p.rs.y, p.rs.z, p.rs.w);
                 } else {
                     const uint32_t sb = hash(seed[s] + 1u);       // wgsl:268, 355 (i = 0)
                     r_sb = rf(sb);
@@ -1663,7 +1664,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Singl
 // accumulator load at all.
 template <int kPix, bool kReset>
 __device__ __forceinline__ void single_body(
-    const float4* __restrict__ a_cand, const SingleFrame* __restrict__ a_fr,
+    const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const uint32_t* __restrict__ a_order, const SingleParams& p) {
     static_assert(kPix >= 1 && kPix <= 4, "1 to 4 tiles per wave");
@@ -1676,22 +1677,6 @@ __device__ __forceinline__ void single_body(
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t tiles_x = (a_width + 7u) >> 3;
-    // the frame's per-frame values: the update graph's staged record at a_fr (a leading,
-    // preloaded argument, always a valid address) when p.graph, else p.f0 — both loaded
-    // unconditionally and selected (a conditional load compiles to a wait per field)
-    SingleFrame fr;
-    {
-        const SingleFrame t = *(const kconst SingleFrame*)a_fr;
-        const bool g = p.graph != 0u;
-        fr.hinted = g ? t.hinted : p.f0.hinted;
-        fr.n_hint = g ? t.n_hint : p.f0.n_hint;
-        fr.seed_b = g ? t.seed_b : p.f0.seed_b;
-        fr.n_exact = g ? t.n_exact : p.f0.n_exact;
-        fr.ng_bits = g ? t.ng_bits : p.f0.ng_bits;
-        fr.n_after_bits = g ? t.n_after_bits : p.f0.n_after_bits;
-        fr.rcp_hint = g ? t.rcp_hint : p.f0.rcp_hint;
-        fr.rs = g ? t.rs : p.f0.rs;
-    }
     // workgroups by decreasing candidate-list load (wg_order, launch_wg_order): the
     // costliest are dispatched first and the cheap ones fill the tail
     uint32_t gx = blockIdx.x, lband = (p.lbands & 0xFFFFu) + blockIdx.y * (p.lbands >> 16);
@@ -1702,7 +1687,6 @@ __device__ __forceinline__ void single_body(
         lband = e >> 16;
     }
     SST_S(1, lband);
-    const uint32_t* __restrict__ a_hx = p.hx;
     const uint32_t tx0 = (gx * kSingleWg + wave) * S;
     const uint32_t band_first = a_bands & 0xFFFFu, band_step = (a_bands >> 16) & 0x7FFFu;
     TileCoord tc[S];
@@ -1746,7 +1730,7 @@ __device__ __forceinline__ void single_body(
                                                       : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s)
-        acc[s] = (RT_SKO & 1) ? make_float4(0.0f, 0.0f, 0.0f, (float)fr.n_hint)
+        acc[s] = (RT_SKO & 1) ? make_float4(0.0f, 0.0f, 0.0f, (float)p.n_hint)
                  : kReset     ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)   // (discarded: no load)
                               : a_in[tc[s].valid ? tc[s].idx : 0];                // wgsl:339
     if (kSingleDisk == 1 && p.defocus_angle > 0.0f) {             // (disk_unit's table)
@@ -1785,21 +1769,20 @@ __device__ __forceinline__ void single_body(
     uint32_t n[S];
     bool pending[S];
     bool any_pending = true;
-    if (fr.hinted) {
+    if (p.hinted) {
         // Every pixel is expected to hold n_hint (the host's count bookkeeping): trace with
         // it while the accumulator loads are in flight, then verify.
-        const uint32_t ng = fr.n_hint;
+        const uint32_t ng = p.n_hint;
         v3 col[S];
         if (ng < spp) {                                           // wgsl:352
             uint32_t seed[S];
             bool live[S];
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
-                seed[s] = 1u + ng + fr.seed_b;                    // wgsl:353
+                seed[s] = 1u + ng + p.seed_b;                     // wgsl:353
                 live[s] = tc[s].valid;
             }
-            single_sample<S, true>(p, fr, cam, tc, hxy, seed, blk, ncand, live, bv, lblk,
-                                   col);
+            single_sample<S, true>(p, cam, tc, hxy, seed, blk, ncand, live, bv, lblk, col);
         }
         any_pending = false;
 #pragma unroll
@@ -1812,7 +1795,7 @@ __device__ __forceinline__ void single_body(
             // conversion with its saturation selects
             n[s] = ng;
             pending[s] = tc[s].valid && !kReset &&
-                         (fr.n_exact ? __float_as_uint(acc[s].w) != fr.ng_bits
+                         (p.n_exact ? __float_as_uint(acc[s].w) != p.ng_bits
                                     : f2u(acc[s].w) != ng);
 #else
             n[s] = kReset ? 0u : f2u(acc[s].w);                   // wgsl:339-350
@@ -1823,7 +1806,7 @@ __device__ __forceinline__ void single_body(
                 const v3 num = sub(col[s], c[s]);
                 if (RT_SINGLE_ACC_F64 && ng < (1u << 24) &&
                     rt_ballot(tc[s].valid && !acc_f64_ok(num)) == 0ull) {
-                    c[s] = acc_f64(c[s], num, fr.rcp_hint);
+                    c[s] = acc_f64(c[s], num, p.rcp_hint);
                 } else {
                     const float k = (float)(ng + 1u);             // wgsl:356
                     c[s] = mk(c[s].x + num.x / k, c[s].y + num.y / k, c[s].z + num.z / k);
@@ -1849,9 +1832,9 @@ __device__ __forceinline__ void single_body(
                 n[s] = kReset ? 0u : f2u(acc[s].w);
             }
             live[s] = pending[s] && n[s] < spp;                   // wgsl:352
-            seed[s] = 1u + n[s] + fr.seed_b;                      // wgsl:353
+            seed[s] = 1u + n[s] + p.seed_b;                       // wgsl:353
         }
-        single_sample<S, false>(p, fr, cam, tc, hxy, seed, blk, ncand, live, bv, lblk, col);
+        single_sample<S, false>(p, cam, tc, hxy, seed, blk, ncand, live, bv, lblk, col);
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s)
             if (live[s]) {                                        // wgsl:356-357
@@ -1881,8 +1864,8 @@ __device__ __forceinline__ void single_body(
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
             // (every pixel of a wave without a foreign count holds the hinted count after
             // the frame: f32 of it from the host)
-            const uint32_t nb = (RT_SINGLE_NCHK && fr.hinted && !wave_pending)
-                                    ? fr.n_after_bits
+            const uint32_t nb = (RT_SINGLE_NCHK && p.hinted && !wave_pending)
+                                    ? p.n_after_bits
                                     : __float_as_uint((float)n[s]);
             const u32x4 v = {__float_as_uint(c[s].x), __float_as_uint(c[s].y),
                              __float_as_uint(c[s].z), nb};
@@ -1905,20 +1888,18 @@ __device__ __forceinline__ void single_body(
 }
 
 template <int kPix>
-__global__ __launch_bounds__(64 * kSingleWg, kPix == 1 ? RT_SINGLE_MIN_WAVES_ONE
-                                                         : RT_SINGLE_MIN_WAVES) void rt_single_kernel(
-    const float4* __restrict__ a_cand, const SingleFrame* __restrict__ a_fr,
+__global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single_kernel(
+    const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const uint32_t* __restrict__ a_order, const SingleParams p) {
-    single_body<kPix, false>(a_cand, a_fr, a_in, a_width, a_height, a_bands, a_order, p);
+    single_body<kPix, false>(a_cand, a_hx, a_in, a_width, a_height, a_bands, a_order, p);
 }
 template <int kPix>
-__global__ __launch_bounds__(64 * kSingleWg, kPix == 1 ? RT_SINGLE_MIN_WAVES_ONE
-                                                         : RT_SINGLE_MIN_WAVES) void rt_single_reset_kernel(
-    const float4* __restrict__ a_cand, const SingleFrame* __restrict__ a_fr,
+__global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single_reset_kernel(
+    const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const uint32_t* __restrict__ a_order, const SingleParams p) {
-    single_body<kPix, true>(a_cand, a_fr, a_in, a_width, a_height, a_bands, a_order, p);
+    single_body<kPix, true>(a_cand, a_hx, a_in, a_width, a_height, a_bands, a_order, p);
 }
 
 // ---- Bounce paths with workgroup-wide compaction (kTraceBounce) -----------------------
@@ -2015,14 +1996,18 @@ __device__ __forceinline__ uint32_t compact_slot(bool live, uint32_t wave, uint3
                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Register plan of the bounce instance.  RT_BOUNCE_RELOAD: the camera (per frame) and the
+// grid parameters (per bounce scan) are re-read from the kernarg segment through a pointer
+// the compiler cannot see through (scalar-cache hits), instead of staying live in SGPRs for
+// the whole launch; with it a 7-wave plan fits 94 SGPRs (106 and 6 waves before).  K5 per
+// 64-spp step (profiles/r03f_ab_k5.log, two rounds): 31.3 ms as before, 29.7 reloading at 6
+// waves, 28.8 reloading at 7 (the default), 30.2 at 8 (78 SGPRs, 53 spilled to VGPR lanes),
+// 30.5 at 7 without reloading (81 spilled).
 #ifndef RT_BOUNCE_MIN_WAVES
-#define RT_BOUNCE_MIN_WAVES 6
+#define RT_BOUNCE_MIN_WAVES 7
 #endif
-// RT_BOUNCE_RELOAD: the camera (per frame) and the grid parameters (per bounce scan) are
-// re-read from the kernarg segment through a pointer the compiler cannot see through
-// (scalar-cache hits), instead of staying live in SGPRs for the whole launch.
 #ifndef RT_BOUNCE_RELOAD
-#define RT_BOUNCE_RELOAD 0
+#define RT_BOUNCE_RELOAD 1
 #endif
 __device__ __forceinline__ const kconst TraceParams* karg_bounce_params() {
     // rt_bounce_kernel's only argument: the TraceParams block at kernarg offset 0
@@ -2043,9 +2028,6 @@ constexpr uint32_t bounce_waves() {
     return kMode == kBounceCompact ? kBounceWaves : kMode == kBouncePair ? 2u : 1u;
 }
 __shared__ float4 s_pair_col[64];   // kBouncePair: wave 1's colours of the current pair
-#ifndef RT_BOUNCE_MIN_WAVES
-#define RT_BOUNCE_MIN_WAVES 6
-#endif
 template <int kMode>
 __global__ __launch_bounds__(64 * bounce_waves<kMode>(), RT_BOUNCE_MIN_WAVES) void
 rt_bounce_kernel(const TraceParams p) {
@@ -2683,36 +2665,15 @@ static void launch_bounce(const TraceParams& p, hipStream_t stream) {
         hipLaunchKernelGGL(rt_bounce_kernel<kBounceWave>, grid, dim3(64), lds, stream, p);
 }
 
-// The per-frame record of frame f of p (p.hint_*, p.seed_b): what a one-frame launch reads.
-SingleFrame single_frame(const TraceParams& p, uint32_t f) {
-    SingleFrame r;
-    std::memset(&r, 0, sizeof(r));
-    r.hinted = p.hint_frames > f ? 1u : 0u;
-    r.n_hint = p.hint_n[f];
-    r.seed_b = p.seed_b[f];
-    r.rcp_hint = p.hint_rcp[f];
-    const uint32_t ng = r.n_hint;
-    const uint32_t after = ng < p.spp ? ng + 1u : ng;                  // wgsl:352-357
-    const float fng = (float)ng, faft = (float)after;
-    std::memcpy(&r.ng_bits, &fng, 4);
-    std::memcpy(&r.n_after_bits, &faft, 4);
-    r.n_exact = ng < (1u << 24) ? 1u : 0u;
-    r.rs = p.hint_rs[f * (p.depth ? p.depth : 1u)];
-    return r;
-}
-
-// One part of a one-frame update (kSingleWg waves of kPix tiles each per workgroup along a
-// stripe band): its grid and argument values.  tab == nullptr: the frame's values in the
-// parameters (a direct launch); otherwise record `slot` of the update graph's table.
+// kSingleWg waves of kPix tiles each per workgroup along a stripe band.
 template <int kPix>
-static bool single_setup(const TraceParams& p, const SingleFrame* fr, SingleNodeArgs& a,
-                         dim3& grid) {
+static void launch_single(const TraceParams& p, hipStream_t stream) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     const uint32_t per = kSingleWg * kPix;
     const uint32_t cols = (tiles_x + per - 1u) / per;
     const uint32_t parts = p.parts > 1u ? p.parts : 1u, part = parts > 1u ? p.part : 0u;
     // this part's workgroups: its sub-list of the order, or every parts-th local band
-    grid = dim3(cols, p.local_bands);
+    dim3 grid(cols, p.local_bands);
     const uint32_t* order = p.wg_order;
     uint32_t lbands = 1u << 16;
     if (parts > 1u) {
@@ -2726,20 +2687,30 @@ static bool single_setup(const TraceParams& p, const SingleFrame* fr, SingleNode
             lbands = part | (parts << 16);
         }
     }
-    if (grid.x == 0 || grid.y == 0) return false;
+    if (grid.x == 0 || grid.y == 0) return;
     SingleParams q;
     std::memset(&q, 0, sizeof(q));
     q.lbands = lbands;
     q.out = p.out;
     q.geom = p.geom;
     q.sph = p.sph;
-    q.hx = p.hx;
     q.count = p.count;
     q.depth = p.depth;
     q.spp = p.spp;
+    q.hinted = p.hint_frames != 0u;
+    q.n_hint = p.hint_n[0];
+    q.seed_b = p.seed_b[0];
     q.hy_off = (uint32_t)(p.hy - p.hx);
-    q.graph = fr ? 1u : 0u;
-    if (!fr) q.f0 = single_frame(p, 0);
+    q.rcp_hint = p.hint_rcp[0];
+    {
+        const uint32_t ng = q.n_hint;
+        const uint32_t after = ng < q.spp ? ng + 1u : ng;           // wgsl:352-357
+        const float fng = (float)ng, faft = (float)after;
+        std::memcpy(&q.ng_bits, &fng, 4);
+        std::memcpy(&q.n_after_bits, &faft, 4);
+        q.n_exact = ng < (1u << 24) ? 1u : 0u;
+    }
+    q.rs = p.hint_rs[0];
     for (int k = 0; k < 8; ++k) q.disk_rcp[k] = p.disk_rcp[k];
     for (int i = 0; i < 3; ++i) {
         q.center[i] = p.center[i];
@@ -2750,85 +2721,17 @@ static bool single_setup(const TraceParams& p, const SingleFrame* fr, SingleNode
         q.ddv[i] = p.ddv[i];
     }
     q.defocus_angle = p.defocus_angle;
-    static_assert(sizeof(SingleParams) <= sizeof(a.params), "SingleParams fits");
-    std::memcpy(a.params, &q, sizeof(q));
-    a.cand = p.cand;
-    a.fr = fr ? fr : p.frame_rec;   // (a valid address either way: the kernel loads it)
-    a.in = p.in;
-    a.width = p.width;
-    a.height = p.height;
-    a.bands = pack_bands(p.band_first, p.band_step, false);
-    a.order = order;
-    void* ptrs[8] = {&a.cand, &a.fr, &a.in, &a.width, &a.height, &a.bands, &a.order, a.params};
-    std::memcpy(a.ptrs, ptrs, sizeof(ptrs));
-    return true;
-}
-
-template <int kPix>
-static const void* single_func(bool reset) {
-    return reset ? reinterpret_cast<const void*>(&rt_single_reset_kernel<kPix>)
-                 : reinterpret_cast<const void*>(&rt_single_kernel<kPix>);
-}
-
-template <int kPix>
-static void launch_single(const TraceParams& p, hipStream_t stream) {
-    SingleNodeArgs a;
-    dim3 grid;
-    if (!single_setup<kPix>(p, nullptr, a, grid)) return;
-    (void)hipLaunchKernel(single_func<kPix>(p.reset_first != 0u), grid, dim3(64 * kSingleWg),
-                          a.ptrs, 0, stream);
-}
-
-bool single_node(const TraceParams& p, int kernel, const SingleFrame* fr, SingleNodeArgs& args,
-                 hipKernelNodeParams& node) {
-    dim3 grid;
-    const bool one = kernel == kTraceSingleOne;
-    const bool any = one ? single_setup<1>(p, fr, args, grid)
-                         : single_setup<(int)kSinglePix>(p, fr, args, grid);
-    if (!any || !args.fr) return false;
-    std::memset(&node, 0, sizeof(node));
-    node.func = const_cast<void*>(one ? single_func<1>(p.reset_first != 0u)
-                                      : single_func<(int)kSinglePix>(p.reset_first != 0u));
-    node.gridDim = grid;
-    node.blockDim = dim3(64 * kSingleWg);
-    node.sharedMemBytes = 0;
-    node.kernelParams = args.ptrs;
-    node.extra = nullptr;
-    return true;
-}
-
-// An update graph's first node: copies the window's records rec[next, next + frames) to
-// cur[0, frames), where the graph's frame launches read them, and advances next (one wave;
-// vector loads and stores).
-__global__ __launch_bounds__(64) void rt_graph_stage_kernel(SingleFrameTab* tab,
-                                                            uint32_t frames) {
-    const uint32_t base = tab->next;
-    constexpr uint32_t kWords = sizeof(SingleFrame) / 4u;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(&tab->rec[base]);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&tab->cur[0]);
-    for (uint32_t i = threadIdx.x; i < frames * kWords; i += 64u) dst[i] = src[i];
-    if (threadIdx.x == 0) tab->next = base + frames;
-}
-
-void stage_node(SingleFrameTab* tab, uint32_t frames, SingleNodeArgs& args,
-                hipKernelNodeParams& node) {
-    std::memset(&node, 0, sizeof(node));
-    // (the argument values live in args: its tab and width fields)
-    args.tab = tab;
-    args.width = frames;
-    args.ptrs[0] = &args.tab;
-    args.ptrs[1] = &args.width;
-    node.func = reinterpret_cast<void*>(&rt_graph_stage_kernel);
-    node.gridDim = dim3(1);
-    node.blockDim = dim3(64);
-    node.sharedMemBytes = 0;
-    node.kernelParams = args.ptrs;
-    node.extra = nullptr;
+    if (p.reset_first)
+        hipLaunchKernelGGL(rt_single_reset_kernel<kPix>, grid, dim3(64 * kSingleWg), 0, stream,
+                           p.cand, p.hx, p.in, p.width, p.height,
+                           pack_bands(p.band_first, p.band_step, false), order, q);
+    else
+        hipLaunchKernelGGL(rt_single_kernel<kPix>, grid, dim3(64 * kSingleWg), 0, stream,
+                           p.cand, p.hx, p.in, p.width, p.height,
+                           pack_bands(p.band_first, p.band_step, false), order, q);
 }
 
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
-    if ((kernel == kTraceSingle || kernel == kTraceSingleOne) && !p.frame_rec)
-        return hipErrorInvalidValue;   // (the one-frame kernel loads *frame_rec)
     if (kernel == kTraceSingle)
         launch_single<(int)kSinglePix>(p, stream);
     else if (kernel == kTraceSingleOne)

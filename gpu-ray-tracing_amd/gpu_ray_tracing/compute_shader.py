@@ -84,11 +84,6 @@ class ComputeShaderPipeline:
         parts on their own streams (0 = automatic, 1 = one launch per update)."""
         _lib.call("rt_set_update_queues", self._ctx, int(queues))
 
-    def set_update_graphs(self, mode: str) -> None:
-        """rt_set_update_graphs: runs of one-frame updates in update_frames replayed as HIP
-        graphs ("auto", the default) or launched one by one ("off")."""
-        _lib.call("rt_set_update_graphs", self._ctx, {"auto": 0, "off": 1}[mode])
-
     def set_path_compaction(self, mode: str) -> None:
         """rt_set_path_compaction for bounce launches: "auto" (default), "per_wave",
         "compact" (paths repacked across four waves after every bounce) or "pair" (two waves

@@ -194,7 +194,6 @@ typedef struct rt_launch_info {
     uint32_t max_frames_per_launch;
     int32_t kernel;
     uint32_t queues;
-    uint32_t graph_frames;   /* frames replayed as update graphs (rt_set_update_graphs) */
 } rt_launch_info;
 RT_API rt_status rt_last_launch_info(const rt_ctx* ctx, rt_launch_info* out);
 /* Diagnostic: the per-tile candidate lists of camera rays the context built last (culled
@@ -307,16 +306,6 @@ RT_API rt_status rt_set_tile_order(rt_ctx* ctx, int mode);
  * launch per update, at most RT_MAX_UPDATE_QUEUES.  Pixel results are identical. */
 #define RT_MAX_UPDATE_QUEUES 4u
 RT_API rt_status rt_set_update_queues(rt_ctx* ctx, uint32_t queues);
-/* Runs of one-frame updates in rt_update_frames (after a reset frame, in windows of four
- * frames) replayed as instantiated HIP graphs: per window one graph launch instead of one
- * launch per part per frame; each frame's seed and sample-count hint reach the kernels
- * through a per-context device table written once per call.  The context caches the
- * graphs by their launches' arguments (images, camera, scene, stripe map, parts), so a
- * steady progressive render instantiates once.  AUTO (default): on; OFF: direct launches.
- * Pixel results are identical. */
-#define RT_UPDATE_GRAPHS_AUTO 0
-#define RT_UPDATE_GRAPHS_OFF 1
-RT_API rt_status rt_set_update_graphs(rt_ctx* ctx, int mode);
 /* Bounce paths (max_depth >= 2): RT_PATHS_PER_WAVE keeps every path in the wave of its
  * pixel (one tile per workgroup); RT_PATHS_PAIR runs two waves per tile on alternate
  * frames, the second handing its colours to the first through LDS (shorter chains for

@@ -187,16 +187,14 @@ def test_bench_dispatch_chain_matches_fixture(rt, cfg, single):
         p.close()
 
 
-@pytest.mark.parametrize("graphs", ["auto", "off"])
 @pytest.mark.parametrize("order", ["auto", "off"])
 @pytest.mark.parametrize("single", ["auto", "one"])
-def test_update_queues_match_one_launch(rt, single, order, graphs):
+def test_update_queues_match_one_launch(rt, single, order):
     """rt_set_update_queues: one-frame updates as 2-4 concurrent parts on their own streams
     (each part every queues-th workgroup of the cost order, or every queues-th band when
-    the order is off), launched directly or replayed as update graphs, leave both
-    ping-pong images bit-identical to one direct launch per update — whole image and a
-    rank share, across the reset frame, the order's first build and a second call — and
-    match the oracle's sampled pixels (tests/golden/bench_k3.npz)."""
+    the order is off) leave both ping-pong images bit-identical to one launch per update —
+    whole image and a rank share, across the reset frame, the order's first build and a
+    second call — and match the oracle's sampled pixels (tests/golden/bench_k3.npz)."""
     g = load_golden("bench_k3.npz")
     w, h = int(g["width"]), int(g["height"])
     cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
@@ -211,8 +209,6 @@ def test_update_queues_match_one_launch(rt, single, order, graphs):
             ref = None
             for q in (1, 2, 3, 4):
                 p.set_update_queues(q)
-                # (the reference images: one direct launch per update)
-                p.set_update_graphs("off" if q == 1 else graphs)
                 a, b = p.new_image(w, rows), p.new_image(w, rows)
                 n0 = p.update_frames(a, b, w, h, cam, sc, g["seeds"][:5], rank, nranks)
                 if n0 == 1:
@@ -220,7 +216,6 @@ def test_update_queues_match_one_launch(rt, single, order, graphs):
                 newest = p.update_frames(a, b, w, h, cam_t, sc, g["seeds"][5:25], rank, nranks)
                 info = p.last_launch_info()
                 assert info["queues"] == q and info["launches"] == 20 * q, (q, info)
-                assert info["graph_frames"] == (20 if graphs == "auto" and q > 1 else 0)
                 imgs = (host(b if newest == 1 else a), host(a if newest == 1 else b))
                 if ref is None:
                     ref = imgs
@@ -230,43 +225,6 @@ def test_update_queues_match_one_launch(rt, single, order, graphs):
                 else:
                     for x, y in zip(imgs, ref):
                         assert_same(x, y)
-    finally:
-        p.close()
-
-
-def test_update_graphs_match_direct(rt):
-    """Update graphs (rt_set_update_graphs): calls of 5 (with the reset frame), 7, 9, 4, 2
-    and 6 frames — windows of four replayed as graphs, the rest launched directly, the
-    cached graph reused across calls and image parities — leave both images bit-identical
-    to direct launches, whole image and a rank share, and report the replayed frames."""
-    w, h = 640, 360
-    sc = rt.synthetic_scene(500)
-    cam = camera(rt, w, h, depth=1, spp=1000, seed=0.40625)
-    cam_t = cam.with_fields(camera_has_moved=0.0)
-    seeds = rt.frame_seeds(0x61, 40)
-    calls = [5, 7, 9, 4, 2, 6]
-    p = rt.ComputeShaderPipeline(0)
-    p.set_frames_per_launch(1)
-    try:
-        for rank, nranks in ((0, 1), (1, 3)):
-            rows = rt.stripe_local_rows(h, rank, nranks)
-            out = {}
-            for mode in ("off", "auto"):
-                p.set_update_graphs(mode)
-                a, b = p.new_image(w, rows), p.new_image(w, rows)
-                f = 0
-                for i, n in enumerate(calls):
-                    newest = p.update_frames(a, b, w, h, cam if i == 0 else cam_t, sc,
-                                             seeds[f:f + n], rank, nranks)
-                    f += n
-                    info = p.last_launch_info()
-                    want = 0 if mode == "off" else ((n - (i == 0)) // 4) * 4
-                    assert info["graph_frames"] == want, (mode, i, info)
-                    if newest == 1:
-                        a, b = b, a
-                out[mode] = (host(a), host(b))
-            for x, y in zip(out["auto"], out["off"]):
-                assert_same(x, y)
     finally:
         p.close()
 

@@ -21,7 +21,7 @@ def header_functions():
 
 def test_library_exports_every_declared_symbol(rt):
     declared = header_functions()
-    assert len(declared) == 43
+    assert len(declared) == 42
     nm = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True,
                         text=True, check=True).stdout
     exported = set(re.findall(r" T (rt_\w+)$", nm, flags=re.M))
@@ -146,7 +146,6 @@ def test_argument_errors_without_device(rt):
     assert L.rt_set_frame_pairs(None, 0) == 6
     assert L.rt_set_tile_order(None, 0) == 6
     assert L.rt_set_update_queues(None, 1) == 6
-    assert L.rt_set_update_graphs(None, 0) == 6
     assert L.rt_get_frames_per_launch(None, None, None) == 6
     assert L.rt_selftest_fastmath(None, 0, None) == 6
     assert L.rt_last_launch_info(None, None) == 6

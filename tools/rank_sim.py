@@ -1,7 +1,7 @@
 """Per-rank frame time of the stripe partition on ONE GPU (diagnostic, not the bench): times
 rank 0's share of a W x H progressive render for world sizes 1, 2, 4, 8, i.e. what each rank
 of `bench.py --gpus N` computes per step, to predict strong-scaling efficiency without an
-8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] [RT_QUEUES=q] [RT_GRAPHS=auto|off] [RT_PATHS=auto|per_wave|pair|compact] python tools/rank_sim.py [K3|K2|K5] [steps]"""
+8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] [RT_QUEUES=q] [RT_PATHS=auto|per_wave|pair|compact] python tools/rank_sim.py [K3|K2|K5] [steps]"""
 import json
 import sys
 import time
@@ -37,8 +37,6 @@ def main(cfg="K3", steps=50):
         pipe.set_tile_order(os.environ.get("RT_TILE_ORDER", "auto"))
     if hasattr(rt._lib.lib(), "rt_set_update_queues"):
         pipe.set_update_queues(int(os.environ.get("RT_QUEUES", "0")))
-    if hasattr(rt._lib.lib(), "rt_set_update_graphs"):
-        pipe.set_update_graphs(os.environ.get("RT_GRAPHS", "auto"))
     base = None
     for world in (1, 2, 4, 8):
         r = StripeRenderer(pipe, w, h, 0, world)
@@ -59,9 +57,7 @@ def main(cfg="K3", steps=50):
                           "us_per_step": round(us, 2), "ideal_us": round(base / world, 2),
                           "predicted_efficiency": round(base / world / us, 3),
                           "host_issue_us_per_step": round(host_us, 2),
-                          "queues": pipe.last_launch_info().get("queues"),
-                          "graph_frames": pipe.last_launch_info().get("graph_frames")}),
-              flush=True)
+                          "queues": pipe.last_launch_info().get("queues")}), flush=True)
     pipe.close()
 
 
