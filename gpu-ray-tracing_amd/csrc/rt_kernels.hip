@@ -17,6 +17,7 @@
 #include "rt_device.h"
 #include "rt_kernels.h"
 
+#include <cstddef>
 #include <cstring>
 
 namespace rtk {
@@ -1365,9 +1366,11 @@ struct SingleParams {
     // step, first | step << 16 — one of the update's concurrent parts (launch_single)
     uint32_t lbands;
     float4 rs;             // (rf(sb), random_unit_vector(sb)) of frame 0, bounce 0
-    double disk_rcp[8];
     float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3];
     float defocus_angle;
+#if RT_SINGLE_DISK == 1
+    double disk_rcp[8];    // (the LDS-table form only: every byte here is host launch cost)
+#endif
 };
 
 // Tiles per wave of the two instances: kTraceSingle (whole-image launches) and
@@ -1738,7 +1741,9 @@ __device__ __forceinline__ void single_body(
             double v = 0.0;
 #pragma unroll
             for (uint32_t k = 0; k < 8u; ++k)
+#if RT_SINGLE_DISK == 1
                 if (threadIdx.x == k) v = p.disk_rcp[k];
+#endif
             s_disk_rcp[threadIdx.x] = v;
         }
         __syncthreads();
@@ -2667,7 +2672,7 @@ static void launch_bounce(const TraceParams& p, hipStream_t stream) {
 
 // kSingleWg waves of kPix tiles each per workgroup along a stripe band.
 template <int kPix>
-static void launch_single(const TraceParams& p, hipStream_t stream) {
+static hipError_t launch_single(const TraceParams& p, hipStream_t stream) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     const uint32_t per = kSingleWg * kPix;
     const uint32_t cols = (tiles_x + per - 1u) / per;
@@ -2687,7 +2692,7 @@ static void launch_single(const TraceParams& p, hipStream_t stream) {
             lbands = part | (parts << 16);
         }
     }
-    if (grid.x == 0 || grid.y == 0) return;
+    if (grid.x == 0 || grid.y == 0) return hipSuccess;
     SingleParams q;
     std::memset(&q, 0, sizeof(q));
     q.lbands = lbands;
@@ -2711,7 +2716,9 @@ static void launch_single(const TraceParams& p, hipStream_t stream) {
         q.n_exact = ng < (1u << 24) ? 1u : 0u;
     }
     q.rs = p.hint_rs[0];
+#if RT_SINGLE_DISK == 1
     for (int k = 0; k < 8; ++k) q.disk_rcp[k] = p.disk_rcp[k];
+#endif
     for (int i = 0; i < 3; ++i) {
         q.center[i] = p.center[i];
         q.vul[i] = p.vul[i];
@@ -2721,22 +2728,49 @@ static void launch_single(const TraceParams& p, hipStream_t stream) {
         q.ddv[i] = p.ddv[i];
     }
     q.defocus_angle = p.defocus_angle;
-    if (p.reset_first)
-        hipLaunchKernelGGL(rt_single_reset_kernel<kPix>, grid, dim3(64 * kSingleWg), 0, stream,
-                           p.cand, p.hx, p.in, p.width, p.height,
-                           pack_bands(p.band_first, p.band_step, false), order, q);
-    else
-        hipLaunchKernelGGL(rt_single_kernel<kPix>, grid, dim3(64 * kSingleWg), 0, stream,
-                           p.cand, p.hx, p.in, p.width, p.height,
-                           pack_bands(p.band_first, p.band_step, false), order, q);
+    // hipModuleLaunchKernel with the arguments packed in the kernel's layout and a cached
+    // function handle: no per-launch symbol lookup or per-argument marshalling (320-byte
+    // arguments: 4.2-4.4 against 5.0-6.0 µs of host time per launch through the
+    // hipLaunchKernelGGL path, profiles/r03j_launch_rate.jsonl) — the host's issue rate
+    // bounds small rank shares and the concurrent parts
+    struct {
+        const float4* cand;
+        const uint32_t* hx;
+        const float4* in;
+        uint32_t width, height, bands;
+        const uint32_t* order;
+        SingleParams q;
+    } args{p.cand, p.hx, p.in, p.width, p.height, pack_bands(p.band_first, p.band_step, false),
+           order, q};
+    static_assert(offsetof(decltype(args), q) == 48, "rt_single_kernel's argument layout");
+    size_t bytes = sizeof(args);
+    void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes,
+                     HIP_LAUNCH_PARAM_END};
+    // (function handles are per device: the caller's DeviceGuard has made it current)
+    constexpr int kMaxDevices = 64;
+    static hipFunction_t fn[kMaxDevices][2] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+    const int r = p.reset_first ? 1 : 0;
+    if (!fn[dev][r]) {
+        e = hipGetFuncBySymbol(&fn[dev][r],
+                               r ? reinterpret_cast<const void*>(&rt_single_reset_kernel<kPix>)
+                                 : reinterpret_cast<const void*>(&rt_single_kernel<kPix>));
+        if (e != hipSuccess) {
+            fn[dev][r] = nullptr;
+            return e;
+        }
+    }
+    return hipModuleLaunchKernel(fn[dev][r], grid.x, grid.y, 1, 64 * kSingleWg, 1, 1, 0, stream,
+                                 nullptr, extra);
 }
 
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
-    if (kernel == kTraceSingle)
-        launch_single<(int)kSinglePix>(p, stream);
-    else if (kernel == kTraceSingleOne)
-        launch_single<1>(p, stream);
-    else if (kernel == kTraceCulled)
+    if (kernel == kTraceSingle) return launch_single<(int)kSinglePix>(p, stream);
+    if (kernel == kTraceSingleOne) return launch_single<1>(p, stream);
+    if (kernel == kTraceCulled)
         launch_trace_as<kTraceCulled>(p, (size_t)p.lds_records * sizeof(float4), stream);
     else if (kernel == kTraceList)
         launch_trace_as<kTraceList>(p, 0, stream);

@@ -58,6 +58,38 @@ int main() {
                                 std::chrono::duration<double, std::micro>(t2 - t0).count() / n);
             }
         }
+    // the 320-byte kernel through hipModuleLaunchKernel with a cached function handle and a
+    // pre-packed argument buffer (HIP_LAUNCH_PARAM_BUFFER_POINTER): no per-launch symbol
+    // lookup or per-argument marshalling
+    {
+        hipFunction_t fn = nullptr;
+        CHECK(hipGetFuncBySymbol(&fn, reinterpret_cast<const void*>(&k_big)));
+        struct {
+            float* out;
+            Big b;
+        } packed{out, b};
+        size_t sz = sizeof(packed);
+        void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &packed, HIP_LAUNCH_PARAM_BUFFER_SIZE,
+                         &sz, HIP_LAUNCH_PARAM_END};
+        for (int ns : {1, 2}) {
+            for (int rep = 0; rep < 2; ++rep) {
+                CHECK(hipDeviceSynchronize());
+                const auto t0 = std::chrono::steady_clock::now();
+                for (int i = 0; i < n; ++i)
+                    CHECK(hipModuleLaunchKernel(fn, 1024, 1, 1, 256, 1, 1, 0, s[i % ns], nullptr,
+                                                extra));
+                const auto t1 = std::chrono::steady_clock::now();
+                CHECK(hipDeviceSynchronize());
+                const auto t2 = std::chrono::steady_clock::now();
+                if (rep)
+                    std::printf("{\"args\": \"320 B packed\", \"api\": \"hipModuleLaunchKernel\", "
+                                "\"streams\": %d, \"host_us_per_launch\": %.3f, "
+                                "\"gpu_us_per_launch\": %.3f}\n", ns,
+                                std::chrono::duration<double, std::micro>(t1 - t0).count() / n,
+                                std::chrono::duration<double, std::micro>(t2 - t0).count() / n);
+            }
+        }
+    }
     // a captured graph of `per` launches (the 320-byte kernel) replayed: host cost of one
     // hipGraphLaunch per `per` kernels
     for (int per : {20, 100}) {
