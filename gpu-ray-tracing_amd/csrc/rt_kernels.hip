@@ -2011,6 +2011,11 @@ __device__ __forceinline__ uint32_t compact_slot(bool live, uint32_t wave, uint3
 #ifndef RT_BOUNCE_MIN_WAVES
 #define RT_BOUNCE_MIN_WAVES 7
 #endif
+// RT_BOUNCE_PRIO: the first RT_BOUNCE_PRIO workgroups of the cost order run at raised wave
+// priority (s_setprio), 0 = off.
+#ifndef RT_BOUNCE_PRIO
+#define RT_BOUNCE_PRIO 0
+#endif
 #ifndef RT_BOUNCE_RELOAD
 #define RT_BOUNCE_RELOAD 1
 #endif
@@ -2045,10 +2050,16 @@ rt_bounce_kernel(const TraceParams p) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     uint32_t gx = blockIdx.x, lband = blockIdx.y;       // group of kW tiles
     if (p.tile_order) {                                 // costliest groups first
-        const uint32_t t = __builtin_amdgcn_readfirstlane(p.tile_order[blockIdx.y * gridDim.x +
-                                                                       blockIdx.x]);
+        const uint32_t pos = blockIdx.y * gridDim.x + blockIdx.x;
+        const uint32_t t = __builtin_amdgcn_readfirstlane(p.tile_order[pos]);
         gx = t & 0xFFFFu;
         lband = t >> 16;
+#if RT_BOUNCE_PRIO
+        // the costliest tiles' waves carry the launch's critical path (a small rank
+        // share's launch lasts as long as its heaviest tile's frames): they win the
+        // SIMD's instruction arbitration over the cheap waves that fill around them
+        if (pos < RT_BOUNCE_PRIO) __builtin_amdgcn_s_setprio(2);
+#endif
     }
     const uint32_t tx = kPair ? gx : gx * kW + wave;   // (pairs: both waves, one tile)
     const bool wave_in = tx < tiles_x;
