@@ -1400,6 +1400,12 @@ static_assert(kSinglePix >= 1 && kSinglePix <= 4, "1 to 4 tiles per wave");
 #define RT_SINGLE_WG 4
 #endif
 constexpr uint32_t kSingleWg = RT_SINGLE_WG;
+// RT_SINGLE_PRIO: the first RT_SINGLE_PRIO workgroups of wg_order (the costliest) run at
+// raised wave priority (s_setprio), so that on a SIMD shared with cheap waves the launch's
+// longest waves issue first; 0 = off.
+#ifndef RT_SINGLE_PRIO
+#define RT_SINGLE_PRIO 0
+#endif
 // sphere scan of the one-frame kernel: 0 = both tiles' lists in one loop, RT_LIST_CHUNK
 // records of each per step; k > 0 = each tile's list on its own, k records per step
 #ifndef RT_SINGLE_SCAN
@@ -1684,10 +1690,14 @@ __device__ __forceinline__ void single_body(
     // costliest are dispatched first and the cheap ones fill the tail
     uint32_t gx = blockIdx.x, lband = (p.lbands & 0xFFFFu) + blockIdx.y * (p.lbands >> 16);
     if (a_order) {   // (a leading, preloadable argument: one scalar load to the entry)
-        const uint32_t e = __builtin_amdgcn_readfirstlane(
-            a_order[blockIdx.y * gridDim.x + blockIdx.x]);
+        const uint32_t pos = blockIdx.y * gridDim.x + blockIdx.x;
+        const uint32_t e = __builtin_amdgcn_readfirstlane(a_order[pos]);
         gx = e & 0xFFFFu;
         lband = e >> 16;
+#if RT_SINGLE_PRIO
+        // (the costliest workgroups of the order: raised wave priority, see RT_SINGLE_PRIO)
+        if (pos < RT_SINGLE_PRIO) __builtin_amdgcn_s_setprio(2);
+#endif
     }
     SST_S(1, lband);
     const uint32_t tx0 = (gx * kSingleWg + wave) * S;

@@ -1,8 +1,9 @@
 """Per-rank frame time of the stripe partition on ONE GPU (diagnostic, not the bench): times
 rank 0's share of a W x H progressive render for world sizes 1, 2, 4, 8, i.e. what each rank
 of `bench.py --gpus N` computes per step, to predict strong-scaling efficiency without an
-8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] [RT_QUEUES=q] [RT_PATHS=auto|per_wave|pair|compact] python tools/rank_sim.py [K3|K2|K5] [steps]"""
+8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] [RT_QUEUES=q] [RT_REPS=r] [RT_PATHS=auto|per_wave|pair|compact] python tools/rank_sim.py [K3|K2|K5] [steps]"""
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -21,12 +22,12 @@ CONF = {"K2": (1920, 1080, rt.SCENE_THREE, 3, 1), "K3": (1920, 1080, rt.SCENE_N,
 def main(cfg="K3", steps=50):
     w, h, kind, n, depth = CONF[cfg]
     sc = rt.SphereCollection.generate(kind, n, 1)
-    seeds = rt.frame_seeds(0x5EED, steps + 69)
+    reps = int(os.environ.get("RT_REPS", "1"))
+    seeds = rt.frame_seeds(0x5EED, steps * reps + 69)
     settings = rt.CameraSettings(max_depth=depth, samples_per_pixel=1000)
     cam = rt.SceneCamera.from_settings(settings, w, h, float(seeds[0]))
     pipe = rt.ComputeShaderPipeline(0)
     pipe.set_spheres(sc)
-    import os
     pipe.set_frame_pairs(os.environ.get("RT_FRAME_PAIRS", "auto"))
     # RT_FPL=1: one launch per frame (the reference's dispatch structure)
     pipe.set_frames_per_launch(int(os.environ.get("RT_FPL", "0")))
@@ -43,20 +44,27 @@ def main(cfg="K3", steps=50):
         r.frames(cam, sc, seeds[:5])                       # reset frame + warmup
         cam_t = cam.with_fields(camera_has_moved=0.0)
         r.frames(cam_t, sc, seeds[5:69])                   # (tile costs of a long launch)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        t0 = time.perf_counter()
-        r.frames(cam_t, sc, seeds[69:69 + steps])
-        host_us = (time.perf_counter() - t0) * 1e6 / steps      # the issuing call's own time
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / steps
+        # RT_REPS timed blocks of `steps` frames (the median reported, all listed)
+        runs, host = [], []
+        for rep in range(reps):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            t0 = time.perf_counter()
+            off = 69 + rep * steps
+            r.frames(cam_t, sc, seeds[off:off + steps])
+            host.append((time.perf_counter() - t0) * 1e6 / steps)  # the issuing call's time
+            e1.record()
+            torch.cuda.synchronize()
+            runs.append(e0.elapsed_time(e1) * 1e3 / steps)
+        us = sorted(runs)[len(runs) // 2]
+        host_us = sorted(host)[len(host) // 2]
         base = base or us
         print(json.dumps({"cfg": cfg, "world": world, "rank0_rows": r.rows,
                           "us_per_step": round(us, 2), "ideal_us": round(base / world, 2),
                           "predicted_efficiency": round(base / world / us, 3),
                           "host_issue_us_per_step": round(host_us, 2),
+                          "runs_us": [round(x, 2) for x in runs],
                           "queues": pipe.last_launch_info().get("queues")}), flush=True)
     pipe.close()
 
