@@ -2022,9 +2022,12 @@ __device__ __forceinline__ uint32_t compact_slot(bool live, uint32_t wave, uint3
 #define RT_BOUNCE_MIN_WAVES 7
 #endif
 // RT_BOUNCE_PRIO: the first RT_BOUNCE_PRIO workgroups of the cost order run at raised wave
-// priority (s_setprio), 0 = off.
+// priority (s_setprio), 0 = off.  K5 per-rank prediction (profiles/r03m_rank_sim_k5_*: two
+// rounds of five 64-frame launches each, the same frames for every build): 8-rank share
+// 74.7 µs per spp off, 72.6 with 512 (efficiency 0.745 -> 0.769), 73.5 with 2048; the
+// whole image unchanged (445 µs per spp).
 #ifndef RT_BOUNCE_PRIO
-#define RT_BOUNCE_PRIO 0
+#define RT_BOUNCE_PRIO 512
 #endif
 #ifndef RT_BOUNCE_RELOAD
 #define RT_BOUNCE_RELOAD 1
