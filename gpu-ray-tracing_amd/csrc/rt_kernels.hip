@@ -287,6 +287,11 @@ constexpr bool fast_core(int bit) { return is_list_kernel(kScan) && (RT_FAST_COR
 #define RT_TRACE_DISK 1
 #endif
 constexpr int kTraceDisk = RT_TRACE_DISK;
+// get_ray: the lens centre copied to VGPRs before the defocus branch (1) or left to the
+// compiler (0)
+#ifndef RT_ORIGIN_VGPR
+#define RT_ORIGIN_VGPR 0
+#endif
 
 // Scan records are read through the constant address space: they do not change during a
 // launch, and only then may the compiler use scalar loads (s_load_dwordx8/16 into SGPRs)
@@ -742,11 +747,25 @@ __device__ __forceinline__ double disk_rcp_reg(float len2) {
     const uint32_t lo = (m << 28) | (__umul24(m, m) << 4);
     return __hiloint2double(0x3FF00000, (int)lo);
 }
-// kTable: 0 = sqrt_core / div_core, 1 = the LDS table (s_disk_rcp), 2 = disk_rcp_reg
+// kTable: 0 = sqrt_core / div_core, 1 = the LDS table (s_disk_rcp), 2 = disk_rcp_reg,
+// 3 = all-f32: len = sqrtf(len2) = 1 - m 2^-24 (bits 0x3F800000 - m) and y = RN32(1 / len)
+// = 1 + ((m + 1) >> 1) 2^-23 (m = 1: 1 + 2^-24 + 2^-48 rounds up; m = 3: 1 + 1.5 ulp + 9
+// 2^-48 rounds to 2 ulp) from the bits of len2, then one Markstein step — q0 = RN(a y), the
+// exact residual r = fma(-len, q0, a), q = RN(q0 + r y) — the correctly rounded a / len
+// for a correctly rounded y (checked against the IEEE division for all 2^32 seeds by
+// rt_selftest_fastmath).  Six f32 operations and four integer ones instead of the f64 path's
+// two conversions, multiply and conversion back per component.
 template <int kTable>
 __device__ __forceinline__ void disk_unit(float sa, float ca, float& ux, float& uy) {
     const float len2 = fmaf(sa, sa, ca * ca);
-    if (kTable) {
+    if (kTable == 3) {
+        const uint32_t m = (0x3F800001u - __float_as_uint(len2)) >> 1;
+        const float len = __uint_as_float(0x3F800000u - m);
+        const float y = __uint_as_float(0x3F800000u + ((m + 1u) >> 1));
+        const float qx = ca * y, qy = sa * y;
+        ux = fmaf(fmaf(-len, qx, ca), y, qx);
+        uy = fmaf(fmaf(-len, qy, sa), y, qy);
+    } else if (kTable) {
         const double y = kTable == 2 ? disk_rcp_reg(len2)
                                      : s_disk_rcp[__float_as_uint(len2) - kDiskLen2Lo];
         ux = (float)((double)ca * y);
@@ -774,14 +793,23 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
     const float sx = ((float)x + 0.5f) + offx;
     const float sy = ((float)y + 0.5f) + offy;
     const v3 pc = fmas(sy, cam.pdv, fmas(sx, cam.pdu, cam.vul));
+#if RT_ORIGIN_VGPR
+    // the lens centre in VGPRs first (the copies the lens-less path needs anyway), so that
+    // fma(u, ddu, centre) has one scalar operand (gfx950 VALU: one SGPR per instruction)
+    // instead of a second copy per component
+    v3 c0 = cam.center;
+    asm volatile("" : "+v"(c0.x), "+v"(c0.y), "+v"(c0.z));
+#else
+    const v3 c0 = cam.center;
+#endif
     if (cam.defocus_angle > 0.0f) {                     // defocus_disk_sample wgsl:327-331
         const float ang = (float)hash(seed + 1u) * 0x1.921fb4p-30f;  // 2*3.1415926 * rf
         float sa, ca, ux, uy;
         sincos_k(ang, sa, ca, cam.k1s, cam.k1c);
         disk_unit<kTable>(sa, ca, ux, uy);
-        o = fmas(uy, cam.ddv, fmas(ux, cam.ddu, cam.center));
+        o = fmas(uy, cam.ddv, fmas(ux, cam.ddu, c0));
     } else {
-        o = cam.center;
+        o = c0;
     }
     d = sub(pc, o);
 }
@@ -2603,11 +2631,14 @@ __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cn
         sincos_c(ang, sa, ca);
         const float len_ref = sqrtf(fmaf(sa, sa, ca * ca));
         const float ux_ref = ca / len_ref, uy_ref = sa / len_ref;
-        float ux, uy, tx, ty, gx, gy;
+        float ux, uy, tx, ty, gx, gy, fx, fy;
         disk_unit<0>(sa, ca, ux, uy);
         disk_unit<1>(sa, ca, tx, ty);
         disk_unit<2>(sa, ca, gx, gy);
-        bad0 += (__float_as_uint(ux) != __float_as_uint(ux_ref)) ||
+        disk_unit<3>(sa, ca, fx, fy);
+        bad0 += (__float_as_uint(fx) != __float_as_uint(ux_ref)) ||
+                (__float_as_uint(fy) != __float_as_uint(uy_ref)) ||
+                (__float_as_uint(ux) != __float_as_uint(ux_ref)) ||
                 (__float_as_uint(uy) != __float_as_uint(uy_ref)) ||
                 (__float_as_uint(tx) != __float_as_uint(ux_ref)) ||
                 (__float_as_uint(ty) != __float_as_uint(uy_ref)) ||
