@@ -130,6 +130,29 @@ __device__ __forceinline__ void sst_put(int k, unsigned long long t) {
 __device__ __forceinline__ unsigned long long rt_ballot(bool x) {
     return __builtin_amdgcn_ballot_w64(x);
 }
+// the one-frame kernel (and normalize_w)'s wave-uniform decisions from lane masks (mask_*) instead of ballots
+#ifndef RT_SINGLE_MASKS
+#define RT_SINGLE_MASKS 0
+#endif
+// Lane masks straight from one compare (llvm.amdgcn.icmp / fcmp: the v_cmp's SGPR result),
+// combined with & and | as 64-bit scalars.  A ballot of a boolean that crosses blocks or
+// combines earlier booleans compiles to a v_cndmask 0/1 + v_cmp_ne round trip (two 4-cycle
+// VALU operations) at every use; these do not (RT_SINGLE_MASKS).
+__device__ __forceinline__ uint64_t mask_ult(uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_uicmp(a, b, 36);          // ICMP_ULT
+}
+__device__ __forceinline__ uint64_t mask_uge(uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_uicmp(a, b, 35);          // ICMP_UGE
+}
+__device__ __forceinline__ uint64_t mask_ne(uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_uicmp(a, b, 33);          // ICMP_NE
+}
+__device__ __forceinline__ uint64_t mask_sge(int a, int b) {
+    return __builtin_amdgcn_sicmp(a, b, 39);          // ICMP_SGE
+}
+__device__ __forceinline__ uint64_t mask_not_lt(float a, float b) {
+    return __builtin_amdgcn_fcmpf(a, b, 11);          // FCMP_UGE: !(a < b)
+}
 
 // Constant address space (read-only for the whole launch; eligible for scalar loads).
 // (The host pass of hipcc also parses device code; there the qualifier is dropped.)
@@ -274,6 +297,10 @@ __device__ __forceinline__ bool acc_f64_ok(v3 num) {
     // |x| >= 2^-102 or x == +-0 (NaN, inf pass): one unsigned compare per channel
     return min(min(abs_bits(num.x) - 1u, abs_bits(num.y) - 1u), abs_bits(num.z) - 1u) >=
            kBits2m102 - 1u;
+}
+// (acc_f64_ok(num) == min_bits >= kBits2m102 - 1)
+__device__ __forceinline__ uint32_t acc_min_bits(v3 num) {
+    return min(min(abs_bits(num.x) - 1u, abs_bits(num.y) - 1u), abs_bits(num.z) - 1u);
 }
 __device__ __forceinline__ v3 acc_f64(v3 c, v3 num, double y) {
     return mk(c.x + (float)((double)num.x * y), c.y + (float)((double)num.y * y),
@@ -828,9 +855,11 @@ template <bool kFast>
 __device__ __forceinline__ v3 normalize_w(v3 v) {
     if (kFast) {
         const float dd = dot(v, v);
-        const bool in = __float_as_uint(dd) - kBits2m20 < kBits2p40 - kBits2m20 &&
-                        min(min(abs_bits(v.x), abs_bits(v.y)), abs_bits(v.z)) >= kBits2m100;
-        if (rt_ballot(!in) == 0ull) {
+        const uint32_t span = __float_as_uint(dd) - kBits2m20;
+        const uint32_t vmin = min(min(abs_bits(v.x), abs_bits(v.y)), abs_bits(v.z));
+        const bool in = span < kBits2p40 - kBits2m20 && vmin >= kBits2m100;
+        if ((RT_SINGLE_MASKS ? (mask_uge(span, kBits2p40 - kBits2m20) | mask_ult(vmin, kBits2m100))
+                             : rt_ballot(!in)) == 0ull) {
             const float len = sqrt_core(dd);
             const float y = rcp_refined(len);
             return mk(div_core(v.x, len, y), div_core(v.y, len, y), div_core(v.z, len, y));
@@ -1486,13 +1515,14 @@ constexpr int kSingleDisk = RT_SINGLE_DISK;
 // sets the scattered direction and attenuation, or black (metal absorbed).  r_sb / ruv are
 // the scatter's random numbers.  Lanes with !hit compute garbage that the caller drops.
 __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, v3 d,
-                                          float r_sb, v3 ruv, bool hit, v3& nd, v3& att,
-                                          bool& black) {
+                                          float r_sb, v3 ruv, bool hit, uint64_t hm, v3& nd,
+                                          v3& att, bool& black) {
     const v3 hp = fmas(t, d, o);
     const v3 rel = sub(hp, mk(pr.x, pr.y, pr.z));
     v3 outward;                                                   // wgsl:209
-    if (rt_ballot(hit && min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z)) <
-                            kBits2m100) == 0ull) {
+    const uint32_t rel_min = min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z));
+    if ((RT_SINGLE_MASKS ? (mask_ult(rel_min, kBits2m100) & hm)
+                         : rt_ballot(hit && rel_min < kBits2m100)) == 0ull) {
         const float y = rcp_refined(pr.w);
         outward = mk(div_core(rel.x, pr.w, y), div_core(rel.y, pr.w, y),
                      div_core(rel.z, pr.w, y));
@@ -1508,7 +1538,8 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
     att = mk(mat.x, mat.y, mat.z);
     black = false;
     const bool other = hit && !(mat.w < -1.0f);
-    if (rt_ballot(other) != 0ull && other) {
+    if ((RT_SINGLE_MASKS ? (mask_not_lt(mat.w, -1.0f) & hm) : rt_ballot(other)) != 0ull &&
+        other) {
         if (mat.w <= 1.0f) {                                      // metal wgsl:95-100
             const v3 refl = fmas(mat.w, ruv, normalize_w<true>(reflect(d, n)));
             black = !(dot(refl, n) > 0.0f);                       // wgsl:277-279
@@ -1555,6 +1586,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                                               const float4* const (&blk)[S],
                                               const uint32_t (&ncand)[S],
                                               const bool (&live)[S],
+                                              const uint64_t (&live_m)[S],
                                               const float4 (&bv)[S], float4* lblk,
                                               v3 (&col)[S]) {
     constexpr int K = RT_LIST_CHUNK;
@@ -1644,11 +1676,17 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
             hit[s] = live[s] && idx[s] >= 0;
             any = any || hit[s];
         }
+        uint64_t hm[S], any_m = 0;
+#pragma unroll
+        for (uint32_t s = 0; s < S; ++s) {
+            hm[s] = RT_SINGLE_MASKS ? (mask_sge(idx[s], 0) & live_m[s]) : 0ull;
+            any_m |= hm[s];
+        }
         if (RT_SKO & 8) {
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s)
                 if (hit[s]) cf[s] = mk(tmax[s], 0.5f, 0.5f);
-        } else if (rt_ballot(any) != 0ull) {
+        } else if ((RT_SINGLE_MASKS ? any_m : rt_ballot(any)) != 0ull) {
             float4 pr[S], mat[S];
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
@@ -1664,7 +1702,8 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
             }
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
-                if (RT_SINGLE_GATE && rt_ballot(hit[s]) == 0ull) continue;   // (sky tiles)
+                if (RT_SINGLE_GATE && (RT_SINGLE_MASKS ? hm[s] : rt_ballot(hit[s])) == 0ull)
+                    continue;                                     // (sky tiles)
                 float r_sb;
                 v3 ruv;
                 if (kUniRs) {
@@ -1677,8 +1716,8 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                 }
                 v3 nd, att;
                 bool blk_s;
-                shade_hit(pr[s], mat[s], tmax[s], o[s], d[s], r_sb, ruv, hit[s], nd, att,
-                          blk_s);
+                shade_hit(pr[s], mat[s], tmax[s], o[s], d[s], r_sb, ruv, hit[s], hm[s], nd,
+                          att, blk_s);
                 if (hit[s]) {                                     // wgsl:285-286
                     cf[s] = att;
                     dsky[s] = nd;
@@ -1763,6 +1802,12 @@ __device__ __forceinline__ void single_body(
                   : a_hx[min(tc[s].x, a_width - 1u)];
         hxy[s] = hx ^ hy;                                         // wgsl:309-310
     }
+    uint64_t valid_m[S];        // (RT_SINGLE_MASKS: tc[s].valid as a lane mask)
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s)
+        valid_m[s] = RT_SINGLE_MASKS
+                         ? (mask_ult(tc[s].x, a_width) & mask_ult(tc[s].y, a_height))
+                         : 0ull;
     // (issued after the seed-table loads: vmcnt waits in issue order, and the camera rays
     // need the seeds long before the scan and the accumulation need these)
 #pragma unroll
@@ -1812,6 +1857,7 @@ __device__ __forceinline__ void single_body(
     uint32_t n[S];
     bool pending[S];
     bool any_pending = true;
+    uint64_t pend_m = 0;        // (RT_SINGLE_MASKS: the lanes with pending pixels)
     if (p.hinted) {
         // Every pixel is expected to hold n_hint (the host's count bookkeeping): trace with
         // it while the accumulator loads are in flight, then verify.
@@ -1825,7 +1871,8 @@ __device__ __forceinline__ void single_body(
                 seed[s] = 1u + ng + p.seed_b;                     // wgsl:353
                 live[s] = tc[s].valid;
             }
-            single_sample<S, true>(p, cam, tc, hxy, seed, blk, ncand, live, bv, lblk, col);
+            single_sample<S, true>(p, cam, tc, hxy, seed, blk, ncand, live, valid_m, bv, lblk,
+                                   col);
         }
         any_pending = false;
 #pragma unroll
@@ -1843,12 +1890,14 @@ __device__ __forceinline__ void single_body(
 #else
             n[s] = kReset ? 0u : f2u(acc[s].w);                   // wgsl:339-350
             pending[s] = tc[s].valid && n[s] != ng;               // a foreign count
+            if (RT_SINGLE_MASKS && !kReset) pend_m |= mask_ne(n[s], ng) & valid_m[s];
 #endif
             any_pending = any_pending || pending[s];
             if (ng < spp) {                                       // wgsl:352-357
                 const v3 num = sub(col[s], c[s]);
                 if (RT_SINGLE_ACC_F64 && ng < (1u << 24) &&
-                    rt_ballot(tc[s].valid && !acc_f64_ok(num)) == 0ull) {
+                    (RT_SINGLE_MASKS ? (mask_ult(acc_min_bits(num), kBits2m102 - 1u) & valid_m[s])
+                                     : rt_ballot(tc[s].valid && !acc_f64_ok(num))) == 0ull) {
                     c[s] = acc_f64(c[s], num, p.rcp_hint);
                 } else {
                     const float k = (float)(ng + 1u);             // wgsl:356
@@ -1859,9 +1908,13 @@ __device__ __forceinline__ void single_body(
         }
     } else {
 #pragma unroll
-        for (uint32_t s = 0; s < S; ++s) pending[s] = tc[s].valid;
+        for (uint32_t s = 0; s < S; ++s) {
+            pending[s] = tc[s].valid;
+            pend_m |= valid_m[s];
+        }
     }
-    const bool wave_pending = rt_ballot(any_pending) != 0ull;
+    const bool wave_pending =
+        ((RT_SINGLE_MASKS && !RT_SINGLE_NCHK) ? pend_m : rt_ballot(any_pending)) != 0ull;
     if (wave_pending) {
         // pixels whose count is not the hinted one (or no hint): traced with their own
         // count and per-pixel random numbers
@@ -1877,7 +1930,10 @@ __device__ __forceinline__ void single_body(
             live[s] = pending[s] && n[s] < spp;                   // wgsl:352
             seed[s] = 1u + n[s] + p.seed_b;                       // wgsl:353
         }
-        single_sample<S, false>(p, cam, tc, hxy, seed, blk, ncand, live, bv, lblk, col);
+        uint64_t live_m[S];
+#pragma unroll
+        for (uint32_t s = 0; s < S; ++s) live_m[s] = RT_SINGLE_MASKS ? rt_ballot(live[s]) : 0ull;
+        single_sample<S, false>(p, cam, tc, hxy, seed, blk, ncand, live, live_m, bv, lblk, col);
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s)
             if (live[s]) {                                        // wgsl:356-357
@@ -1903,7 +1959,7 @@ __device__ __forceinline__ void single_body(
         band, 0, (int)(RT_STRIPE_ROWS * 16u * a_width), 0x00020000);
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s)
-        if (tc[s].valid) {                                        // wgsl:362-363
+        if (RT_SINGLE_MASKS || tc[s].valid) {                     // wgsl:362-363
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
             // (every pixel of a wave without a foreign count holds the hinted count after
             // the frame: f32 of it from the host)
@@ -1912,8 +1968,11 @@ __device__ __forceinline__ void single_body(
                                     : __float_as_uint((float)n[s]);
             const u32x4 v = {__float_as_uint(c[s].x), __float_as_uint(c[s].y),
                              __float_as_uint(c[s].z), nb};
+            // RT_SINGLE_MASKS: no branch — a pixel past the image edge stores to an offset
+            // past the band's buffer record, which the buffer unit drops
+            const uint32_t off = ((lane >> 3) * a_width + tc[s].x) * 16u;
             __builtin_amdgcn_raw_buffer_store_b128(
-                v, rsrc, (int)(((lane >> 3) * a_width + tc[s].x) * 16u), 0, 16);
+                v, rsrc, (int)((RT_SINGLE_MASKS && !tc[s].valid) ? 0x7FFFFFF0u : off), 0, 16);
         }
 #else
 #pragma unroll
