@@ -94,6 +94,10 @@ def parse():
     ap.add_argument("--queues", type=int, default=int(os.environ.get("RT_QUEUES", "0")),
                     help="concurrent parts per one-frame update (rt_set_update_queues; "
                          "0 = the library's choice)")
+    ap.add_argument("--submit", default=os.environ.get("RT_SUBMIT", "auto"),
+                    choices=["auto", "hip", "aql"],
+                    help="how one-frame updates are submitted (rt_set_update_submit): HIP "
+                         "launches (auto) or AQL packets on the context's HSA queues")
     ap.add_argument("--scan", default="culled", choices=["culled", "exhaustive"],
                     help="sphere-list scan: exact culling (default) or the reference's "
                          "exhaustive linear walk; images are bit-identical")
@@ -274,6 +278,7 @@ def main():
     if dispatch:
         pipe.set_frames_per_launch(1)          # one `update` launch per frame
     pipe.set_update_queues(args.queues)
+    pipe.set_update_submit(args.submit)
     # the job's one gather: RCCL behind the C ABI (rt_comm_create + rt_gather_stripes)
     use_abi = world > 1 and backend == "nccl" and os.environ.get("RT_GATHER", "abi") == "abi"
     comm = StripeComm.from_process_group(pipe) if use_abi else None
@@ -361,7 +366,7 @@ def main():
             "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
             "kernel": kernel, "kernel_avg_us": round(launch_s * 1e6, 2),
             "frames_per_launch": fpl, "launches_per_step": launches_per_step,
-            "queues": queues,
+            "queues": queues, "submit": info.get("submit"),
             "algorithmic_bytes_per_launch": bytes_launch,
             "binding": "valu",
             # the same bytes against the measured streaming floor of the pattern (no tracing)

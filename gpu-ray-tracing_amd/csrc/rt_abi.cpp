@@ -82,7 +82,7 @@ struct rt_ctx {
     };
     std::vector<CountRecord> counts;
     uint32_t frames_per_launch = 0;  // rt_update_frames fusion cap (0 = automatic)
-    rt_launch_info last = {0, 0, 0, -1, 0};  // the last call's launches (rt_last_launch_info)
+    rt_launch_info last = {0, 0, 0, -1, 0, 0};  // the last call's launches (rt_last_launch_info)
     int path_compaction = RT_PATHS_AUTO;
     int frame_pairs = RT_FRAME_PAIRS_AUTO;
     int single_kernel = RT_SINGLE_AUTO;
@@ -92,6 +92,11 @@ struct rt_ctx {
     hipStream_t aux[RT_MAX_UPDATE_QUEUES - 1] = {};
     hipEvent_t fork_ev = nullptr;
     hipEvent_t join_ev[RT_MAX_UPDATE_QUEUES - 1] = {};
+    // One-frame updates as AQL packets on the context's own HSA queues (rt_chain.cpp,
+    // rt_set_update_submit), created on first use.
+    int update_submit = RT_SUBMIT_AUTO;
+    rtc::Chain* chain = nullptr;
+    bool chain_tried = false;
 };
 
 namespace {
@@ -843,6 +848,21 @@ uint32_t update_parts(const rt_ctx* ctx, const rtk::TraceParams& p, int kernel) 
     return std::max(1u, std::min(q, p.local_bands));
 }
 
+// Parts of a one-frame update submitted as AQL packets: a packet costs the host ≈0.25 µs
+// (profiles/r03r_aql_probe.txt), so the host never bounds the parts; but four HSA queues
+// beside HIP's own measured 38.7 µs per K3 update against 20.4 with two
+// (profiles/r03s_ab_aql_nckarg.log): AUTO takes 2 from 2 000 tiles, else 1
+// (rt_set_update_queues overrides).
+constexpr uint64_t kAqlQueues4MinTiles = ~0ull, kAqlQueues2MinTiles = 2000;
+uint32_t update_parts_aql(const rt_ctx* ctx, const rtk::TraceParams& p) {
+    uint32_t q = ctx->update_queues;
+    if (q == 0) {
+        const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
+        q = tiles >= kAqlQueues4MinTiles ? 4u : tiles >= kAqlQueues2MinTiles ? 2u : 1u;
+    }
+    return std::max(1u, std::min(q, p.local_bands));
+}
+
 // The context's extra streams and fork/join events (created on first use, on ctx->device).
 rt_status ensure_aux_streams(rt_ctx* ctx, uint32_t n) {
     if (!ctx->fork_ev) {
@@ -880,12 +900,50 @@ rt_status join_aux(rt_ctx* ctx, uint32_t n, hipStream_t stream) {
 }
 
 void note_launch(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t frames,
-                 uint32_t parts = 1u) {
+                 uint32_t parts = 1u, bool aql = false) {
     ctx->last.launches += parts;
     ctx->last.queues = parts;
+    ctx->last.submit = aql ? RT_SUBMIT_AQL : RT_SUBMIT_HIP;
     ctx->last.frames += frames;
     ctx->last.max_frames_per_launch = std::max(ctx->last.max_frames_per_launch, frames);
     ctx->last.kernel = kernel != rtk::kTraceBounce ? kernel : RT_KERNEL_BOUNCE + (int)p.compact;
+}
+
+// The context's AQL chain if one-frame updates go through it (rt_set_update_submit AQL):
+// created on first use; the call fails with the reason when the machine does not offer it.
+rt_status usable_chain(rt_ctx* ctx, rtc::Chain** out) {
+    *out = nullptr;
+    // AUTO = HIP: AQL packets measured slower at every size (rt_abi.h rt_set_update_submit)
+    if (ctx->update_submit != RT_SUBMIT_AQL) return RT_OK;
+    if (!ctx->chain_tried) {
+        ctx->chain_tried = true;
+        rt_status st = RT_OK;
+        ctx->chain = rtc::chain_create(ctx->device, &st);
+        if (st != RT_OK) return st;
+    }
+    const char* why = "";
+    if (rtc::chain_ok(ctx->chain, &why)) {
+        *out = ctx->chain;
+        return RT_OK;
+    }
+    if (ctx->update_submit == RT_SUBMIT_AQL)
+        return fail(RT_ERR_HIP, std::string("AQL submission unavailable: ") + why);
+    return RT_OK;
+}
+
+// Whether plan_wg_order would issue work on the stream or reallocate for this launch (an
+// open AQL segment still reads the current order: it is closed first).
+bool wg_order_pending(const rt_ctx* ctx, const rtk::TraceParams& p, int kernel) {
+    const uint32_t parts = p.parts > 1u ? p.parts : 1u;
+    if ((kernel != rtk::kTraceSingle && kernel != rtk::kTraceSingleOne) || p.cand_k == 0 ||
+        p.local_bands < 2 || ctx->tile_order_mode == RT_TILE_ORDER_OFF)
+        return false;
+    const uint64_t gen = ctx->cand_gen;
+    if (ctx->band_gen != gen) return ctx->band_seen_gen == gen;   // builds on this launch
+    const uint32_t pix = kernel == rtk::kTraceSingle ? rtk::single_pix() : 1u;
+    const uint32_t per = rtk::single_wg_tiles(pix);
+    const uint64_t units = (uint64_t)((((p.width + 7u) >> 3) + per - 1u) / per) * p.local_bands;
+    return units > ctx->wg_cap || ctx->wg_pix != pix || ctx->wg_parts != parts;
 }
 
 // Shared body of rt_update / rt_render / rt_render_stripes: `frames` accumulated in
@@ -1012,6 +1070,7 @@ rt_status rt_destroy(rt_ctx* ctx) {
             if (ctx->join_ev[k]) (void)hipEventDestroy(ctx->join_ev[k]);
         }
         if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
+        rtc::chain_destroy(ctx->chain);
     }
     delete ctx;
     return RT_OK;
@@ -1063,6 +1122,38 @@ rt_status rt_set_update_queues(rt_ctx* ctx, uint32_t queues) {
     if (queues > RT_MAX_UPDATE_QUEUES)
         return fail(RT_ERR_INVALID_ARGUMENT, "queues above RT_MAX_UPDATE_QUEUES");
     ctx->update_queues = queues;
+    return RT_OK;
+}
+
+rt_status rt_set_update_submit(rt_ctx* ctx, int mode) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (mode != RT_SUBMIT_AUTO && mode != RT_SUBMIT_HIP && mode != RT_SUBMIT_AQL)
+        return fail(RT_ERR_INVALID_ARGUMENT, "unknown submit mode");
+    ctx->update_submit = mode;
+    return RT_OK;
+}
+
+rt_status rt_update_submit_status(rt_ctx* ctx, int* aql_available, uint32_t* go_give_ups,
+                                  uint64_t* packets) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    if (!ctx->chain_tried) {
+        ctx->chain_tried = true;
+        rt_status st = RT_OK;
+        ctx->chain = rtc::chain_create(ctx->device, &st);
+        if (st != RT_OK) return st;
+    }
+    const char* why = "";
+    const bool ok = rtc::chain_ok(ctx->chain, &why);
+    if (aql_available) *aql_available = ok ? 1 : 0;
+    if (packets) *packets = rtc::chain_packets(ctx->chain);
+    if (go_give_ups) {
+        *go_give_ups = 0;
+        if (ok)
+            if (rt_status s = rtc::chain_errors(ctx->chain, go_give_ups)) return s;
+    }
+    if (!ok) fail(RT_OK, std::string("AQL submission unavailable: ") + why);
     return RT_OK;
 }
 
@@ -1149,9 +1240,16 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
     // instances run one frame per launch.
     const uint32_t per = frames_per_launch_for(ctx, p);
     int cur = 0;
-    ctx->last = {0, 0, 0, -1, 0};
+    ctx->last = {0, 0, 0, -1, 0, 0};
     uint32_t aux_live = 0;      // aux streams with work of this call not yet joined
     bool forked = false;        // aux streams ordered after the last work on `stream`
+    // One-frame launches of the one-frame instances go out as AQL packets when the call has
+    // two or more of them (rt_set_update_submit; a single update gains nothing from it).
+    rtc::Chain* chain = nullptr;
+    if (per == 1u && frames >= 2u)
+        if (rt_status s = usable_chain(ctx, &chain)) return s;
+    bool seg_open = false;      // an AQL segment of this call is open
+    uint32_t seg_parts = 0, seg_packets = 0;
     for (uint32_t f0 = 0; f0 < frames; f0 += per) {
         const uint32_t nf = std::min<uint32_t>(per, frames - f0);
         p.in = img[cur];
@@ -1187,10 +1285,17 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
             kernel = quad ? rtk::kTraceListQuad : rtk::kTraceListPair;
         }
         kernel = single_or(ctx, p, kernel);
-        const uint32_t parts = update_parts(ctx, p, kernel);
+        const bool aql = chain && nf == 1u &&
+                         (kernel == rtk::kTraceSingle || kernel == rtk::kTraceSingleOne);
+        const uint32_t parts = aql ? update_parts_aql(ctx, p) : update_parts(ctx, p, kernel);
         p.parts = parts;
         p.part = 0;
-        if (parts == 1u && aux_live) {          // back to one launch: wait for the parts
+        if (seg_open && (!aql || parts != seg_parts || wg_order_pending(ctx, p, kernel) ||
+                         seg_packets + parts > rtc::kMaxSegmentPackets)) {
+            if (rt_status s = rtc::chain_end(chain, stream)) return s;
+            seg_open = false;
+        }
+        if ((parts == 1u || aql) && aux_live) {  // back to one launch: wait for the parts
             if (rt_status s = join_aux(ctx, aux_live, stream)) return s;
             aux_live = 0;
             forked = false;
@@ -1198,7 +1303,20 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         const uint64_t builds = ctx->wg_builds;
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         if (rt_status s = plan_wg_order(ctx, p, kernel, stream)) return s;
-        if (parts > 1u) {
+        if (aql) {
+            // frame f of part k is a packet on the chain's queue k, after part k's frame f - 1
+            if (!seg_open) {
+                if (rt_status s = rtc::chain_begin(chain, stream, parts)) return s;
+                seg_open = true;
+                seg_parts = parts;
+                seg_packets = 0;
+            }
+            for (uint32_t k = 0; k < parts; ++k) {
+                p.part = k;
+                if (rt_status s = rtc::chain_frame(chain, p, kernel, k)) return s;
+            }
+            seg_packets += parts;
+        } else if (parts > 1u) {
             // every part's next frame reads only the pixels its own previous frame wrote;
             // what `stream` prepared (lists, order, the input image) is forked to the others
             if (rt_status s = ensure_aux_streams(ctx, parts - 1u)) return s;
@@ -1217,7 +1335,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
             if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         }
         finish_tile_order(ctx, p);
-        note_launch(ctx, p, kernel, nf, parts);
+        note_launch(ctx, p, kernel, nf, parts, aql);
         // frame f of the launch wrote img[(cur + 1 + f) % 2]
         const int newest = (nf & 1u) ? 1 - cur : cur;
         if (known) {
@@ -1229,7 +1347,9 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         }
         cur = newest;
     }
-    if (aux_live)   // the call's work ends on the caller's stream
+    if (seg_open)   // the call's work ends on the caller's stream
+        if (rt_status s = rtc::chain_end(chain, stream)) return s;
+    if (aux_live)
         if (rt_status s = join_aux(ctx, aux_live, stream)) return s;
     if (out_newest) *out_newest = cur;
     return RT_OK;

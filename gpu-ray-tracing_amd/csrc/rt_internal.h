@@ -1,5 +1,5 @@
 // rt_internal.h — helpers shared by the C-ABI translation units of librt_hip.so
-// (rt_abi.cpp, rt_comm.cpp).  Internal; not part of the public boundary.
+// (rt_abi.cpp, rt_comm.cpp, rt_chain.cpp).  Internal; not part of the public boundary.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -33,3 +33,27 @@ struct DeviceGuard {
 };
 
 }  // namespace rti
+
+namespace rtk {
+struct TraceParams;
+}
+
+// One-frame updates as AQL packets on context-owned HSA queues (rt_chain.cpp).  A segment
+// is begin, up to kMaxSegmentPackets frame packets (one per frame and part, part k on queue
+// k), end; it is ordered after the work issued on `stream` before begin, and `stream`'s
+// later work after it.  chain_create never fails softly: chain_ok tells whether the
+// machine offers what the chain needs (why: the reason if not), a hard error is returned.
+namespace rtc {
+struct Chain;
+constexpr uint32_t kMaxSegmentPackets = 1024;
+Chain* chain_create(int device, rt_status* status);
+void chain_destroy(Chain* c);
+bool chain_ok(const Chain* c, const char** why);
+rt_status chain_begin(Chain* c, hipStream_t stream, uint32_t parts);
+rt_status chain_frame(Chain* c, const rtk::TraceParams& p, int kernel, uint32_t part);
+rt_status chain_end(Chain* c, hipStream_t stream);
+// go waits that gave up (the segment ran before the caller's stream reached it); waits for
+// every segment in flight
+rt_status chain_errors(Chain* c, uint32_t* out);
+uint64_t chain_packets(const Chain* c);
+}  // namespace rtc

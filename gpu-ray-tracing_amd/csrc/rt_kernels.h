@@ -194,6 +194,18 @@ inline void part_range(uint32_t n, uint32_t parts, uint32_t k, uint32_t& first, 
 }
 uint32_t single_wg_tiles(uint32_t pix);
 uint32_t single_pix();   // tiles per wave of kTraceSingle
+// Frame chains (rt_chain.cpp): one-frame launches submitted as AQL packets.  The chain
+// kernels (rt_chain_kernel / rt_chain_reset_kernel for one tile or kTraceSingle's tiles per
+// wave, the go and the done packet's kernels), a part of each mangled name to find them
+// among the code object's symbols, and the packet's kernel arguments for one part of a
+// one-frame launch (chain_args: bytes written, 0 = the part has no workgroup).
+constexpr int kChainPix1 = 0, kChainPix1Reset = 1, kChainPix = 2, kChainPixReset = 3,
+              kChainGo = 4, kChainDone = 5, kChainKernels = 6;
+constexpr uint32_t kHiddenArgsBytes = 256;   // code object v5 hidden arguments
+hipError_t chain_load_kernels();
+const char* chain_kernel_symbol(int which);
+uint32_t chain_args(const TraceParams& p, int kernel, unsigned char* out, uint32_t cap,
+                    uint32_t grid[2], uint32_t* group_threads, int* which);
 hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t width,
                                uint32_t height, uint32_t nranks, uint32_t max_local_rows,
                                hipStream_t stream);

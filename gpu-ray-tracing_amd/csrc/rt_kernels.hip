@@ -1428,6 +1428,9 @@ struct SingleParams {
 #if RT_SINGLE_DISK == 1
     double disk_rcp[8];    // (the LDS-table form only: every byte here is host launch cost)
 #endif
+    // the launch's workgroups per row (rt_chain_kernel reads it here instead of the hidden
+    // kernel arguments: its packets are written by rt_chain.cpp)
+    uint32_t grid_x;
 };
 
 // Tiles per wave of the two instances: kTraceSingle (whole-image launches) and
@@ -1738,12 +1741,14 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
 // separate kernel (rt_single_reset_kernel), so that the steady-state kernel carries no
 // per-pixel selects between the loaded and the zero accumulator, and the reset kernel no
 // accumulator load at all.
-template <int kPix, bool kReset>
+template <int kPix, bool kReset, bool kChain>
 __device__ __forceinline__ void single_body(
     const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const uint32_t* __restrict__ a_order, const SingleParams& p) {
     static_assert(kPix >= 1 && kPix <= 4, "1 to 4 tiles per wave");
+    static_assert(!kChain || (RT_SINGLE_WT && !(RT_SKO & 16)),
+                  "frame chains hand the image over through write-through stores");
     constexpr uint32_t S = kPix;
     WAVE_TRACE(0);
 #if RT_SSTAMPS
@@ -1757,7 +1762,7 @@ __device__ __forceinline__ void single_body(
     // costliest are dispatched first and the cheap ones fill the tail
     uint32_t gx = blockIdx.x, lband = (p.lbands & 0xFFFFu) + blockIdx.y * (p.lbands >> 16);
     if (a_order) {   // (a leading, preloadable argument: one scalar load to the entry)
-        const uint32_t pos = blockIdx.y * gridDim.x + blockIdx.x;
+        const uint32_t pos = blockIdx.y * (kChain ? p.grid_x : gridDim.x) + blockIdx.x;
         const uint32_t e = __builtin_amdgcn_readfirstlane(a_order[pos]);
         gx = e & 0xFFFFu;
         lband = e >> 16;
@@ -1814,11 +1819,27 @@ __device__ __forceinline__ void single_body(
     for (uint32_t s = 0; s < S; ++s)
         bv[s] = (kSingleLds<S> && tx0 + s < tiles_x) ? blk[s][lane]
                                                       : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    // Frame chains (rt_chain.cpp): consecutive frames of a part are AQL packets with no
+    // cache acquire between them, so the accumulator the previous frame stored (write-
+    // through, sc1) is read with sc1 loads: this CU's L1 may hold lines of an older frame.
+    if (kChain && !kReset) {
+        const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)a_in, 0, (int)0x7FFFFFFF, 0x00020000);
 #pragma unroll
-    for (uint32_t s = 0; s < S; ++s)
-        acc[s] = (RT_SKO & 1) ? make_float4(0.0f, 0.0f, 0.0f, (float)p.n_hint)
-                 : kReset     ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)   // (discarded: no load)
-                              : a_in[tc[s].valid ? tc[s].idx : 0];                // wgsl:339
+        for (uint32_t s = 0; s < S; ++s) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+                rin, (int)((tc[s].valid ? tc[s].idx : 0) * 16u), 0, 16);   // sc1, wgsl:339
+            acc[s] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y),
+                                 __uint_as_float(v.z), __uint_as_float(v.w));
+        }
+    } else {
+#pragma unroll
+        for (uint32_t s = 0; s < S; ++s)
+            acc[s] = (RT_SKO & 1) ? make_float4(0.0f, 0.0f, 0.0f, (float)p.n_hint)
+                     : kReset     ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)   // (discarded: no load)
+                                  : a_in[tc[s].valid ? tc[s].idx : 0];            // wgsl:339
+    }
     if (kSingleDisk == 1 && p.defocus_angle > 0.0f) {             // (disk_unit's table)
         if (threadIdx.x < 8u) {
             double v = 0.0;
@@ -1994,14 +2015,55 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single
     const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const uint32_t* __restrict__ a_order, const SingleParams p) {
-    single_body<kPix, false>(a_cand, a_hx, a_in, a_width, a_height, a_bands, a_order, p);
+    single_body<kPix, false, false>(a_cand, a_hx, a_in, a_width, a_height, a_bands, a_order, p);
 }
 template <int kPix>
 __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_single_reset_kernel(
     const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const uint32_t* __restrict__ a_order, const SingleParams p) {
-    single_body<kPix, true>(a_cand, a_hx, a_in, a_width, a_height, a_bands, a_order, p);
+    single_body<kPix, true, false>(a_cand, a_hx, a_in, a_width, a_height, a_bands, a_order, p);
+}
+// The same kernels for frame chains (rt_chain.cpp: one AQL packet per frame and part on
+// context-owned HSA queues; accumulator loads sc1, see single_body).
+template <int kPix>
+__global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_chain_kernel(
+    const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
+    const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
+    const uint32_t* __restrict__ a_order, const SingleParams p) {
+    single_body<kPix, false, true>(a_cand, a_hx, a_in, a_width, a_height, a_bands, a_order, p);
+}
+template <int kPix>
+__global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_chain_reset_kernel(
+    const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
+    const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
+    const uint32_t* __restrict__ a_order, const SingleParams p) {
+    single_body<kPix, true, true>(a_cand, a_hx, a_in, a_width, a_height, a_bands, a_order, p);
+}
+// 10 s at s_memrealtime's 100 MHz: the caller's stream work queued ahead of a chain
+constexpr uint64_t kChainGoTicks = 1000000000ull;
+// A chain's first packet: wait until the caller's stream has reached the chain (its
+// hipStreamWriteValue32 of `want` into *go, signal memory).  Bounded (s_memrealtime, 100
+// MHz): a wait that gives up counts in *err and the call reports an error.
+__global__ __launch_bounds__(64) void rt_chain_go_kernel(const uint32_t* go, uint32_t want,
+                                                         uint32_t* err) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+        const uint32_t v = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        if ((int32_t)(v - want) >= 0) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kChainGoTicks) {
+            if (threadIdx.x == 0u) atomicAdd(err, 1u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+// A chain's last packet (barrier bit: after every frame): the caller's stream, waiting in
+// hipStreamWaitValue32 for `value`, continues.
+__global__ __launch_bounds__(64) void rt_chain_done_kernel(uint32_t* done, uint32_t value) {
+    if (threadIdx.x == 0u)
+        __hip_atomic_store(done, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---- Bounce paths with workgroup-wide compaction (kTraceBounce) -----------------------
@@ -2784,15 +2846,27 @@ static void launch_bounce(const TraceParams& p, hipStream_t stream) {
         hipLaunchKernelGGL(rt_bounce_kernel<kBounceWave>, grid, dim3(64), lds, stream, p);
 }
 
-// kSingleWg waves of kPix tiles each per workgroup along a stripe band.
+// The explicit arguments of rt_single_kernel / rt_chain_kernel, in the kernels' layout.
+struct SingleArgs {
+    const float4* cand;
+    const uint32_t* hx;
+    const float4* in;
+    uint32_t width, height, bands;
+    const uint32_t* order;
+    SingleParams q;
+};
+static_assert(offsetof(SingleArgs, q) == 48, "rt_single_kernel's argument layout");
+
+// One part of a one-frame launch (kSingleWg waves of kPix tiles each per workgroup along a
+// stripe band): its arguments and grid; false when the part has no workgroup.
 template <int kPix>
-static hipError_t launch_single(const TraceParams& p, hipStream_t stream) {
+static bool single_args(const TraceParams& p, SingleArgs& args, dim3& grid) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     const uint32_t per = kSingleWg * kPix;
     const uint32_t cols = (tiles_x + per - 1u) / per;
     const uint32_t parts = p.parts > 1u ? p.parts : 1u, part = parts > 1u ? p.part : 0u;
     // this part's workgroups: its sub-list of the order, or every parts-th local band
-    dim3 grid(cols, p.local_bands);
+    grid = dim3(cols, p.local_bands);
     const uint32_t* order = p.wg_order;
     uint32_t lbands = 1u << 16;
     if (parts > 1u) {
@@ -2806,9 +2880,16 @@ static hipError_t launch_single(const TraceParams& p, hipStream_t stream) {
             lbands = part | (parts << 16);
         }
     }
-    if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    SingleParams q;
-    std::memset(&q, 0, sizeof(q));
+    if (grid.x == 0 || grid.y == 0) return false;
+    SingleParams& q = args.q;
+    std::memset(&args, 0, sizeof(args));
+    args.cand = p.cand;
+    args.hx = p.hx;
+    args.in = p.in;
+    args.width = p.width;
+    args.height = p.height;
+    args.bands = pack_bands(p.band_first, p.band_step, false);
+    args.order = order;
     q.lbands = lbands;
     q.out = p.out;
     q.geom = p.geom;
@@ -2842,21 +2923,20 @@ static hipError_t launch_single(const TraceParams& p, hipStream_t stream) {
         q.ddv[i] = p.ddv[i];
     }
     q.defocus_angle = p.defocus_angle;
+    q.grid_x = grid.x;
+    return true;
+}
+
+template <int kPix>
+static hipError_t launch_single(const TraceParams& p, hipStream_t stream) {
+    SingleArgs args;
+    dim3 grid;
+    if (!single_args<kPix>(p, args, grid)) return hipSuccess;
     // hipModuleLaunchKernel with the arguments packed in the kernel's layout and a cached
     // function handle: no per-launch symbol lookup or per-argument marshalling (320-byte
     // arguments: 4.2-4.4 against 5.0-6.0 µs of host time per launch through the
     // hipLaunchKernelGGL path, profiles/r03j_launch_rate.jsonl) — the host's issue rate
     // bounds small rank shares and the concurrent parts
-    struct {
-        const float4* cand;
-        const uint32_t* hx;
-        const float4* in;
-        uint32_t width, height, bands;
-        const uint32_t* order;
-        SingleParams q;
-    } args{p.cand, p.hx, p.in, p.width, p.height, pack_bands(p.band_first, p.band_step, false),
-           order, q};
-    static_assert(offsetof(decltype(args), q) == 48, "rt_single_kernel's argument layout");
     size_t bytes = sizeof(args);
     void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes,
                      HIP_LAUNCH_PARAM_END};
@@ -2879,6 +2959,71 @@ static hipError_t launch_single(const TraceParams& p, hipStream_t stream) {
     }
     return hipModuleLaunchKernel(fn[dev][r], grid.x, grid.y, 1, 64 * kSingleWg, 1, 1, 0, stream,
                                  nullptr, extra);
+}
+
+// ---- Frame chains (rt_chain.cpp) ----------------------------------------------------------
+// The code object's chain kernels: [pix == 1 ? 0 : 1][reset], the go and the done kernel.
+// hipGetFuncBySymbol makes HIP load the code object on the current device, so that the
+// HSA loader lists their symbols (rt_chain.cpp looks them up by these mangled-name parts).
+hipError_t chain_load_kernels() {
+    const void* k[] = {reinterpret_cast<const void*>(&rt_chain_kernel<1>),
+                       reinterpret_cast<const void*>(&rt_chain_reset_kernel<1>),
+                       reinterpret_cast<const void*>(&rt_chain_kernel<(int)kSinglePix>),
+                       reinterpret_cast<const void*>(&rt_chain_reset_kernel<(int)kSinglePix>),
+                       reinterpret_cast<const void*>(&rt_chain_go_kernel),
+                       reinterpret_cast<const void*>(&rt_chain_done_kernel)};
+    for (const void* f : k) {
+        hipFunction_t h = nullptr;
+        hipError_t e = hipGetFuncBySymbol(&h, f);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+const char* chain_kernel_symbol(int which) {
+    // (Itanium mangling of rtk::rt_chain_kernel<N> etc.: "ILi<N>E" is the template argument)
+    static const char* const pix1[2] = {"15rt_chain_kernelILi1EE", "21rt_chain_reset_kernelILi1EE"};
+    static const char* const pix2[2] = {"15rt_chain_kernelILi2EE", "21rt_chain_reset_kernelILi2EE"};
+    static const char* const pix3[2] = {"15rt_chain_kernelILi3EE", "21rt_chain_reset_kernelILi3EE"};
+    static const char* const pix4[2] = {"15rt_chain_kernelILi4EE", "21rt_chain_reset_kernelILi4EE"};
+    const char* const* big = kSinglePix == 2 ? pix2 : kSinglePix == 3 ? pix3 : kSinglePix == 4 ? pix4 : pix1;
+    switch (which) {
+        case kChainPix1: return pix1[0];
+        case kChainPix1Reset: return pix1[1];
+        case kChainPix: return big[0];
+        case kChainPixReset: return big[1];
+        case kChainGo: return "18rt_chain_go_kernel";
+        default: return "20rt_chain_done_kernel";
+    }
+}
+// The kernel arguments of one part of a one-frame launch of `kernel` (kTraceSingle /
+// kTraceSingleOne) for an AQL packet: the explicit arguments, then the hidden ones of code
+// object v5 at the next 8-byte boundary (block counts, group sizes, grid dimensions; the
+// chain kernels read none of them — the workgroups per row come in SingleParams::grid_x).
+// Returns the bytes written (0: the part has no workgroup), the grid in workgroups and the
+// chain kernel (kChain*).
+uint32_t chain_args(const TraceParams& p, int kernel, unsigned char* out, uint32_t cap,
+                    uint32_t grid[2], uint32_t* group_threads, int* which) {
+    SingleArgs args;
+    dim3 g;
+    const bool one = kernel == kTraceSingleOne;
+    const bool any = one ? single_args<1>(p, args, g) : single_args<(int)kSinglePix>(p, args, g);
+    if (!any) return 0;
+    const uint32_t hb = (uint32_t)((sizeof(args) + 7u) & ~(size_t)7u);
+    const uint32_t total = hb + kHiddenArgsBytes;
+    if (total > cap) return 0;
+    std::memset(out, 0, total);
+    std::memcpy(out, &args, sizeof(args));
+    const uint32_t bc[3] = {g.x, g.y, 1u};
+    const uint16_t gs[3] = {(uint16_t)(64u * kSingleWg), 1u, 1u};
+    const uint16_t dims = 2;
+    std::memcpy(out + hb, bc, sizeof(bc));                 // hidden_block_count_x/y/z
+    std::memcpy(out + hb + 12, gs, sizeof(gs));            // hidden_group_size_x/y/z
+    std::memcpy(out + hb + 64, &dims, sizeof(dims));       // hidden_grid_dims
+    grid[0] = g.x;
+    grid[1] = g.y;
+    *group_threads = 64u * kSingleWg;
+    *which = (one ? kChainPix1 : kChainPix) + (p.reset_first ? 1 : 0);
+    return total;
 }
 
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {

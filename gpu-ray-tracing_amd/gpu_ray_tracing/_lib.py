@@ -120,6 +120,9 @@ _SIGS = {
     "rt_set_frame_pairs": (ctypes.c_int, [P, ctypes.c_int]),
     "rt_set_tile_order": (ctypes.c_int, [P, ctypes.c_int]),
     "rt_set_update_queues": (ctypes.c_int, [P, U32]),
+    "rt_set_update_submit": (ctypes.c_int, [P, ctypes.c_int]),
+    "rt_update_submit_status": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(U32),
+                                               ctypes.POINTER(ctypes.c_uint64)]),
     "rt_last_launch_info": (ctypes.c_int, [P, P]),
     "rt_set_path_compaction": (ctypes.c_int, [P, ctypes.c_int]),
     "rt_set_single_kernel": (ctypes.c_int, [P, ctypes.c_int]),
@@ -139,7 +142,7 @@ _SIGS = {
 class LaunchInfoC(ctypes.Structure):
     """rt_launch_info (rt_abi.h)."""
     _fields_ = [("launches", U32), ("frames", U32), ("max_frames_per_launch", U32),
-                ("kernel", ctypes.c_int32), ("queues", U32)]
+                ("kernel", ctypes.c_int32), ("queues", U32), ("submit", U32)]
 
 _lib = None
 

@@ -84,6 +84,22 @@ class ComputeShaderPipeline:
         parts on their own streams (0 = automatic, 1 = one launch per update)."""
         _lib.call("rt_set_update_queues", self._ctx, int(queues))
 
+    def set_update_submit(self, mode: str) -> None:
+        """rt_set_update_submit: how update_frames submits one-frame updates — "hip" (HIP
+        launches; "auto" = hip) or "aql" (AQL packets on the context's own HSA queues, an
+        error if unavailable; measured slower, opt-in); identical pixels."""
+        _lib.call("rt_set_update_submit", self._ctx, {"auto": 0, "hip": 1, "aql": 2}[mode])
+
+    def submit_status(self) -> dict:
+        """rt_update_submit_status: whether AQL submission is available (and why not), the go
+        waits that gave up (0 in a correct run) and the AQL packets submitted so far."""
+        avail, give_ups, packets = ctypes.c_int(0), _lib.U32(0), ctypes.c_uint64(0)
+        _lib.call("rt_update_submit_status", self._ctx, ctypes.byref(avail),
+                  ctypes.byref(give_ups), ctypes.byref(packets))
+        why = "" if avail.value else _lib.lib().rt_last_error().decode()
+        return {"aql_available": bool(avail.value), "go_give_ups": int(give_ups.value),
+                "packets": int(packets.value), "why": why}
+
     def set_path_compaction(self, mode: str) -> None:
         """rt_set_path_compaction for bounce launches: "auto" (default), "per_wave",
         "compact" (paths repacked across four waves after every bounce) or "pair" (two waves
@@ -107,11 +123,16 @@ class ComputeShaderPipeline:
 
     def last_launch_info(self) -> dict:
         """rt_last_launch_info: what the last trace call launched — launches, frames,
-        max_frames_per_launch, kernel (RT_KERNEL_* id) and its rocprofv3 name."""
+        max_frames_per_launch, kernel (RT_KERNEL_* id) and its rocprofv3 name, the parts
+        (queues) and the submission ("hip" or "aql")."""
         info = _lib.LaunchInfoC()
         _lib.call("rt_last_launch_info", self._ctx, ctypes.byref(info))
         d = {k: int(getattr(info, k)) for k, _ in info._fields_}
         d["kernel_name"] = _lib.lib().rt_kernel_name(d["kernel"]).decode()
+        d["submit"] = {1: "hip", 2: "aql"}.get(d["submit"], "none")
+        if d["submit"] == "aql" and d["kernel_name"].startswith("rt_single_kernel"):
+            # the AQL path dispatches the chain instances of the same kernel
+            d["kernel_name"] = d["kernel_name"].replace("rt_single_kernel", "rt_chain_kernel")
         return d
 
     def candidate_stats(self) -> dict:

@@ -158,7 +158,7 @@ typedef struct rt_ctx rt_ctx;
 
 /* Version / introspection ------------------------------------------------------------ */
 RT_API uint32_t rt_abi_version(void); /* RT_ABI_VERSION */
-#define RT_ABI_VERSION 2u
+#define RT_ABI_VERSION 3u
 /* Text of the last error on this thread (never NULL). */
 RT_API const char* rt_last_error(void);
 /* Trace-kernel instances (rt_launch_info.kernel) and their names as rocprofv3 lists them
@@ -186,14 +186,16 @@ RT_API const char* rt_last_error(void);
 RT_API const char* rt_kernel_name(int which);
 /* What the last rt_update / rt_render / rt_render_stripes / rt_update_frames call on this
  * context launched: trace launches, frames traced, the most frames one launch carried, the
- * instance of its last launch (RT_KERNEL_*, -1 before any launch) and the concurrent parts
- * (streams) its last frame ran as (rt_set_update_queues; each part is one launch). */
+ * instance of its last launch (RT_KERNEL_*, -1 before any launch), the concurrent parts
+ * (streams or queues) its last frame ran as (rt_set_update_queues; each part is one launch)
+ * and how its last launch was submitted (RT_SUBMIT_HIP or RT_SUBMIT_AQL). */
 typedef struct rt_launch_info {
     uint32_t launches;
     uint32_t frames;
     uint32_t max_frames_per_launch;
     int32_t kernel;
     uint32_t queues;
+    uint32_t submit;
 } rt_launch_info;
 RT_API rt_status rt_last_launch_info(const rt_ctx* ctx, rt_launch_info* out);
 /* Diagnostic: the per-tile candidate lists of camera rays the context built last (culled
@@ -306,6 +308,36 @@ RT_API rt_status rt_set_tile_order(rt_ctx* ctx, int mode);
  * launch per update, at most RT_MAX_UPDATE_QUEUES.  Pixel results are identical. */
 #define RT_MAX_UPDATE_QUEUES 4u
 RT_API rt_status rt_set_update_queues(rt_ctx* ctx, uint32_t queues);
+/* How rt_update_frames submits one-frame updates when a call carries two or more of them.
+ *   RT_SUBMIT_HIP   HIP launches on the caller's stream (and the context's extra streams for
+ *                   concurrent parts).
+ *   RT_SUBMIT_AQL   every frame of every part is an AQL dispatch packet on an HSA queue the
+ *                   context owns (one queue per part, frames in order on it), written by the
+ *                   library (≈0.25 µs of host time per frame and part against 3-4 µs per HIP
+ *                   launch) with no cache fence between a part's frames (the chain kernels
+ *                   hand the image over through write-through stores and L1-bypassing
+ *                   loads); ordered after the work issued on the caller's stream before the
+ *                   call and before the work issued after it (when the stream is busy it
+ *                   writes a value a one-wave kernel on the queues waits for; the stream
+ *                   waits for a value the queues' last packet writes), so the call stays
+ *                   asynchronous.  Measured slower than HIP at every size on MI355X / ROCm
+ *                   7.2 (K3 per update 23.5 / 20.4 µs at 1 / 2 parts against 22.3 / 19.5,
+ *                   an 8-rank share 7.1 against 5.3 µs: the packets' arguments live in host
+ *                   memory, which each frame's first waves read over PCIe; four HSA queues
+ *                   beside HIP's are oversubscribed, 38.7 µs), so it is opt-in.
+ *   RT_SUBMIT_AUTO  (default) = RT_SUBMIT_HIP.
+ * Parts under AQL (rt_set_update_queues 0): 2 for launches of 2 000 tiles or more, else 1.
+ * Pixel results are identical in every mode. */
+#define RT_SUBMIT_AUTO 0
+#define RT_SUBMIT_HIP 1
+#define RT_SUBMIT_AQL 2
+RT_API rt_status rt_set_update_submit(rt_ctx* ctx, int mode);
+/* Whether AQL submission is available on the context's device (*aql_available; if not,
+ * rt_last_error() says why), the go waits that gave up so far (*go_give_ups: a chain whose
+ * caller's stream had not reached it after 10 s ran early; 0 in a correct run) and the AQL
+ * packets submitted so far.  Synchronous: waits for the context's AQL work in flight. */
+RT_API rt_status rt_update_submit_status(rt_ctx* ctx, int* aql_available, uint32_t* go_give_ups,
+                                         uint64_t* packets);
 /* Bounce paths (max_depth >= 2): RT_PATHS_PER_WAVE keeps every path in the wave of its
  * pixel (one tile per workgroup); RT_PATHS_PAIR runs two waves per tile on alternate
  * frames, the second handing its colours to the first through LDS (shorter chains for

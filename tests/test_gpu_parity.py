@@ -156,17 +156,20 @@ def test_bench_k4_launches_match_golden(rt, pairs):
 
 @pytest.mark.parametrize("single", ["auto", "one", "off"])
 @pytest.mark.parametrize("cfg", ["k2", "k3"])
-def test_bench_dispatch_chain_matches_fixture(rt, cfg, single):
+@pytest.mark.parametrize("submit", ["auto", "aql"])
+def test_bench_dispatch_chain_matches_fixture(rt, cfg, single, submit):
     """bench.py --config K2/K3's timed structure: one update launch per frame
     (rt_set_frames_per_launch(1)), 5 + 20 frames from a reset at 1920x1080 (the driver's
-    --warmup 5 --steps 20), checked against the oracle's sampled pixels
-    (tests/golden/bench_k*.npz)."""
+    --warmup 5 --steps 20), submitted as HIP launches (auto) or AQL packets, checked against
+    the oracle's sampled pixels (tests/golden/bench_k*.npz)."""
     g = load_golden(f"bench_{cfg}.npz")
     w, h = int(g["width"]), int(g["height"])
     cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
     p = rt.ComputeShaderPipeline(0)
     p.set_frames_per_launch(1)
     p.set_single_kernel(single)
+    p.set_update_submit(submit)
+    aql = submit == "aql" and single != "off"
     try:
         a, b = p.new_image(w, h), p.new_image(w, h)
         n0 = p.update_frames(a, b, w, h, cam, sc, g["seeds"][:5])
@@ -175,11 +178,14 @@ def test_bench_dispatch_chain_matches_fixture(rt, cfg, single):
         newest = p.update_frames(a, b, w, h, cam.with_fields(camera_has_moved=0.0), sc,
                                  g["seeds"][5:25])
         info = p.last_launch_info()
-        # (the library's choice of concurrent parts per update: 2 at this size)
+        # (the library's choice of concurrent parts per update at this size: 2 streams or
+        # queues)
         assert info["launches"] == 20 * info["queues"] and info["max_frames_per_launch"] == 1
         assert info["queues"] == (1 if single == "off" else 2)
-        assert info["kernel_name"] == {"off": "rt_trace_kernel<2>", "one": "rt_single_kernel<1>",
-                                       "auto": "rt_single_kernel<2>"}[single]
+        assert info["submit"] == ("aql" if aql else "hip")
+        name = {"off": "rt_trace_kernel<2>", "one": "rt_single_kernel<1>",
+                "auto": "rt_single_kernel<2>"}[single]
+        assert info["kernel_name"] == (name.replace("single", "chain") if aql else name)
         img = host(b if newest == 1 else a)
         k = list(g["frame_counts"]).index(25)
         assert_same(img[g["py"], g["px"]], g["pixels"][k])
@@ -189,9 +195,10 @@ def test_bench_dispatch_chain_matches_fixture(rt, cfg, single):
 
 @pytest.mark.parametrize("order", ["auto", "off"])
 @pytest.mark.parametrize("single", ["auto", "one"])
-def test_update_queues_match_one_launch(rt, single, order):
+@pytest.mark.parametrize("submit", ["auto", "aql"])
+def test_update_queues_match_one_launch(rt, single, order, submit):
     """rt_set_update_queues: one-frame updates as 2-4 concurrent parts on their own streams
-    (each part every queues-th workgroup of the cost order, or every queues-th band when
+    or HSA queues (rt_set_update_submit; each part every queues-th workgroup of the cost order, or every queues-th band when
     the order is off) leave both ping-pong images bit-identical to one launch per update —
     whole image and a rank share, across the reset frame, the order's first build and a
     second call — and match the oracle's sampled pixels (tests/golden/bench_k3.npz)."""
@@ -203,6 +210,7 @@ def test_update_queues_match_one_launch(rt, single, order):
     p.set_frames_per_launch(1)
     p.set_single_kernel(single)
     p.set_tile_order(order)
+    p.set_update_submit(submit)
     try:
         for rank, nranks in ((0, 1), (3, 8)):
             rows = rt.stripe_local_rows(h, rank, nranks)
@@ -225,6 +233,57 @@ def test_update_queues_match_one_launch(rt, single, order):
                 else:
                     for x, y in zip(imgs, ref):
                         assert_same(x, y)
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("single", ["auto", "one"])
+def test_update_submit_aql_matches_hip(rt, single):
+    """rt_set_update_submit: one-frame updates as AQL packets on the context's HSA queues
+    (1-4 parts, one queue each, no cache fence between a part's frames) leave both ping-pong
+    images bit-identical to HIP launches — whole image and a rank share, across the reset
+    frame, the workgroup order's first build and a second call; the first call starts on an
+    idle stream (no go packet), the second is issued while the stream still waits for the
+    first (the go packet path) — and match the oracle's sampled pixels; no go wait gave up."""
+    g = load_golden("bench_k3.npz")
+    w, h = int(g["width"]), int(g["height"])
+    cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
+    cam_t = cam.with_fields(camera_has_moved=0.0)
+    p = rt.ComputeShaderPipeline(0)
+    st = p.submit_status()
+    assert st["aql_available"], st["why"]
+    p.set_frames_per_launch(1)
+    p.set_single_kernel(single)
+    try:
+        for rank, nranks in ((0, 1), (5, 8)):
+            rows = rt.stripe_local_rows(h, rank, nranks)
+            ref = None
+            for mode, q in (("hip", 1), ("aql", 1), ("aql", 2), ("aql", 3), ("aql", 4),
+                            ("aql", 0), ("auto", 0)):
+                p.set_update_submit(mode)
+                p.set_update_queues(q)
+                a, b = p.new_image(w, rows), p.new_image(w, rows)
+                torch.cuda.synchronize()
+                n0 = p.update_frames(a, b, w, h, cam, sc, g["seeds"][:5], rank, nranks)
+                if n0 == 1:
+                    a, b = b, a
+                newest = p.update_frames(a, b, w, h, cam_t, sc, g["seeds"][5:25], rank, nranks)
+                info = p.last_launch_info()
+                want = "hip" if mode == "auto" else mode
+                assert info["submit"] == want and info["frames"] == 20, (mode, q, info)
+                if q:
+                    assert info["queues"] == q, (mode, q, info)
+                imgs = (host(b if newest == 1 else a), host(a if newest == 1 else b))
+                if ref is None:
+                    ref = imgs
+                    if nranks == 1:
+                        k = list(g["frame_counts"]).index(25)
+                        assert_same(imgs[0][g["py"], g["px"]], g["pixels"][k])
+                else:
+                    for x, y in zip(imgs, ref):
+                        assert_same(x, y)
+        st = p.submit_status()
+        assert st["go_give_ups"] == 0 and st["packets"] > 0, st
     finally:
         p.close()
 

@@ -1,7 +1,7 @@
 """Per-rank frame time of the stripe partition on ONE GPU (diagnostic, not the bench): times
 rank 0's share of a W x H progressive render for world sizes 1, 2, 4, 8, i.e. what each rank
 of `bench.py --gpus N` computes per step, to predict strong-scaling efficiency without an
-8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] [RT_QUEUES=q] [RT_REPS=r] [RT_PATHS=auto|per_wave|pair|compact] python tools/rank_sim.py [K3|K2|K5] [steps]"""
+8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] [RT_QUEUES=q] [RT_SUBMIT=auto|hip|aql] [RT_REPS=r] [RT_PATHS=auto|per_wave|pair|compact] python tools/rank_sim.py [K3|K2|K5] [steps]"""
 import json
 import os
 import sys
@@ -38,6 +38,8 @@ def main(cfg="K3", steps=50):
         pipe.set_tile_order(os.environ.get("RT_TILE_ORDER", "auto"))
     if hasattr(rt._lib.lib(), "rt_set_update_queues"):
         pipe.set_update_queues(int(os.environ.get("RT_QUEUES", "0")))
+    if hasattr(rt._lib.lib(), "rt_set_update_submit"):
+        pipe.set_update_submit(os.environ.get("RT_SUBMIT", "auto"))
     base = None
     for world in (1, 2, 4, 8):
         r = StripeRenderer(pipe, w, h, 0, world)
@@ -65,7 +67,8 @@ def main(cfg="K3", steps=50):
                           "predicted_efficiency": round(base / world / us, 3),
                           "host_issue_us_per_step": round(host_us, 2),
                           "runs_us": [round(x, 2) for x in runs],
-                          "queues": pipe.last_launch_info().get("queues")}), flush=True)
+                          "queues": pipe.last_launch_info().get("queues"),
+                          "submit": pipe.last_launch_info().get("submit")}), flush=True)
     pipe.close()
 
 
