@@ -131,8 +131,10 @@ __device__ __forceinline__ unsigned long long rt_ballot(bool x) {
     return __builtin_amdgcn_ballot_w64(x);
 }
 // the one-frame kernel (and normalize_w)'s wave-uniform decisions from lane masks (mask_*) instead of ballots
+// (default since round 3 with RT_SINGLE_DISK 3 and RT_ORIGIN_VGPR 1: K3 19.5-19.8 -> 18.9-19.1 µs,
+// K2 13.6-13.8 -> 13.4 µs per update, profiles/r03t_ab_single_masks_all.log)
 #ifndef RT_SINGLE_MASKS
-#define RT_SINGLE_MASKS 0
+#define RT_SINGLE_MASKS 1
 #endif
 // Lane masks straight from one compare (llvm.amdgcn.icmp / fcmp: the v_cmp's SGPR result),
 // combined with & and | as 64-bit scalars.  A ballot of a boolean that crosses blocks or
@@ -317,7 +319,7 @@ constexpr int kTraceDisk = RT_TRACE_DISK;
 // get_ray: the lens centre copied to VGPRs before the defocus branch (1) or left to the
 // compiler (0)
 #ifndef RT_ORIGIN_VGPR
-#define RT_ORIGIN_VGPR 0
+#define RT_ORIGIN_VGPR 1
 #endif
 
 // Scan records are read through the constant address space: they do not change during a
@@ -1497,11 +1499,14 @@ constexpr uint32_t kSingleWg = RT_SINGLE_WG;
 #endif
 // The defocus disk's reciprocal in the one-frame kernel: 1 = the workgroup's LDS table
 // (filled by wave 0 from the launch parameters, one barrier), 2 = its closed form in
-// registers (disk_rcp_reg: no table, no barrier).  2 (default): K3 23.30 -> 22.46 us, K2
-// 17.13 -> 16.0 us per update, 8-rank K3 share 6.26 -> 5.52 us (profiles/r03a_ab_single.log):
-// the barrier made every wave of a workgroup wait for wave 0's kernarg read at wave start.
+// registers (disk_rcp_reg: no table, no barrier), 3 = all-f32 (disk_unit<3>: the length and
+// its reciprocal from the bits of len2, one Markstein step; no f64).  2 over 1: K3 23.30 ->
+// 22.46 us, K2 17.13 -> 16.0 us per update, 8-rank K3 share 6.26 -> 5.52 us
+// (profiles/r03a_ab_single.log): the barrier made every wave of a workgroup wait for wave 0's
+// kernarg read at wave start.  3 (default since round 3, with RT_SINGLE_MASKS and
+// RT_ORIGIN_VGPR): profiles/r03t_ab_single_masks_all.log.
 #ifndef RT_SINGLE_DISK
-#define RT_SINGLE_DISK 2
+#define RT_SINGLE_DISK 3
 #endif
 constexpr int kSingleDisk = RT_SINGLE_DISK;
 // hash(x*73) ^ hash(y*51) (wgsl:309-310) of the one-frame kernel: from the per-column /
