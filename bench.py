@@ -98,6 +98,11 @@ def parse():
                     choices=["auto", "hip", "aql"],
                     help="how one-frame updates are submitted (rt_set_update_submit): HIP "
                          "launches (auto) or AQL packets on the context's HSA queues")
+    ap.add_argument("--warm-ms", type=float, default=float(os.environ.get("RT_WARM_MS", "50")),
+                    help="before the warmup steps, keep the GPU busy this long with the same "
+                         "update frames on scratch images (untimed; the clock the chip "
+                         "settles at under this load, not the idle clock, is what a step "
+                         "of a running render sees; 0 = off)")
     ap.add_argument("--scan", default="culled", choices=["culled", "exhaustive"],
                     help="sphere-list scan: exact culling (default) or the reference's "
                          "exhaustive linear walk; images are bit-identical")
@@ -297,6 +302,21 @@ def main():
             for _ in range(n):
                 r.frames(cam0, spheres, seeds)
 
+    # Clock warm-up (untimed, scratch images): a progressive render's steps run back to back
+    # on a chip that has long left its idle clock; a 20-step timed region (~0.4 ms) right
+    # after process start would otherwise time the clock ramp (K3: 22.2 against 16.2 µs per
+    # update, profiles/r03w_driver_warm.log).  The same frames on separate images: the timed
+    # images, their counts and the fixture check are untouched.
+    warm_s = 0.0
+    if args.warm_ms > 0:
+        scratch = StripeRenderer(pipe, w, h, rank, world, comm=None)
+        torch.cuda.synchronize()
+        t_w = time.perf_counter()
+        while time.perf_counter() - t_w < args.warm_ms / 1e3:
+            scratch.frames(cam0, spheres, seeds[:20] if dispatch else seeds)
+            torch.cuda.synchronize()
+        warm_s = time.perf_counter() - t_w
+        del scratch
     # warmup (untimed); the dispatch configs' frame 0 resets the accumulator
     if args.warmup:
         step_block(args.warmup, True)
@@ -425,6 +445,10 @@ def main():
                 "Mrays_per_s": round(w * h * spf * args.steps / (dt + dt_gather) / 1e6, 2),
                 "what": "the K steps plus the one gather of the finished tiles"},
         "candidate_lists": cand_stats,
+        "warm_up": {"ms": round(warm_s * 1e3, 2), "steps": args.warmup,
+                    "what": "untimed update frames on scratch images before the warmup steps "
+                            "(--warm-ms), so the timed steps run at the clock a running "
+                            "render holds"},
     }
 
     # ---- side measurements (after the timed region and its image check) -------------

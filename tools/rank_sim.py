@@ -1,7 +1,7 @@
 """Per-rank frame time of the stripe partition on ONE GPU (diagnostic, not the bench): times
 rank 0's share of a W x H progressive render for world sizes 1, 2, 4, 8, i.e. what each rank
 of `bench.py --gpus N` computes per step, to predict strong-scaling efficiency without an
-8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] [RT_QUEUES=q] [RT_SUBMIT=auto|hip|aql] [RT_REPS=r] [RT_PATHS=auto|per_wave|pair|compact] python tools/rank_sim.py [K3|K2|K5] [steps]"""
+8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] [RT_QUEUES=q] [RT_SUBMIT=auto|hip|aql] [RT_REPS=r] [RT_WARM_MS=50] [RT_PATHS=auto|per_wave|pair|compact] python tools/rank_sim.py [K3|K2|K5] [steps]"""
 import json
 import os
 import sys
@@ -40,6 +40,14 @@ def main(cfg="K3", steps=50):
         pipe.set_update_queues(int(os.environ.get("RT_QUEUES", "0")))
     if hasattr(rt._lib.lib(), "rt_set_update_submit"):
         pipe.set_update_submit(os.environ.get("RT_SUBMIT", "auto"))
+    # untimed clock warm-up (as bench.py --warm-ms): the whole image for RT_WARM_MS ms
+    warm = StripeRenderer(pipe, w, h, 0, 1)
+    torch.cuda.synchronize()
+    t_w = time.perf_counter()
+    while time.perf_counter() - t_w < float(os.environ.get("RT_WARM_MS", "50")) / 1e3:
+        warm.frames(cam, sc, seeds[:20])
+        torch.cuda.synchronize()
+    del warm
     base = None
     for world in (1, 2, 4, 8):
         r = StripeRenderer(pipe, w, h, 0, world)
