@@ -36,6 +36,8 @@
 #include <hsa/hsa_ext_amd.h>
 #include <hsa/hsa_ven_amd_loader.h>
 
+#include <immintrin.h>
+
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -53,6 +55,11 @@ constexpr uint32_t kMaxQueues = 4;
 constexpr uint32_t kQueuePackets = 1024;      // per queue (power of two)
 constexpr uint32_t kSlotBytes = 512;          // kernel arguments per packet (>= chain_args)
 constexpr uint32_t kSets = 4;                 // segments in flight (signals, argument buffers)
+// VRAM argument ring: a slot is rewritten only after ~kRingSlots other packets (at most kSets
+// segments of at most kMaxSegmentPackets each are in flight), so no cache can still hold the
+// line it read last time; each queue's first packet of a segment acquires at system scope too.
+constexpr uint32_t kRingSlots = 65536;
+static_assert(kSets * kMaxSegmentPackets * 8 <= kRingSlots, "argument ring");
 
 struct KernelObj {
     uint64_t object = 0;
@@ -82,6 +89,12 @@ struct Chain {
     hsa_queue_t* q[kMaxQueues] = {};
     KernelObj k[rtk::kChainKernels];
     unsigned char* small = nullptr;        // host kernarg pool, 2 slots per set
+    // frame packets' arguments: a ring in VRAM the host writes through its large-BAR mapping
+    // (one HDP flush + read-back per segment), or per-set non-coherent host buffers
+    unsigned char* ring = nullptr;
+    uint32_t ring_head = 0;
+    uint32_t* hdp_flush = nullptr;
+    unsigned char* seg_args = nullptr;     // the open segment's first slot
     SignalSet sets[kSets];
     uint32_t set = 0;                      // set of the open / next segment
     uint32_t* go = nullptr;                // signal memory: the caller's stream writes seq
@@ -155,6 +168,23 @@ hsa_status_t sym_cb(hsa_executable_t, hsa_agent_t, hsa_executable_symbol_t s, vo
 hsa_status_t exec_cb(hsa_executable_t e, void* d) {
     FindSyms* f = static_cast<FindSyms*>(d);
     hsa_executable_iterate_agent_symbols(e, f->agent, sym_cb, d);
+    return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t vram_pool_cb(hsa_amd_memory_pool_t pool, void* d) {
+    hsa_amd_segment_t seg;
+    if (hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) !=
+            HSA_STATUS_SUCCESS ||
+        seg != HSA_AMD_SEGMENT_GLOBAL)
+        return HSA_STATUS_SUCCESS;
+    uint32_t flags = 0;
+    bool alloc = false;
+    hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+    hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc);
+    if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) && alloc) {
+        *static_cast<hsa_amd_memory_pool_t*>(d) = pool;
+        return HSA_STATUS_INFO_BREAK;
+    }
     return HSA_STATUS_SUCCESS;
 }
 
@@ -294,14 +324,36 @@ rt_status setup(Chain* c) {
         c->why = "kernarg memory not accessible by the GPU";
         return RT_OK;
     }
-    for (uint32_t i = 0; i < kSets; ++i) {
-        SignalSet& s = c->sets[i];
-        s.small = c->small + (size_t)i * 2 * kSlotBytes;
-        const size_t bytes = (size_t)rtc::kMaxSegmentPackets * kSlotBytes;
-        he = hipHostMalloc(reinterpret_cast<void**>(&s.args), bytes, hipHostMallocNonCoherent);
-        if (he != hipSuccess) return rti::hip_fail(he, "chain argument buffers");
-        s.frames.reserve(rtc::kMaxSegmentPackets);
+    for (uint32_t i = 0; i < kSets; ++i) c->sets[i].small = c->small + (size_t)i * 2 * kSlotBytes;
+    // the argument ring in VRAM, host-visible (large BAR) and flushed through the HDP
+    hsa_amd_memory_pool_t vpool{};
+    hsa_amd_hdp_flush_t hdp{};
+    void* ring = nullptr;
+    if (hsa_amd_agent_iterate_memory_pools(c->gpu, vram_pool_cb, &vpool) == HSA_STATUS_INFO_BREAK &&
+        hsa_agent_get_info(c->gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &hdp) ==
+            HSA_STATUS_SUCCESS &&
+        hdp.HDP_MEM_FLUSH_CNTL &&
+        hsa_amd_memory_pool_allocate(vpool, (size_t)kRingSlots * kSlotBytes, 0, &ring) ==
+            HSA_STATUS_SUCCESS) {
+        hsa_amd_pointer_info_t info;
+        std::memset(&info, 0, sizeof(info));
+        info.size = sizeof(info);
+        if (hsa_amd_agents_allow_access(1, &c->cpu, nullptr, ring) == HSA_STATUS_SUCCESS &&
+            hsa_amd_pointer_info(ring, &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS &&
+            info.hostBaseAddress == ring) {
+            c->ring = static_cast<unsigned char*>(ring);
+            c->hdp_flush = hdp.HDP_MEM_FLUSH_CNTL;
+        } else {
+            hsa_amd_memory_pool_free(ring);
+        }
     }
+    for (uint32_t i = 0; i < kSets && !c->ring; ++i) {
+        const size_t bytes = (size_t)rtc::kMaxSegmentPackets * kSlotBytes;
+        he = hipHostMalloc(reinterpret_cast<void**>(&c->sets[i].args), bytes,
+                           hipHostMallocNonCoherent);
+        if (he != hipSuccess) return rti::hip_fail(he, "chain argument buffers");
+    }
+    for (SignalSet& s : c->sets) s.frames.reserve(rtc::kMaxSegmentPackets);
     for (SignalSet& s : c->sets) {
         bool ok = hsa_signal_create(0, 0, nullptr, &s.go) == HSA_STATUS_SUCCESS &&
                   hsa_signal_create(0, 0, nullptr, &s.done) == HSA_STATUS_SUCCESS;
@@ -362,6 +414,7 @@ void chain_destroy(Chain* c) {
             if (t.handle) hsa_signal_destroy(t);
     }
     for (SignalSet& s : c->sets) (void)hipHostFree(s.args);
+    if (c->ring) hsa_amd_memory_pool_free(c->ring);
     if (c->small) hsa_amd_memory_pool_free(c->small);
     (void)hipFree(c->go);
     (void)hipFree(c->done);
@@ -381,6 +434,12 @@ rt_status chain_begin(Chain* c, hipStream_t stream, uint32_t parts) {
     SignalSet& s = c->sets[c->set];
     if (s.used) wait_zero(s.done);    // this set's previous segment (and its buffers) is done
     s.frames.clear();
+    if (c->ring) {
+        if (c->ring_head + kMaxSegmentPackets > kRingSlots) c->ring_head = 0;
+        c->seg_args = c->ring + (size_t)c->ring_head * kSlotBytes;
+    } else {
+        c->seg_args = s.args;
+    }
     c->open = true;
     c->seg_parts = parts;
     return RT_OK;
@@ -391,7 +450,7 @@ rt_status chain_frame(Chain* c, const rtk::TraceParams& p, int kernel, uint32_t 
     SignalSet& s = c->sets[c->set];
     if (s.frames.size() >= kMaxSegmentPackets)
         return rti::fail(RT_ERR_INVALID_ARGUMENT, "chain segment too long");
-    unsigned char* a = s.args + s.frames.size() * kSlotBytes;
+    unsigned char* a = c->seg_args + s.frames.size() * kSlotBytes;
     uint32_t grid[2] = {0, 0}, threads = 0;
     int which = 0;
     const uint32_t n = rtk::chain_args(p, kernel, a, kSlotBytes, grid, &threads, &which);
@@ -407,6 +466,16 @@ rt_status chain_end(Chain* c, hipStream_t stream) {
     SignalSet& s = c->sets[c->set];
     if (s.frames.empty()) return RT_OK;
     c->set = (c->set + 1u) % kSets;
+    if (c->ring) {
+        // the arguments written through the BAR reach VRAM before any packet is published:
+        // drain the write-combining buffers, flush the HDP, read back (MI355X: 2.4 µs)
+        c->ring_head += (uint32_t)s.frames.size();
+        _mm_sfence();
+        *c->hdp_flush = 1u;
+        (void)*reinterpret_cast<volatile uint32_t*>(c->hdp_flush);
+        (void)*reinterpret_cast<volatile uint32_t*>(c->seg_args +
+                                                     (s.frames.size() - 1) * kSlotBytes);
+    }
     s.used = true;
     const uint32_t seq = ++c->seq;
     const uint32_t parts = c->seg_parts;
@@ -438,7 +507,7 @@ rt_status chain_end(Chain* c, hipStream_t stream) {
     for (uint32_t k = 0; k < kMaxQueues; ++k) first[k] = true;
     for (size_t i = 0; i < s.frames.size(); ++i) {
         const Pending& f = s.frames[i];
-        dispatch(c, f.part, c->k[f.which], s.args + i * kSlotBytes, f.gx, f.gy, f.threads,
+        dispatch(c, f.part, c->k[f.which], c->seg_args + i * kSlotBytes, f.gx, f.gy, f.threads,
                  first[f.part] ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_NONE,
                  HSA_FENCE_SCOPE_NONE, hsa_signal_t{0});
         first[f.part] = false;

@@ -320,11 +320,11 @@ RT_API rt_status rt_set_update_queues(rt_ctx* ctx, uint32_t queues);
  *                   call and before the work issued after it (when the stream is busy it
  *                   writes a value a one-wave kernel on the queues waits for; the stream
  *                   waits for a value the queues' last packet writes), so the call stays
- *                   asynchronous.  Measured slower than HIP at every size on MI355X / ROCm
- *                   7.2 (K3 per update 23.5 / 20.4 µs at 1 / 2 parts against 22.3 / 19.5,
- *                   an 8-rank share 7.1 against 5.3 µs: the packets' arguments live in host
- *                   memory, which each frame's first waves read over PCIe; four HSA queues
- *                   beside HIP's are oversubscribed, 38.7 µs), so it is opt-in.
+ *                   asynchronous.  The packets' arguments live in VRAM written through the
+ *                   host's large-BAR mapping (one HDP flush per call), else in host memory.
+ *                   Measured at parity with HIP launches, not faster (K3 15.2-15.3 µs per
+ *                   update at 2 queues against 14.9-15.0; an 8-rank share 5.6 against 5.1;
+ *                   four HSA queues beside HIP's are oversubscribed), so it is opt-in.
  *   RT_SUBMIT_AUTO  (default) = RT_SUBMIT_HIP.
  * Parts under AQL (rt_set_update_queues 0): 2 for launches of 2 000 tiles or more, else 1.
  * Pixel results are identical in every mode. */
