@@ -375,13 +375,12 @@ rt_status setup(Chain* c) {
     if (he == hipSuccess) he = hipMemset(c->done, 0, 8);
     if (he == hipSuccess) he = hipDeviceSynchronize();
     if (he != hipSuccess) return rti::hip_fail(he, "chain words");
-    for (uint32_t i = 0; i < kMaxQueues; ++i) {
-        if (hsa_queue_create(c->gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
-                             UINT32_MAX, UINT32_MAX, &c->q[i]) != HSA_STATUS_SUCCESS) {
-            c->q[i] = nullptr;
-            c->why = "hsa_queue_create failed";
-            return RT_OK;
-        }
+    // (queues are created as segments need them: chain_begin)
+    if (hsa_queue_create(c->gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
+                         UINT32_MAX, UINT32_MAX, &c->q[0]) != HSA_STATUS_SUCCESS) {
+        c->q[0] = nullptr;
+        c->why = "hsa_queue_create failed";
+        return RT_OK;
     }
     c->why = "";
     c->ok = true;
@@ -431,6 +430,16 @@ rt_status chain_begin(Chain* c, hipStream_t stream, uint32_t parts) {
     (void)stream;
     if (!c->ok || c->open) return rti::fail(RT_ERR_INVALID_ARGUMENT, "chain_begin");
     parts = parts < 1u ? 1u : parts > kMaxQueues ? kMaxQueues : parts;
+    // one HSA queue per part, created on first use (idle queues still occupy the device's
+    // hardware queue slots, which HIP's own streams share)
+    for (uint32_t k = 1; k < parts; ++k) {
+        if (c->q[k]) continue;
+        if (hsa_queue_create(c->gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
+                             UINT32_MAX, UINT32_MAX, &c->q[k]) != HSA_STATUS_SUCCESS) {
+            c->q[k] = nullptr;
+            return rti::fail(RT_ERR_HIP, "hsa_queue_create failed");
+        }
+    }
     SignalSet& s = c->sets[c->set];
     if (s.used) wait_zero(s.done);    // this set's previous segment (and its buffers) is done
     s.frames.clear();
