@@ -99,10 +99,10 @@ def parse():
                     help="how one-frame updates are submitted (rt_set_update_submit): HIP "
                          "launches (auto) or AQL packets on the context's HSA queues")
     ap.add_argument("--warm-ms", type=float, default=float(os.environ.get("RT_WARM_MS", "50")),
-                    help="before the warmup steps, keep the GPU busy this long with the same "
-                         "update frames on scratch images (untimed; the clock the chip "
-                         "settles at under this load, not the idle clock, is what a step "
-                         "of a running render sees; 0 = off)")
+                    help="before the warmup steps, render this long with the same update "
+                         "frames on scratch images (untimed: a running render's steps, not a "
+                         "freshly started process's first launches, are what is timed; 0 = "
+                         "off)")
     ap.add_argument("--scan", default="culled", choices=["culled", "exhaustive"],
                     help="sphere-list scan: exact culling (default) or the reference's "
                          "exhaustive linear walk; images are bit-identical")
@@ -302,11 +302,13 @@ def main():
             for _ in range(n):
                 r.frames(cam0, spheres, seeds)
 
-    # Clock warm-up (untimed, scratch images): a progressive render's steps run back to back
-    # on a chip that has long left its idle clock; a 20-step timed region (~0.4 ms) right
-    # after process start would otherwise time the clock ramp (K3: 22.2 against 16.2 µs per
-    # update, profiles/r03w_driver_warm.log).  The same frames on separate images: the timed
-    # images, their counts and the fixture check are untouched.
+    # Warm-up (untimed, scratch images): a progressive render's steps run back to back in a
+    # process that has long been issuing them; a 20-step timed region (~0.4 ms) right after
+    # process start would otherwise time the start-up (K3: 22.2 against 16.2 µs per update,
+    # profiles/r03w_driver_warm.log; the launches themselves run the same, the in-kernel
+    # clock reads 1.83 GHz cold and 1.88 warm, profiles/r03zb_stamps_single_k3_*.jsonl).  The
+    # same frames on separate images: the timed images, their counts and the fixture check
+    # are untouched.
     warm_s = 0.0
     if args.warm_ms > 0:
         scratch = StripeRenderer(pipe, w, h, rank, world, comm=None)
@@ -447,8 +449,8 @@ def main():
         "candidate_lists": cand_stats,
         "warm_up": {"ms": round(warm_s * 1e3, 2), "steps": args.warmup,
                     "what": "untimed update frames on scratch images before the warmup steps "
-                            "(--warm-ms), so the timed steps run at the clock a running "
-                            "render holds"},
+                            "(--warm-ms): the timed steps are a running render's, not a "
+                            "freshly started process's first launches"},
     }
 
     # ---- side measurements (after the timed region and its image check) -------------

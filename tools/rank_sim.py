@@ -40,7 +40,7 @@ def main(cfg="K3", steps=50):
         pipe.set_update_queues(int(os.environ.get("RT_QUEUES", "0")))
     if hasattr(rt._lib.lib(), "rt_set_update_submit"):
         pipe.set_update_submit(os.environ.get("RT_SUBMIT", "auto"))
-    # untimed clock warm-up (as bench.py --warm-ms): the whole image for RT_WARM_MS ms
+    # untimed warm-up (as bench.py --warm-ms): the whole image for RT_WARM_MS ms
     warm = StripeRenderer(pipe, w, h, 0, 1)
     torch.cuda.synchronize()
     t_w = time.perf_counter()

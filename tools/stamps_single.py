@@ -5,10 +5,14 @@ available: entry -> order resolved -> seed tables + counts -> camera rays -> lis
 shading + sky -> accumulator consumed -> stores issued (rt_kernels.hip RT_SSTAMPS).  Prints,
 per scenario, the mean / p90 duration of each phase (us at the stamped clock), the wave
 lifetime, the launch span (s_memrealtime, per XCC), and the resident waves per SIMD.
-usage: RT_HIP_LIB=... python tools/stamps_single.py [K3|K2] [worlds, e.g. 1,8,135]"""
+Before each stamped launch the GPU is warmed with whole-image frames (RT_WARM_MS, default 50
+ms first, 5 ms between launches; 0 = cold, as before round 3's warm-up).
+usage: RT_HIP_LIB=... [RT_WARM_MS=50] python tools/stamps_single.py [K3|K2] [worlds, e.g. 1,8,135]"""
 import ctypes
 import json
+import os
 import sys
+import time
 from pathlib import Path
 
 import numpy as np
@@ -25,8 +29,21 @@ PHASES = ["order", "seeds+counts", "camera_ray", "list_walk", "shade+sky", "accu
 NW = 1 << 17
 
 
+def warm(pipe, cfg, cam, sc, seeds, ms):
+    """Untimed whole-image update frames for `ms` milliseconds (bench.py --warm-ms): the
+    stamped launch then runs at the clock a running render holds."""
+    w, h, *_ = CONF[cfg]
+    a, b = pipe.new_image(w, h), pipe.new_image(w, h)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < ms / 1e3:
+        pipe.update_frames(a, b, w, h, cam, sc, seeds[:20])
+        torch.cuda.synchronize()
+
+
 def scenario(pipe, L, buf, cfg, world, cam, sc, seeds, repeat=5):
     w, h, *_ = CONF[cfg]
+    warm_ms = float(os.environ.get("RT_WARM_MS", "50"))
     rows = rt.stripe_local_rows(h, 0, world)
     a, b = pipe.new_image(w, rows), pipe.new_image(w, rows)
     pipe.set_frames_per_launch(1)
@@ -35,6 +52,8 @@ def scenario(pipe, L, buf, cfg, world, cam, sc, seeds, repeat=5):
     pipe.update_frames(a, b, w, h, c2, sc, seeds[4:12], 0, world)
     out = []
     for r in range(repeat):
+        if warm_ms > 0:
+            warm(pipe, cfg, cam, sc, seeds, warm_ms if r == 0 else 5.0)
         torch.cuda.synchronize()
         assert L.rt_diag_single_stamps(buf, NW) == 0                 # clear
         pipe.update_frames(a, b, w, h, c2, sc, seeds[12 + r:13 + r], 0, world)
@@ -78,6 +97,9 @@ def main(cfg="K3", worlds="1,2,4,8,135"):
                                        w, h, float(seeds[0]))
     pipe = rt.ComputeShaderPipeline(0)
     pipe.set_spheres(sc)
+    # one launch per update: the stamps are indexed by the wave's place in its launch, and
+    # concurrent parts (rt_set_update_queues) would overwrite each other's
+    pipe.set_update_queues(1)
     L = rt._lib.lib()
     L.rt_diag_single_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint]
     buf = (ctypes.c_ulonglong * (12 * NW))()
