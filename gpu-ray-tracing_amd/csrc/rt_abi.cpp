@@ -909,12 +909,21 @@ void note_launch(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t fr
     ctx->last.kernel = kernel != rtk::kTraceBounce ? kernel : RT_KERNEL_BOUNCE + (int)p.compact;
 }
 
-// The context's AQL chain if one-frame updates go through it (rt_set_update_submit AQL):
-// created on first use; the call fails with the reason when the machine does not offer it.
-rt_status usable_chain(rt_ctx* ctx, rtc::Chain** out) {
+// The context's AQL chain if one-frame updates go through it (rt_set_update_submit AQL, or
+// AUTO for mid-sized launches): created on first use; AQL fails the call with the reason when
+// the machine does not offer it, AUTO falls back to HIP launches.
+// AUTO submits as AQL packets the launches of [kAqlAutoMinTiles, kAqlAutoMaxTiles) tiles —
+// mid-sized rank shares, where two queues of packets beat HIP launches (a 4-rank K3 share
+// 6.76 against 7.54-7.68 µs per update, profiles/r03zd_rank_sim_*.jsonl, two rounds; whole
+// images and 2-rank shares run alike either way, 8-rank shares faster as one HIP launch).
+constexpr uint64_t kAqlAutoMinTiles = 6000, kAqlAutoMaxTiles = 12000;
+rt_status usable_chain(rt_ctx* ctx, const rtk::TraceParams& p, rtc::Chain** out) {
     *out = nullptr;
-    // AUTO = HIP: AQL packets measured slower at every size (rt_abi.h rt_set_update_submit)
-    if (ctx->update_submit != RT_SUBMIT_AQL) return RT_OK;
+    if (ctx->update_submit == RT_SUBMIT_HIP) return RT_OK;
+    if (ctx->update_submit == RT_SUBMIT_AUTO) {
+        const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
+        if (tiles < kAqlAutoMinTiles || tiles >= kAqlAutoMaxTiles) return RT_OK;
+    }
     if (!ctx->chain_tried) {
         ctx->chain_tried = true;
         rt_status st = RT_OK;
@@ -1247,7 +1256,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
     // two or more of them (rt_set_update_submit; a single update gains nothing from it).
     rtc::Chain* chain = nullptr;
     if (per == 1u && frames >= 2u)
-        if (rt_status s = usable_chain(ctx, &chain)) return s;
+        if (rt_status s = usable_chain(ctx, p, &chain)) return s;
     bool seg_open = false;      // an AQL segment of this call is open
     uint32_t seg_parts = 0, seg_packets = 0;
     for (uint32_t f0 = 0; f0 < frames; f0 += per) {

@@ -85,9 +85,10 @@ class ComputeShaderPipeline:
         _lib.call("rt_set_update_queues", self._ctx, int(queues))
 
     def set_update_submit(self, mode: str) -> None:
-        """rt_set_update_submit: how update_frames submits one-frame updates — "hip" (HIP
-        launches; "auto" = hip) or "aql" (AQL packets on the context's own HSA queues, an
-        error if unavailable; measured slower, opt-in); identical pixels."""
+        """rt_set_update_submit: how update_frames submits one-frame updates — "auto" (AQL
+        packets for launches of 6 000 to 11 999 tiles, HIP launches otherwise), "hip" or
+        "aql" (AQL packets on the context's own HSA queues, an error if unavailable);
+        identical pixels."""
         _lib.call("rt_set_update_submit", self._ctx, {"auto": 0, "hip": 1, "aql": 2}[mode])
 
     def submit_status(self) -> dict:

@@ -322,10 +322,14 @@ RT_API rt_status rt_set_update_queues(rt_ctx* ctx, uint32_t queues);
  *                   waits for a value the queues' last packet writes), so the call stays
  *                   asynchronous.  The packets' arguments live in VRAM written through the
  *                   host's large-BAR mapping (one HDP flush per call), else in host memory.
- *                   Measured at parity with HIP launches, not faster (K3 15.2-15.3 µs per
- *                   update at 2 queues against 14.9-15.0; an 8-rank share 5.6 against 5.1;
- *                   four HSA queues beside HIP's are oversubscribed), so it is opt-in.
- *   RT_SUBMIT_AUTO  (default) = RT_SUBMIT_HIP.
+ *                   Measured at parity with HIP launches on whole images (K3 15.2-15.8 µs
+ *                   per update at 2 queues against 14.9-15.8), faster on mid-sized rank
+ *                   shares (a 4-rank K3 share 6.76 against 7.54-7.68 µs), slower on small
+ *                   ones (an 8-rank share 5.8 against 5.0); four HSA queues beside HIP's are
+ *                   oversubscribed.
+ *   RT_SUBMIT_AUTO  (default) AQL for launches of 6 000 to 11 999 tiles when the machine
+ *                   offers it (HSA queues, host-visible VRAM or host memory for the
+ *                   arguments, the code object's chain kernels), else HIP.
  * Parts under AQL (rt_set_update_queues 0): 2 for launches of 2 000 tiles or more, else 1.
  * Pixel results are identical in every mode. */
 #define RT_SUBMIT_AUTO 0

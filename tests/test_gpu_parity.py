@@ -244,7 +244,8 @@ def test_update_submit_aql_matches_hip(rt, single):
     images bit-identical to HIP launches — whole image and a rank share, across the reset
     frame, the workgroup order's first build and a second call; the first call starts on an
     idle stream (no go packet), the second is issued while the stream still waits for the
-    first (the go packet path) — and match the oracle's sampled pixels; no go wait gave up."""
+    first (the go packet path) — and match the oracle's sampled pixels; no go wait gave up.
+    AUTO picks AQL for the 4-rank share (6 000 to 11 999 tiles) and HIP for the others."""
     g = load_golden("bench_k3.npz")
     w, h = int(g["width"]), int(g["height"])
     cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
@@ -255,8 +256,9 @@ def test_update_submit_aql_matches_hip(rt, single):
     p.set_frames_per_launch(1)
     p.set_single_kernel(single)
     try:
-        for rank, nranks in ((0, 1), (5, 8)):
+        for rank, nranks in ((0, 1), (5, 8), (1, 4)):
             rows = rt.stripe_local_rows(h, rank, nranks)
+            tiles = ((w + 7) // 8) * ((rows + 7) // 8)
             ref = None
             for mode, q in (("hip", 1), ("aql", 1), ("aql", 2), ("aql", 3), ("aql", 4),
                             ("aql", 0), ("auto", 0)):
@@ -269,7 +271,7 @@ def test_update_submit_aql_matches_hip(rt, single):
                     a, b = b, a
                 newest = p.update_frames(a, b, w, h, cam_t, sc, g["seeds"][5:25], rank, nranks)
                 info = p.last_launch_info()
-                want = "hip" if mode == "auto" else mode
+                want = mode if mode != "auto" else ("aql" if 6000 <= tiles < 12000 else "hip")
                 assert info["submit"] == want and info["frames"] == 20, (mode, q, info)
                 if q:
                     assert info["queues"] == q, (mode, q, info)
