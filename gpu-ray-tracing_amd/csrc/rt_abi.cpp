@@ -924,19 +924,21 @@ rt_status usable_chain(rt_ctx* ctx, const rtk::TraceParams& p, rtc::Chain** out)
         const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
         if (tiles < kAqlAutoMinTiles || tiles >= kAqlAutoMaxTiles) return RT_OK;
     }
+    const bool aql = ctx->update_submit == RT_SUBMIT_AQL;
     if (!ctx->chain_tried) {
         ctx->chain_tried = true;
         rt_status st = RT_OK;
         ctx->chain = rtc::chain_create(ctx->device, &st);
-        if (st != RT_OK) return st;
+        // (AUTO: a chain that could not be set up leaves the call on HIP launches)
+        if (st != RT_OK && aql) return st;
     }
     const char* why = "";
-    if (rtc::chain_ok(ctx->chain, &why)) {
+    // AUTO also needs the queues of its parts up front: no failure once frames are packed
+    if (rtc::chain_ok(ctx->chain, &why) && (aql || rtc::chain_queues(ctx->chain, 2u))) {
         *out = ctx->chain;
         return RT_OK;
     }
-    if (ctx->update_submit == RT_SUBMIT_AQL)
-        return fail(RT_ERR_HIP, std::string("AQL submission unavailable: ") + why);
+    if (aql) return fail(RT_ERR_HIP, std::string("AQL submission unavailable: ") + why);
     return RT_OK;
 }
 

@@ -426,20 +426,26 @@ bool chain_ok(const Chain* c, const char** why) {
     return c && c->ok;
 }
 
-rt_status chain_begin(Chain* c, hipStream_t stream, uint32_t parts) {
-    (void)stream;
-    if (!c->ok || c->open) return rti::fail(RT_ERR_INVALID_ARGUMENT, "chain_begin");
-    parts = parts < 1u ? 1u : parts > kMaxQueues ? kMaxQueues : parts;
+bool chain_queues(Chain* c, uint32_t parts) {
     // one HSA queue per part, created on first use (idle queues still occupy the device's
     // hardware queue slots, which HIP's own streams share)
-    for (uint32_t k = 1; k < parts; ++k) {
+    if (!c || !c->ok) return false;
+    for (uint32_t k = 1; k < parts && k < kMaxQueues; ++k) {
         if (c->q[k]) continue;
         if (hsa_queue_create(c->gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
                              UINT32_MAX, UINT32_MAX, &c->q[k]) != HSA_STATUS_SUCCESS) {
             c->q[k] = nullptr;
-            return rti::fail(RT_ERR_HIP, "hsa_queue_create failed");
+            return false;
         }
     }
+    return true;
+}
+
+rt_status chain_begin(Chain* c, hipStream_t stream, uint32_t parts) {
+    (void)stream;
+    if (!c->ok || c->open) return rti::fail(RT_ERR_INVALID_ARGUMENT, "chain_begin");
+    parts = parts < 1u ? 1u : parts > kMaxQueues ? kMaxQueues : parts;
+    if (!chain_queues(c, parts)) return rti::fail(RT_ERR_HIP, "hsa_queue_create failed");
     SignalSet& s = c->sets[c->set];
     if (s.used) wait_zero(s.done);    // this set's previous segment (and its buffers) is done
     s.frames.clear();

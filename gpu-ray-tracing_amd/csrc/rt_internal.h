@@ -49,6 +49,8 @@ constexpr uint32_t kMaxSegmentPackets = 1024;
 Chain* chain_create(int device, rt_status* status);
 void chain_destroy(Chain* c);
 bool chain_ok(const Chain* c, const char** why);
+// the queues of `parts` parts exist (created now if not); false if one cannot be created
+bool chain_queues(Chain* c, uint32_t parts);
 rt_status chain_begin(Chain* c, hipStream_t stream, uint32_t parts);
 rt_status chain_frame(Chain* c, const rtk::TraceParams& p, int kernel, uint32_t part);
 rt_status chain_end(Chain* c, hipStream_t stream);
