@@ -1,7 +1,7 @@
 // rt_chain.cpp — one-frame `update` dispatches submitted as AQL packets on HSA queues the
-// context owns (rt_set_update_submit): the per-frame dispatch loop of ComputeShaderNode::run
-// (lib.rs:366-374, 408-417) with a host cost of a packet write per frame instead of a HIP
-// launch.
+// context owns (rt_set_update_submit; AUTO uses it for mid-sized rank shares, rt_abi.cpp
+// usable_chain): the per-frame dispatch loop of ComputeShaderNode::run (lib.rs:366-374,
+// 408-417) with a host cost of a packet write per frame instead of a HIP launch.
 //
 // A HIP launch costs the host 2.7-4.4 µs (profiles/r03*_launch_rate.jsonl), which bounds
 // how many concurrent parts a small rank share can use, and HIP's dispatches carry cache
