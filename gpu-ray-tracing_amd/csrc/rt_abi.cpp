@@ -916,7 +916,10 @@ void note_launch(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t fr
 // mid-sized rank shares, where two queues of packets beat HIP launches (a 4-rank K3 share
 // 6.76 against 7.54-7.68 µs per update, profiles/r03zd_rank_sim_*.jsonl, two rounds; whole
 // images and 2-rank shares run alike either way, 8-rank shares faster as one HIP launch).
-constexpr uint64_t kAqlAutoMinTiles = 6000, kAqlAutoMaxTiles = 12000;
+#ifndef RT_AQL_AUTO_MAX_TILES
+#define RT_AQL_AUTO_MAX_TILES 12000
+#endif
+constexpr uint64_t kAqlAutoMinTiles = 6000, kAqlAutoMaxTiles = RT_AQL_AUTO_MAX_TILES;
 rt_status usable_chain(rt_ctx* ctx, const rtk::TraceParams& p, rtc::Chain** out) {
     *out = nullptr;
     if (ctx->update_submit == RT_SUBMIT_HIP) return RT_OK;
