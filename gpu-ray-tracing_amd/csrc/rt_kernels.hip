@@ -1513,9 +1513,12 @@ constexpr int kSingleDisk = RT_SINGLE_DISK;
 // per-row tables (two dependent loads behind the order entry) or computed in the wave —
 // one hash per lane (lanes [0, 8*kPix) the wave's columns, the next 8 its rows), handed to
 // the pixels with ds_bpermute — so the camera rays need no memory at all.  Bit k set =
-// computed in the kPix = k + 1 instance.
+// computed in the kPix = k + 1 instance.  Default: the one-tile instance (rank shares)
+// computes them — 4-rank shares 0.1-0.3 µs faster per update, 8-rank unchanged
+// (profiles/r03zn_single_hash1.txt); the two-tile instance (whole images) reads the tables
+// (computing them there cost 0.9 µs at K3, profiles/r03e_ab_single_switches.log).
 #ifndef RT_SINGLE_HASH
-#define RT_SINGLE_HASH 0
+#define RT_SINGLE_HASH 1
 #endif
 
 
