@@ -4,9 +4,13 @@
 
 Configs (BASELINE.json `configs`):
   K2, K3 (default)  1920x1080, 3 / 500 spheres, max_depth 1.  A step is ONE progressive
-                    `update` dispatch (wgsl:333-364) — one launch per frame, the reference's
-                    dispatch structure (lib.rs:408-417): one camera sample per pixel of this
-                    rank's stripe bands, read-modify-write of the RGBA32F accumulator.
+                    `update` (wgsl:333-364): one camera sample per pixel of this rank's stripe
+                    bands, accumulated into the RGBA32F image.  The whole image (N=1) runs
+                    one launch per frame, the reference's dispatch structure (lib.rs:408-417);
+                    rank shares of at most CHAIN_MAX_TILES tiles run the steps' frames as
+                    frame chains — fused launches that still write every frame's image to the
+                    ping-pong buffer its dispatch would write (rt_set_frame_images EVERY), so
+                    only the launch boundary between frames goes (--frame-launch).
   K4                1920x1080, 500 spheres, 64 spp anti-aliased accumulate, max_depth 1.  A
                     step is one 64-spp render from a reset accumulator: 64 chained updates
                     issued by one rt_update_frames call (fused launches of up to 64 frames).
@@ -74,15 +78,37 @@ BENCH_SPP = 65536             # the dispatch configs' spp cap (never reached; fi
 CONFIGS = {
     # name: width, height, scene kind, spheres, max_depth, frames per step, description
     "K2": (1920, 1080, rt.SCENE_THREE, 3, 1, 1,
-           "configs[1]: 1920x1080, 3 spheres, 1 spp, one update dispatch per step"),
+           "configs[1]: 1920x1080, 3 spheres, 1 spp, one progressive update per step"),
     "K3": (1920, 1080, rt.SCENE_N, 500, 1, 1,
-           "configs[2]: 1920x1080, 500 spheres, 1 spp, one update dispatch per step"),
+           "configs[2]: 1920x1080, 500 spheres, 1 spp, one progressive update per step"),
     "K4": (1920, 1080, rt.SCENE_N, 500, 1, 64,
            "configs[3]: 1920x1080, 500 spheres, 64 spp accumulate per step (fused launches)"),
     "K5": (3840, 2160, rt.SCENE_N, 500, 8, 64,
            "configs[4]: 3840x2160, 500 spheres, 64 spp, 8 bounces per step"),
 }
 DEFAULT_STEPS = {"K2": (200, 20), "K3": (200, 20), "K4": (8, 2), "K5": (2, 1)}
+# K2/K3 steps of a rank share of at most this many 8x8 tiles run as frame chains (fused
+# launches writing every frame's image) under --frame-launch auto; larger shares (the whole
+# image: 32 400 tiles) one update launch per frame.  DESIGN.md §6.
+CHAIN_MAX_TILES = 20000
+
+
+def share_tiles(w, rows):
+    return ((w + 7) // 8) * ((rows + 7) // 8)
+
+
+def frame_launch_mode(policy, w, rows):
+    """The K2/K3 step structure for a share of `rows` local rows: 'dispatch' or 'chain'."""
+    if policy != "auto":
+        return policy
+    return "chain" if share_tiles(w, rows) <= CHAIN_MAX_TILES else "dispatch"
+
+
+def set_frame_launch(pipe, mode):
+    """dispatch: one `update` launch per frame (rt_set_frames_per_launch(1)); chain: fused
+    launches (up to 64 frames) that write every frame's image (rt_set_frame_images EVERY)."""
+    pipe.set_frames_per_launch(1 if mode == "dispatch" else 0)
+    pipe.set_frame_images("every" if mode == "chain" else "last_two")
 
 
 def parse():
@@ -103,6 +129,14 @@ def parse():
                          "frames on scratch images (untimed: a running render's steps, not a "
                          "freshly started process's first launches, are what is timed; 0 = "
                          "off)")
+    ap.add_argument("--frame-launch", default=os.environ.get("RT_FRAME_LAUNCH", "auto"),
+                    choices=["auto", "dispatch", "chain"],
+                    help="K2/K3 steps: one update launch per frame (dispatch, the reference's "
+                         "structure), or the rank's consecutive frames in fused launches that "
+                         "still write every frame's image to its ping-pong buffer (chain: "
+                         "rt_set_frame_images EVERY, only the launch boundary between frames "
+                         "removed); auto = dispatch for shares of at least "
+                         "CHAIN_MAX_TILES + 1 tiles (whole images), chain below")
     ap.add_argument("--scan", default="culled", choices=["culled", "exhaustive"],
                     help="sphere-list scan: exact culling (default) or the reference's "
                          "exhaustive linear walk; images are bit-identical")
@@ -230,6 +264,127 @@ def image_check(config, image, frames, cam, w, h):
     return bool(same.all()), f"{want.shape[0]} sampled pixels of the 64-spp render"
 
 
+def share_pixels_ok(config, local, frames, world):
+    """Rank 0's share (local rows of bands 0, world, 2*world, ...) against the fixture's
+    sampled pixels that fall in those bands (the K2/K3 fixtures after `frames` frames, K5's
+    64-spp render)."""
+    img = local.detach().cpu().numpy()
+    if config in ("K2", "K3"):
+        g = dict(np.load(GOLDEN / f"bench_{config.lower()}.npz"))
+        counts = [int(c) for c in g["frame_counts"]]
+        if frames not in counts:
+            return None
+        want = g["pixels"][counts.index(frames)]
+    else:
+        g = dict(np.load(GOLDEN / f"{config.lower()}.npz"))
+        want = g["pixels"]
+    py, px = g["py"], g["px"]
+    mine = (py // 8) % world == 0
+    ly = (py[mine] // 8 // world) * 8 + py[mine] % 8
+    got, want = img[ly, px[mine]], want[mine]
+    same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+    return bool(same.all()) and int(mine.sum()) > 0
+
+
+def driver_record_sides(device, stream, main_cfg, main_us):
+    """Side measurements for the driver's N=1 record (after the timed region), each with its
+    image check: the other per-dispatch config (K2 next to K3), one K5 64-spp step, and rank
+    0's 1/2, 1/4, 1/8 shares of K3 (one update launch per frame, and frame chains) and K5 timed
+    alone on this GPU — what each rank of `bench.py --gpus N` computes per step, so the
+    strong-scaling curve has a per-rank measurement behind it (tools/rank_sim.py's method)."""
+    out = {}
+    pipe = rt.ComputeShaderPipeline(device)
+    try:
+        def setup(cfg):
+            w, h, kind, nsph, depth, spf, _ = CONFIGS[cfg]
+            if spf == 1:
+                sc = rt.SphereCollection.generate(kind, nsph, 1)
+                seeds = rt.frame_seeds(FRAME_SEED, 25)
+                st = rt.CameraSettings(max_depth=depth, samples_per_pixel=BENCH_SPP)
+                cam = rt.SceneCamera.from_settings(st, w, h, float(seeds[0]))
+            else:
+                g = dict(np.load(GOLDEN / f"{cfg.lower()}.npz"))
+                sc, seeds, cam = rt.SphereCollection(g["spheres"]), g["seeds"], rt.SceneCamera(g["camera"])
+            return w, h, sc, seeds, cam
+
+        def dispatch_share(cfg, world, mode):
+            # the driver's structure: 5 frames from a reset, then 20 timed (25-frame fixture);
+            # one untimed pass first on scratch images (the share's lists, order, code)
+            w, h, sc, seeds, cam = setup(cfg)
+            set_frame_launch(pipe, mode)
+            cam_t = cam.with_fields(camera_has_moved=0.0)
+            scratch = StripeRenderer(pipe, w, h, 0, world)
+            scratch.frames(cam, sc, seeds[:20])
+            del scratch
+            r = StripeRenderer(pipe, w, h, 0, world)
+            r.frames(cam, sc, seeds[:5])
+            t = timed(stream, lambda: r.frames(cam_t, sc, seeds[5:25])) / 20
+            info = pipe.last_launch_info()
+            return {"us_per_step": round(t * 1e6, 2), "kernel": info["kernel_name"],
+                    "launches_per_step": round(info["launches"] / 20, 3),
+                    "image_ok": share_pixels_ok(cfg, r.local, 25, world)}
+
+        def k5_share(world):
+            w, h, sc, seeds, cam = setup("K5")
+            pipe.set_frames_per_launch(0)
+            pipe.set_frame_images("last_two")
+            r = StripeRenderer(pipe, w, h, 0, world)
+            r.frames(cam, sc, seeds)                   # records the tile costs
+            t = timed(stream, lambda: r.frames(cam, sc, seeds))
+            info = pipe.last_launch_info()
+            return {"us_per_step": round(t * 1e6, 1), "us_per_spp": round(t / 64 * 1e6, 2),
+                    "kernel": info["kernel_name"],
+                    "image_ok": share_pixels_ok("K5", r.local, 64, world)}
+
+        other = "K2" if main_cfg == "K3" else "K3"
+        d = dispatch_share(other, 1, "dispatch")
+        w, h = CONFIGS[other][:2]
+        out[other.lower()] = dict(d, Mrays_per_s=round(w * h / d["us_per_step"], 1),
+                                  hbm_frac=round(w * h * BYTES_PER_PIXEL_LAUNCH /
+                                                 (d["us_per_step"] * 1e3) / PEAK_HBM_GBS, 4),
+                                  what=f"{other}: 5 + 20 frames from a reset, one update "
+                                       f"launch per frame, µs per update by HIP events")
+        k5 = k5_share(1)
+        out["k5"] = dict(k5, Mrays_per_s=round(3840 * 2160 * 64 / k5["us_per_step"], 1),
+                         what="one 64-spp 3840x2160 depth-8 step (one 64-frame bounce launch, "
+                              "cost-ordered by the step before), 512 sampled pixels")
+        shares = {"K3": {}, "K5": {}}
+        base = {"dispatch": main_us if main_cfg == "K3" else None}
+        for mode in ("dispatch", "chain"):
+            rows = {}
+            for world in (1, 2, 4, 8):
+                if world == 1 and mode == "dispatch" and base["dispatch"]:
+                    rows["1"] = {"us_per_step": round(base["dispatch"], 2), "kernel": "(the timed steps)"}
+                    continue
+                rows[str(world)] = dispatch_share("K3", world, mode)
+            ref = rows["1"]["us_per_step"]
+            for k, v in rows.items():
+                v["predicted_efficiency"] = round(ref / (int(k) * v["us_per_step"]), 3)
+            shares["K3"][mode] = rows
+        # efficiency of each share against the 1-GPU step as the line times it
+        one = shares["K3"]["dispatch"]["1"]["us_per_step"]
+        for mode in ("dispatch", "chain"):
+            for k, v in shares["K3"][mode].items():
+                v["efficiency_vs_1gpu_step"] = round(one / (int(k) * v["us_per_step"]), 3)
+        k5rows = {"1": {"us_per_step": k5["us_per_step"], "us_per_spp": k5["us_per_spp"]}}
+        for world in (2, 4, 8):
+            k5rows[str(world)] = k5_share(world)
+        for k, v in k5rows.items():
+            v["predicted_efficiency"] = round(k5["us_per_step"] / (int(k) * v["us_per_step"]), 3)
+        shares["K5"]["fused_64"] = k5rows
+        shares["what"] = ("rank 0's stripe share (8-row bands dealt round-robin) timed alone on "
+                          "this GPU, i.e. one rank's step of bench.py --gpus N; "
+                          "predicted_efficiency = the 1-rank time / (N x the share's time) in "
+                          "the same launch structure; K3 'dispatch' = one update launch per "
+                          "frame, 'chain' = fused launches writing every frame's image "
+                          "(--frame-launch auto takes chain for shares <= %d tiles)"
+                          % CHAIN_MAX_TILES)
+        out["rank_shares"] = shares
+    finally:
+        pipe.close()
+    return out
+
+
 def timed(stream, fn):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -280,8 +435,12 @@ def main():
     pipe = rt.ComputeShaderPipeline(device)
     pipe.set_scan_mode(args.scan)
     pipe.set_spheres(spheres)
+    launch_mode = None
     if dispatch:
-        pipe.set_frames_per_launch(1)          # one `update` launch per frame
+        # one `update` launch per frame, or (small rank shares) frame chains
+        launch_mode = frame_launch_mode(args.frame_launch, w,
+                                        rt.stripe_local_rows(h, rank, world))
+        set_frame_launch(pipe, launch_mode)
     pipe.set_update_queues(args.queues)
     pipe.set_update_submit(args.submit)
     # the job's one gather: RCCL behind the C ABI (rt_comm_create + rt_gather_stripes)
@@ -302,6 +461,29 @@ def main():
             for _ in range(n):
                 r.frames(cam0, spheres, seeds)
 
+    # Cold start (N=1 side line, before anything else ran on the GPU in this process): the
+    # same W + K frames on scratch images, timed the same way — what the line's value would
+    # be without the warm-up below.
+    cold = None
+    if args.side > 0 and world == 1 and dispatch:
+        cr = StripeRenderer(pipe, w, h, rank, world, comm=None)
+        torch.cuda.synchronize()
+        if args.warmup:
+            cr.frames(cam0, spheres, seeds[:args.warmup])
+        torch.cuda.synchronize()
+        tc0 = time.perf_counter()
+        t_cold = timed(torch.cuda.current_stream(), lambda: cr.frames(
+            cam0 if args.warmup == 0 else cam_t, spheres,
+            seeds[args.warmup:args.warmup + args.steps]))
+        dt_cold = time.perf_counter() - tc0
+        ok, what = image_check(cfg, cr.local, args.warmup + args.steps, cam0, w, h)
+        cold = {"us_per_step_events": round(t_cold / args.steps * 1e6, 2),
+                "us_per_step_wall": round(dt_cold / args.steps * 1e6, 2),
+                "Mrays_per_s": round(w * h * args.steps / dt_cold / 1e6, 1),
+                "image_ok": ok, "image_check": what,
+                "what": "the same warmup + steps frames on scratch images at process start, "
+                        "before the --warm-ms warm-up (wall: synchronize on both sides)"}
+        del cr
     # Warm-up (untimed, scratch images): a progressive render's steps run back to back in a
     # process that has long been issuing them; a 20-step timed region (~0.4 ms) right after
     # process start would otherwise time the chip's start from idle (K3: 22.2 against 16.2 µs
@@ -380,6 +562,10 @@ def main():
     kernel = info["kernel_name"]
     fpl = info["max_frames_per_launch"]
     bytes_launch = local_px * BYTES_PER_PIXEL_LAUNCH
+    if launch_mode == "chain":
+        # a frame chain carries fpl progressive updates: the reference's 32 B per pixel each
+        # (it writes every frame's 16 B; the accumulator stays in registers between frames)
+        bytes_launch *= fpl
     pmc, pmc_path = load_pmc(cfg, kernel, fpl) if world == 1 else (None, None)
     wgt, wgt_path = load_weighted(cfg, kernel) if pmc else (None, None)
     roof = {"bound": "hbm", "achieved": round(bytes_launch / launch_s / 1e9, 1),
@@ -433,7 +619,13 @@ def main():
         "config": {"workload": f"{cfg} {desc}, max_depth {depth}",
                    "width": w, "height": h, "spheres": nsph, "spp_per_step": spf,
                    "max_depth": depth, "parallelism": f"stripes{world}",
-                   "scan": args.scan, "kernel": kernel},
+                   "scan": args.scan, "kernel": kernel,
+                   "frame_launch": launch_mode or "fused_64",
+                   "step": ("one progressive update (1 spp) of every pixel of the rank's "
+                            "bands; " + {"dispatch": "one update launch per frame",
+                                         "chain": "the steps' frames in fused launches, every "
+                                                  "frame's image written",
+                                         None: "64 frames per step"}[launch_mode])},
         "roofline": roof,
         "image_ok": image_ok,
         "image_check": image_what,
@@ -470,12 +662,14 @@ def main():
                 "achieved": round(flops / t_exh / 1e12, 3), "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(flops / t_exh / 1e12 / PEAK_FP32_TFLOPS, 4),
                 "flop_per_frame": flops}
-            # the same frames fused (up to 64 per launch; K4's launches)
+            # the same frames fused (up to 64 per launch; K4's launches, the last two
+            # frames' images written)
+            set_frame_launch(pipe, "dispatch")
             pipe.set_frames_per_launch(0)
             s1 = base + args.side
             t_f = timed(stream, lambda: r.frames(cam_t, spheres, seeds[s1:s1 + args.side]))
             fi = pipe.last_launch_info()
-            pipe.set_frames_per_launch(1)
+            set_frame_launch(pipe, launch_mode)
             side["fused_frames"] = {"kernel": fi["kernel_name"],
                                     "frames_per_launch": fi["max_frames_per_launch"],
                                     "us_per_frame": round(t_f / args.side * 1e6, 2),
@@ -514,6 +708,11 @@ def main():
                                      "achieved": round(w * h * 20 / t_p / 1e9, 1),
                                      "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                      "frac": round(w * h * 20 / t_p / 1e9 / PEAK_HBM_GBS, 4)}
+        if cold is not None:
+            side["cold_start"] = cold
+        if dispatch and depth == 1:
+            # K2 / K5 / rank shares: each with its image check
+            side.update(driver_record_sides(device, stream, cfg, render_s / args.steps * 1e6))
     line.update(side)
 
     if rank == 0:

@@ -97,6 +97,10 @@ struct rt_ctx {
     int update_submit = RT_SUBMIT_AUTO;
     rtc::Chain* chain = nullptr;
     bool chain_tried = false;
+    bool chain_reported = false;     // a chain failure has been returned to the caller once
+    // Images of fused multi-frame launches (rt_set_frame_images): the last two frames' only,
+    // or every frame's (TraceParams::store_each 1 / 2)
+    int frame_images = RT_FRAME_IMAGES_LAST_TWO;
 };
 
 namespace {
@@ -909,20 +913,39 @@ void note_launch(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t fr
     ctx->last.kernel = kernel != rtk::kTraceBounce ? kernel : RT_KERNEL_BOUNCE + (int)p.compact;
 }
 
+// A chain failure (a go wait that gave up, so a segment's frames were dropped; a queue
+// error; a segment that did not complete in time) is returned once, by the context's next
+// call (rt_update_frames, rt_destroy, rt_update_submit_status); the context runs HIP launches
+// from then on.  No synchronisation: the flags live in host memory.
+rt_status chain_report(rt_ctx* ctx) {
+    if (!ctx->chain || ctx->chain_reported || !rtc::chain_failed(ctx->chain)) return RT_OK;
+    ctx->chain_reported = true;
+    const char* why = "";
+    (void)rtc::chain_ok(ctx->chain, &why);
+    return fail(RT_ERR_HIP, std::string("AQL submission failed earlier (") + why +
+                                "); the context runs HIP launches from now on");
+}
+
 // The context's AQL chain if one-frame updates go through it (rt_set_update_submit AQL, or
-// AUTO for mid-sized launches): created on first use; AQL fails the call with the reason when
-// the machine does not offer it, AUTO falls back to HIP launches.
-// AUTO submits as AQL packets the launches of [kAqlAutoMinTiles, kAqlAutoMaxTiles) tiles —
-// mid-sized rank shares, where two queues of packets beat HIP launches (a 4-rank K3 share
-// 6.76 against 7.54-7.68 µs per update, profiles/r03zd_rank_sim_*.jsonl, two rounds; whole
-// images and 2-rank shares run alike either way, 8-rank shares faster as one HIP launch).
-#ifndef RT_AQL_AUTO_MAX_TILES
-#define RT_AQL_AUTO_MAX_TILES 12000
+// AUTO inside [kAqlAutoMinTiles, kAqlAutoMaxTiles) tiles — an empty range since round 4:
+// AQL submission is opt-in): created on first use; AQL fails the call with the reason when
+// the machine does not offer it, AUTO falls back to HIP launches, and after a chain failure
+// every mode runs HIP launches.  Round 3 measured AQL faster only on mid-sized rank shares
+// of per-dispatch updates (a 4-rank K3 share 6.76 against 7.54-7.68 µs per update,
+// profiles/r03zd_rank_sim_*.jsonl; whole images and 2-rank shares alike either way, 8-rank
+// shares slower); rank shares now run fused frame chains in one launch instead
+// (rt_set_frame_images), and no multi-GPU record of AQL submission exists.
+#ifndef RT_AQL_AUTO_MIN_TILES
+#define RT_AQL_AUTO_MIN_TILES 0
 #endif
-constexpr uint64_t kAqlAutoMinTiles = 6000, kAqlAutoMaxTiles = RT_AQL_AUTO_MAX_TILES;
+#ifndef RT_AQL_AUTO_MAX_TILES
+#define RT_AQL_AUTO_MAX_TILES 0
+#endif
+constexpr uint64_t kAqlAutoMinTiles = RT_AQL_AUTO_MIN_TILES,
+                   kAqlAutoMaxTiles = RT_AQL_AUTO_MAX_TILES;
 rt_status usable_chain(rt_ctx* ctx, const rtk::TraceParams& p, rtc::Chain** out) {
     *out = nullptr;
-    if (ctx->update_submit == RT_SUBMIT_HIP) return RT_OK;
+    if (ctx->update_submit == RT_SUBMIT_HIP || ctx->chain_reported) return RT_OK;
     if (ctx->update_submit == RT_SUBMIT_AUTO) {
         const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
         if (tiles < kAqlAutoMinTiles || tiles >= kAqlAutoMaxTiles) return RT_OK;
@@ -1067,6 +1090,7 @@ rt_status rt_create(int device, rt_ctx** out_ctx) {
 
 rt_status rt_destroy(rt_ctx* ctx) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    rt_status st = RT_OK;
     {
         DeviceGuard guard(ctx->device);
         if (ctx->d_geom || ctx->d_sph || ctx->cand) (void)hipDeviceSynchronize();
@@ -1084,10 +1108,12 @@ rt_status rt_destroy(rt_ctx* ctx) {
             if (ctx->join_ev[k]) (void)hipEventDestroy(ctx->join_ev[k]);
         }
         if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
-        rtc::chain_destroy(ctx->chain);
+        st = chain_report(ctx);
+        // (a segment still outstanding after the bound leaves the chain's resources in place)
+        if (rt_status d = rtc::chain_destroy(ctx->chain)) st = d;
     }
     delete ctx;
-    return RT_OK;
+    return st;
 }
 
 rt_status rt_set_scan_mode(rt_ctx* ctx, int mode) {
@@ -1153,21 +1179,30 @@ rt_status rt_update_submit_status(rt_ctx* ctx, int* aql_available, uint32_t* go_
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
     if (!ctx->chain_tried) {
+        // (sets the chain up without any HSA queue: queues are created by the first segment)
         ctx->chain_tried = true;
         rt_status st = RT_OK;
         ctx->chain = rtc::chain_create(ctx->device, &st);
         if (st != RT_OK) return st;
     }
+    uint32_t gave_up = 0;
+    if (ctx->chain && !rtc::chain_failed(ctx->chain))
+        if (rt_status s = rtc::chain_errors(ctx->chain, &gave_up)) return s;
+    if (rt_status s = chain_report(ctx)) return s;
     const char* why = "";
     const bool ok = rtc::chain_ok(ctx->chain, &why);
     if (aql_available) *aql_available = ok ? 1 : 0;
     if (packets) *packets = rtc::chain_packets(ctx->chain);
-    if (go_give_ups) {
-        *go_give_ups = 0;
-        if (ok)
-            if (rt_status s = rtc::chain_errors(ctx->chain, go_give_ups)) return s;
-    }
+    if (go_give_ups) *go_give_ups = (ctx->chain && rtc::chain_failed(ctx->chain)) ? 1u : gave_up;
     if (!ok) fail(RT_OK, std::string("AQL submission unavailable: ") + why);
+    return RT_OK;
+}
+
+rt_status rt_set_frame_images(rt_ctx* ctx, int mode) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (mode != RT_FRAME_IMAGES_LAST_TWO && mode != RT_FRAME_IMAGES_EVERY)
+        return fail(RT_ERR_INVALID_ARGUMENT, "unknown frame-images mode");
+    ctx->frame_images = mode;
     return RT_OK;
 }
 
@@ -1240,6 +1275,8 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
     if (image_a == image_b) return fail(RT_ERR_INVALID_ARGUMENT, "image_a and image_b alias");
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    // an earlier call's AQL segment that failed is reported here, once
+    if (rt_status s = chain_report(ctx)) return s;
     hipStream_t stream = static_cast<hipStream_t>(stream_v);
     rtk::TraceParams p;
     if (rt_status s = prepare(ctx, image_a, image_b, w, h, rank, nranks, cam, spheres, count,
@@ -1255,21 +1292,38 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
     const uint32_t per = frames_per_launch_for(ctx, p);
     int cur = 0;
     ctx->last = {0, 0, 0, -1, 0, 0};
-    uint32_t aux_live = 0;      // aux streams with work of this call not yet joined
+    // What the call has in flight beside the caller's stream, closed on every exit path (an
+    // error return included): an AQL segment still being packed is dropped (nothing of it has
+    // been submitted), and the context's aux streams are joined back into `stream`, so the
+    // caller's later work stays ordered after everything the call issued.
+    struct InFlight {
+        rt_ctx* ctx;
+        hipStream_t stream;
+        rtc::Chain* chain = nullptr;
+        bool seg_open = false;      // an AQL segment of this call is open
+        uint32_t aux_live = 0;      // aux streams with work of this call not yet joined
+        ~InFlight() {
+            if (seg_open) rtc::chain_abort(chain);
+            for (uint32_t k = 0; k < aux_live; ++k)   // (errors here: the call already failed)
+                if (hipEventRecord(ctx->join_ev[k], ctx->aux[k]) == hipSuccess)
+                    (void)hipStreamWaitEvent(stream, ctx->join_ev[k], 0);
+        }
+    } fl{ctx, stream};
     bool forked = false;        // aux streams ordered after the last work on `stream`
     // One-frame launches of the one-frame instances go out as AQL packets when the call has
     // two or more of them (rt_set_update_submit; a single update gains nothing from it).
-    rtc::Chain* chain = nullptr;
     if (per == 1u && frames >= 2u)
-        if (rt_status s = usable_chain(ctx, p, &chain)) return s;
-    bool seg_open = false;      // an AQL segment of this call is open
+        if (rt_status s = usable_chain(ctx, p, &fl.chain)) return s;
+    rtc::Chain* const chain = fl.chain;
     uint32_t seg_parts = 0, seg_packets = 0;
     for (uint32_t f0 = 0; f0 < frames; f0 += per) {
         const uint32_t nf = std::min<uint32_t>(per, frames - f0);
         p.in = img[cur];
         p.out = img[1 - cur];
         p.out2 = img[cur];
-        p.store_each = nf > 1 ? 1u : 0u;   // (nf == 1: the plain single-frame store)
+        // (nf == 1: the plain single-frame store; else the ping-pong images of the last two
+        // frames, or of every frame: rt_set_frame_images)
+        p.store_each = nf == 1u ? 0u : ctx->frame_images == RT_FRAME_IMAGES_EVERY ? 2u : 1u;
         p.frames = nf;
         p.reset_first = (f0 == 0 && cam->camera_has_moved > 0.5f) ? 1u : 0u;
         for (uint32_t f = 0; f < nf; ++f) p.seed_b[f] = host_f2u(seeds[f0 + f] * 4294967296.0f);
@@ -1304,24 +1358,27 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         const uint32_t parts = aql ? update_parts_aql(ctx, p) : update_parts(ctx, p, kernel);
         p.parts = parts;
         p.part = 0;
-        if (seg_open && (!aql || parts != seg_parts || wg_order_pending(ctx, p, kernel) ||
-                         seg_packets + parts > rtc::kMaxSegmentPackets)) {
+        // A new workgroup order (built on the stream by plan_wg_order) changes which pixels
+        // each part owns, and rewrites the order buffer the parts may still be reading: the
+        // parts in flight are joined into `stream` first and forked again after it.
+        const bool new_order = wg_order_pending(ctx, p, kernel);
+        if (fl.seg_open && (!aql || parts != seg_parts || new_order ||
+                            seg_packets + parts > rtc::kMaxSegmentPackets)) {
+            fl.seg_open = false;
             if (rt_status s = rtc::chain_end(chain, stream)) return s;
-            seg_open = false;
         }
-        if ((parts == 1u || aql) && aux_live) {  // back to one launch: wait for the parts
-            if (rt_status s = join_aux(ctx, aux_live, stream)) return s;
-            aux_live = 0;
+        if ((parts == 1u || aql || new_order) && fl.aux_live) {  // wait for the parts
+            if (rt_status s = join_aux(ctx, fl.aux_live, stream)) return s;
+            fl.aux_live = 0;
             forked = false;
         }
-        const uint64_t builds = ctx->wg_builds;
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         if (rt_status s = plan_wg_order(ctx, p, kernel, stream)) return s;
         if (aql) {
             // frame f of part k is a packet on the chain's queue k, after part k's frame f - 1
-            if (!seg_open) {
+            if (!fl.seg_open) {
                 if (rt_status s = rtc::chain_begin(chain, stream, parts)) return s;
-                seg_open = true;
+                fl.seg_open = true;
                 seg_parts = parts;
                 seg_packets = 0;
             }
@@ -1334,7 +1391,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
             // every part's next frame reads only the pixels its own previous frame wrote;
             // what `stream` prepared (lists, order, the input image) is forked to the others
             if (rt_status s = ensure_aux_streams(ctx, parts - 1u)) return s;
-            if (!forked || ctx->wg_builds != builds) {
+            if (!forked) {
                 if (rt_status s = fork_aux(ctx, parts - 1u, stream)) return s;
                 forked = true;
             }
@@ -1342,8 +1399,8 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
                 p.part = k;
                 hipError_t e = rtk::launch_trace(p, kernel, k ? ctx->aux[k - 1] : stream);
                 if (e != hipSuccess) return hip_fail(e, "rt_single_kernel launch");
+                if (k) fl.aux_live = std::max(fl.aux_live, k);
             }
-            aux_live = std::max(aux_live, parts - 1u);
         } else {
             hipError_t e = rtk::launch_trace(p, kernel, stream);
             if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
@@ -1361,10 +1418,15 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         }
         cur = newest;
     }
-    if (seg_open)   // the call's work ends on the caller's stream
+    if (fl.seg_open) {   // the call's work ends on the caller's stream
+        fl.seg_open = false;
         if (rt_status s = rtc::chain_end(chain, stream)) return s;
-    if (aux_live)
-        if (rt_status s = join_aux(ctx, aux_live, stream)) return s;
+    }
+    if (fl.aux_live) {
+        const uint32_t n = fl.aux_live;
+        fl.aux_live = 0;
+        if (rt_status s = join_aux(ctx, n, stream)) return s;
+    }
     if (out_newest) *out_newest = cur;
     return RT_OK;
 }

@@ -39,7 +39,9 @@
 #include <immintrin.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -84,7 +86,12 @@ struct SignalSet {
 struct Chain {
     int device = 0;
     bool ok = false;
+    bool hsa_up = false;                   // hsa_init succeeded (hsa_shut_down in destroy)
     std::string why = "not initialised";
+    // A failed chain (a go wait that gave up, a queue error, a segment that did not complete
+    // within the bound) takes no more segments: the context runs HIP launches from then on.
+    bool failed = false;
+    std::atomic<int> queue_error{0};       // hsa_status_t from the queues' error callback
     hsa_agent_t gpu{}, cpu{};
     hsa_queue_t* q[kMaxQueues] = {};
     KernelObj k[rtk::kChainKernels];
@@ -99,7 +106,13 @@ struct Chain {
     uint32_t set = 0;                      // set of the open / next segment
     uint32_t* go = nullptr;                // signal memory: the caller's stream writes seq
     uint32_t* done = nullptr;              // signal memory: the done packet writes seq
-    uint32_t* err = nullptr;               // go waits that gave up
+    // A go wait that gives up writes both words: `abort` in device memory (every chain
+    // kernel checks it before its image stores, so no frame of a segment runs before the
+    // caller's stream has reached it: the segment's frames are dropped instead) and
+    // `gave_up` in coherent host memory (read by the host without a synchronisation).
+    uint32_t* abort = nullptr;
+    volatile uint32_t* gave_up = nullptr;
+    uint64_t go_ticks = 0;                 // the go wait's bound (s_memrealtime, 100 MHz)
     uint32_t seq = 0;
     // the open segment
     bool open = false;
@@ -266,10 +279,38 @@ void barrier_and(Chain* c, uint32_t qi, const hsa_signal_t* deps, uint32_t n) {
     c->packets++;
 }
 
-void wait_zero(hsa_signal_t s) {
-    while (hsa_signal_wait_scacquire(s, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX,
-                                     HSA_WAIT_STATE_BLOCKED) != 0) {
+// The go wait's bound (RT_CHAIN_GO_MS, default 10 s: the caller's stream work queued ahead
+// of a segment) and the host's bound on a segment's completion: the go bound plus 10 s.
+uint64_t go_bound_ms() {
+    const char* e = std::getenv("RT_CHAIN_GO_MS");
+    const long v = e ? std::strtol(e, nullptr, 10) : 0;
+    return v > 0 ? (uint64_t)v : 10000u;
+}
+
+// Waits until s reaches 0, at most `ms` milliseconds; false on timeout (the caller fails the
+// chain instead of hanging the process).
+bool wait_zero(hsa_signal_t s, uint64_t ms) {
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(ms);
+    for (;;) {
+        // (the timeout is a hint: the loop re-checks the clock)
+        if (hsa_signal_wait_scacquire(s, HSA_SIGNAL_CONDITION_EQ, 0, 100000000ull,
+                                      HSA_WAIT_STATE_BLOCKED) == 0)
+            return true;
+        if (std::chrono::steady_clock::now() >= t_end) return false;
     }
+}
+
+uint64_t wait_bound_ms(const Chain* c) { return c->go_ticks / 100000u + 10000u; }
+
+// Queue errors (a malformed packet, a memory fault in a chain kernel) arrive here on the
+// runtime's thread: the chain is marked failed.
+void queue_error_cb(hsa_status_t status, hsa_queue_t*, void* data) {
+    static_cast<Chain*>(data)->queue_error.store((int)status);
+}
+
+hsa_status_t make_queue(Chain* c, hsa_queue_t** q) {
+    return hsa_queue_create(c->gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, queue_error_cb, c,
+                            UINT32_MAX, UINT32_MAX, q);
 }
 
 rt_status setup(Chain* c) {
@@ -283,6 +324,8 @@ rt_status setup(Chain* c) {
         c->why = "hsa_init failed";
         return RT_OK;
     }
+    c->hsa_up = true;
+    c->go_ticks = go_bound_ms() * 100000ull;
     FindAgent fa;
     fa.bdf = ((uint32_t)prop.pciBusID << 8) | ((uint32_t)prop.pciDeviceID << 3);
     fa.domain = (uint32_t)prop.pciDomainID;
@@ -365,23 +408,23 @@ rt_status setup(Chain* c) {
         }
     }
     // go and done words: signal memory (hipStreamWriteValue32 / hipStreamWaitValue32
-    // targets); the go kernel's give-up counter
+    // targets); the go kernel's abort word (device) and give-up flag (coherent host memory)
     he = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->go), 8, hipMallocSignalMemory);
     if (he == hipSuccess)
         he = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->done), 8, hipMallocSignalMemory);
-    if (he == hipSuccess) he = hipMalloc(&c->err, sizeof(uint32_t));
-    if (he == hipSuccess) he = hipMemset(c->err, 0, sizeof(uint32_t));
+    if (he == hipSuccess) he = hipMalloc(&c->abort, sizeof(uint32_t));
+    if (he == hipSuccess) he = hipMemset(c->abort, 0, sizeof(uint32_t));
+    void* gu = nullptr;
+    if (he == hipSuccess) he = hipHostMalloc(&gu, sizeof(uint32_t), hipHostMallocCoherent);
+    if (he == hipSuccess) {
+        c->gave_up = static_cast<volatile uint32_t*>(gu);
+        *c->gave_up = 0u;
+    }
     if (he == hipSuccess) he = hipMemset(c->go, 0, 8);
     if (he == hipSuccess) he = hipMemset(c->done, 0, 8);
     if (he == hipSuccess) he = hipDeviceSynchronize();
     if (he != hipSuccess) return rti::hip_fail(he, "chain words");
-    // (queues are created as segments need them: chain_begin)
-    if (hsa_queue_create(c->gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
-                         UINT32_MAX, UINT32_MAX, &c->q[0]) != HSA_STATUS_SUCCESS) {
-        c->q[0] = nullptr;
-        c->why = "hsa_queue_create failed";
-        return RT_OK;
-    }
+    // (queues are created as segments need them: chain_queues; an idle context holds none)
     c->why = "";
     c->ok = true;
     return RT_OK;
@@ -400,10 +443,14 @@ Chain* chain_create(int device, rt_status* status) {
     return c;
 }
 
-void chain_destroy(Chain* c) {
-    if (!c) return;
+rt_status chain_destroy(Chain* c) {
+    if (!c) return RT_OK;
+    // every segment in flight completes within the bound (its go wait is bounded too); one
+    // that does not leaves its queues, signals and argument memory in place (the GPU may
+    // still read them) and the call reports the error
     for (SignalSet& s : c->sets)
-        if (s.used) wait_zero(s.done);
+        if (s.used && !wait_zero(s.done, wait_bound_ms(c)))
+            return rti::fail(RT_ERR_HIP, "AQL segment did not complete: chain resources leaked");
     for (hsa_queue_t* q : c->q)
         if (q) hsa_queue_destroy(q);
     for (SignalSet& s : c->sets) {
@@ -417,23 +464,43 @@ void chain_destroy(Chain* c) {
     if (c->small) hsa_amd_memory_pool_free(c->small);
     (void)hipFree(c->go);
     (void)hipFree(c->done);
-    (void)hipFree(c->err);
+    (void)hipFree(c->abort);
+    if (c->gave_up) (void)hipHostFree(const_cast<uint32_t*>(c->gave_up));
+    if (c->hsa_up) hsa_shut_down();
     delete c;
+    return RT_OK;
+}
+
+// Marks the chain failed (and why) if a go wait gave up or a queue reported an error since
+// the last check; true if it has failed.  No synchronisation: both flags live in host memory.
+bool chain_failed(Chain* c) {
+    if (!c) return false;
+    if (!c->failed) {
+        const int qe = c->queue_error.load();
+        if (qe != 0) {
+            c->failed = true;
+            c->why = "HSA queue error " + std::to_string(qe);
+        } else if (c->gave_up && *c->gave_up != 0u) {
+            c->failed = true;
+            c->why = "a segment's go wait gave up (the caller's stream had not reached it "
+                     "within the bound): its frames were dropped";
+        }
+    }
+    return c->failed;
 }
 
 bool chain_ok(const Chain* c, const char** why) {
     if (why) *why = c ? c->why.c_str() : "no chain";
-    return c && c->ok;
+    return c && c->ok && !c->failed;
 }
 
 bool chain_queues(Chain* c, uint32_t parts) {
     // one HSA queue per part, created on first use (idle queues still occupy the device's
     // hardware queue slots, which HIP's own streams share)
-    if (!c || !c->ok) return false;
-    for (uint32_t k = 1; k < parts && k < kMaxQueues; ++k) {
+    if (!c || !c->ok || c->failed) return false;
+    for (uint32_t k = 0; k < parts && k < kMaxQueues; ++k) {
         if (c->q[k]) continue;
-        if (hsa_queue_create(c->gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
-                             UINT32_MAX, UINT32_MAX, &c->q[k]) != HSA_STATUS_SUCCESS) {
+        if (make_queue(c, &c->q[k]) != HSA_STATUS_SUCCESS) {
             c->q[k] = nullptr;
             return false;
         }
@@ -444,10 +511,16 @@ bool chain_queues(Chain* c, uint32_t parts) {
 rt_status chain_begin(Chain* c, hipStream_t stream, uint32_t parts) {
     (void)stream;
     if (!c->ok || c->open) return rti::fail(RT_ERR_INVALID_ARGUMENT, "chain_begin");
+    if (chain_failed(c)) return rti::fail(RT_ERR_HIP, "AQL submission failed: " + c->why);
     parts = parts < 1u ? 1u : parts > kMaxQueues ? kMaxQueues : parts;
     if (!chain_queues(c, parts)) return rti::fail(RT_ERR_HIP, "hsa_queue_create failed");
     SignalSet& s = c->sets[c->set];
-    if (s.used) wait_zero(s.done);    // this set's previous segment (and its buffers) is done
+    // this set's previous segment (and its buffers) is done
+    if (s.used && !wait_zero(s.done, wait_bound_ms(c))) {
+        c->failed = true;
+        c->why = "an AQL segment did not complete within the bound";
+        return rti::fail(RT_ERR_HIP, c->why);
+    }
     s.frames.clear();
     if (c->ring) {
         if (c->ring_head + kMaxSegmentPackets > kRingSlots) c->ring_head = 0;
@@ -468,11 +541,19 @@ rt_status chain_frame(Chain* c, const rtk::TraceParams& p, int kernel, uint32_t 
     unsigned char* a = c->seg_args + s.frames.size() * kSlotBytes;
     uint32_t grid[2] = {0, 0}, threads = 0;
     int which = 0;
-    const uint32_t n = rtk::chain_args(p, kernel, a, kSlotBytes, grid, &threads, &which);
+    const uint32_t n =
+        rtk::chain_args(p, kernel, c->abort, a, kSlotBytes, grid, &threads, &which);
     if (n == 0) return RT_OK;                // an empty part
     if (c->k[which].kernarg > n) return rti::fail(RT_ERR_HIP, "chain kernel argument size mismatch");
     s.frames.push_back(Pending{part, grid[0], grid[1], threads, which});
     return RT_OK;
+}
+
+void chain_abort(Chain* c) {
+    // nothing of an open segment has been published yet: its packed frames are dropped
+    if (!c || !c->open) return;
+    c->open = false;
+    c->sets[c->set].frames.clear();
 }
 
 rt_status chain_end(Chain* c, hipStream_t stream) {
@@ -505,9 +586,11 @@ rt_status chain_end(Chain* c, hipStream_t stream) {
         const uint32_t* go;
         uint32_t want;
         uint32_t pad;
-        uint32_t* err;
-    } ga{c->go, seq, 0u, c->err};
-    static_assert(sizeof(ga) == 24, "rt_chain_go_kernel's argument layout");
+        uint32_t* abort;
+        uint32_t* gave_up;
+        uint64_t ticks;
+    } ga{c->go, seq, 0u, c->abort, const_cast<uint32_t*>(c->gave_up), c->go_ticks};
+    static_assert(sizeof(ga) == 40, "rt_chain_go_kernel's argument layout");
     std::memset(s.small, 0, 2 * kSlotBytes);
     std::memcpy(s.small, &ga, sizeof(ga));
     if (go) {
@@ -563,13 +646,16 @@ rt_status chain_end(Chain* c, hipStream_t stream) {
 
 rt_status chain_errors(Chain* c, uint32_t* out) {
     for (SignalSet& s : c->sets)
-        if (s.used) wait_zero(s.done);
-    uint32_t v = 0;
-    hipError_t e = hipMemcpy(&v, c->err, sizeof(v), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return rti::hip_fail(e, "chain error counter");
-    *out = v;
+        if (s.used && !wait_zero(s.done, wait_bound_ms(c))) {
+            c->failed = true;
+            c->why = "an AQL segment did not complete within the bound";
+            return rti::fail(RT_ERR_HIP, c->why);
+        }
+    *out = (c->gave_up && *c->gave_up) ? 1u : 0u;
     return RT_OK;
 }
+
+const uint32_t* chain_abort_word(const Chain* c) { return c ? c->abort : nullptr; }
 
 uint64_t chain_packets(const Chain* c) { return c ? c->packets : 0; }
 

@@ -43,18 +43,27 @@ struct TraceParams;
 // k), end; it is ordered after the work issued on `stream` before begin, and `stream`'s
 // later work after it.  chain_create never fails softly: chain_ok tells whether the
 // machine offers what the chain needs (why: the reason if not), a hard error is returned.
+// Every wait is bounded: a segment whose go wait gives up drops its frames (the chain
+// kernels check the abort word before storing), a queue error or a segment that does not
+// complete within the bound marks the chain failed (chain_failed), and the context then
+// runs HIP launches.
 namespace rtc {
 struct Chain;
 constexpr uint32_t kMaxSegmentPackets = 1024;
 Chain* chain_create(int device, rt_status* status);
-void chain_destroy(Chain* c);
+// RT_ERR_HIP (and the resources left in place) if a segment did not complete in time
+rt_status chain_destroy(Chain* c);
 bool chain_ok(const Chain* c, const char** why);
+// whether a go wait gave up or a queue reported an error (no synchronisation)
+bool chain_failed(Chain* c);
 // the queues of `parts` parts exist (created now if not); false if one cannot be created
 bool chain_queues(Chain* c, uint32_t parts);
 rt_status chain_begin(Chain* c, hipStream_t stream, uint32_t parts);
 rt_status chain_frame(Chain* c, const rtk::TraceParams& p, int kernel, uint32_t part);
 rt_status chain_end(Chain* c, hipStream_t stream);
-// go waits that gave up (the segment ran before the caller's stream reached it); waits for
+// drops an open segment (nothing of it has been submitted yet)
+void chain_abort(Chain* c);
+// 1 if a go wait gave up (its segment's frames were dropped), else 0; waits (bounded) for
 // every segment in flight
 rt_status chain_errors(Chain* c, uint32_t* out);
 uint64_t chain_packets(const Chain* c);

@@ -42,8 +42,9 @@ struct TraceParams {
     float4* out;
     // store_each (rt_update_frames): frame f of the launch stores its image to out for
     // even f and to out2 (the input buffer) for odd f — the ping-pong of chained `update`
-    // dispatches (lib.rs:366-374), with the accumulator kept in registers.  Only the last
-    // two frames' images survive the launch, so only they are written.
+    // dispatches (lib.rs:366-374), with the accumulator kept in registers.  1: only the last
+    // two frames' images survive the launch, so only they are written; 2: every frame's
+    // image is written (rt_set_frame_images EVERY).
     float4* out2;
     uint32_t store_each;
     const float4* geom;  // per sphere: (cx, cy, cz, r*r) — the scan's 16-B record
@@ -204,8 +205,8 @@ constexpr int kChainPix1 = 0, kChainPix1Reset = 1, kChainPix = 2, kChainPixReset
 constexpr uint32_t kHiddenArgsBytes = 256;   // code object v5 hidden arguments
 hipError_t chain_load_kernels();
 const char* chain_kernel_symbol(int which);
-uint32_t chain_args(const TraceParams& p, int kernel, unsigned char* out, uint32_t cap,
-                    uint32_t grid[2], uint32_t* group_threads, int* which);
+uint32_t chain_args(const TraceParams& p, int kernel, const uint32_t* abort, unsigned char* out,
+                    uint32_t cap, uint32_t grid[2], uint32_t* group_threads, int* which);
 hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t width,
                                uint32_t height, uint32_t nranks, uint32_t max_local_rows,
                                hipStream_t stream);

@@ -1109,8 +1109,10 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
         // buffer; the next frame would read it back (u32(f32(n)), wgsl:341) — here the
         // registers already hold it.  Only the last two frames' images survive the launch
         // (each buffer keeps the last frame written to it, and nothing reads a tile's
-        // pixels during the launch but its own wave), so only they are stored.
-        if (kStoreEach<kScan> && p.store_each && f + 2u >= p.frames && tc.valid)
+        // pixels during the launch but its own wave), so only they are stored — or every
+        // frame's (store_each 2, rt_set_frame_images EVERY).
+        if (kStoreEach<kScan> && p.store_each && (p.store_each == 2u || f + 2u >= p.frames) &&
+            tc.valid)
             ((f & 1u) ? p.out2 : p.out)[tc.idx] = make_float4(c.x, c.y, c.z, (float)n);
         n = f2u((float)n);
     }
@@ -1181,9 +1183,9 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
 #endif
                     na = nb + 1u;
                 }
-                if (fj + 2u >= p.frames && tc.valid)              // wgsl:362-363 (the
-                    ((fj & 1u) ? p.out2 : p.out)[tc.idx] =        // images that survive)
-                        make_float4(c.x, c.y, c.z, (float)na);
+                // wgsl:362-363: the images that survive (or every frame's, store_each 2)
+                if ((p.store_each == 2u || fj + 2u >= p.frames) && tc.valid)
+                    ((fj & 1u) ? p.out2 : p.out)[tc.idx] = make_float4(c.x, c.y, c.z, (float)na);
             }
         }
     }
@@ -1433,6 +1435,9 @@ struct SingleParams {
     // the launch's workgroups per row (rt_chain_kernel reads it here instead of the hidden
     // kernel arguments: its packets are written by rt_chain.cpp)
     uint32_t grid_x;
+    // rt_chain_kernel only: non-zero once a segment's go wait gave up — the frame's image
+    // stores are dropped (rt_chain.cpp; rt_single_kernel ignores it)
+    const uint32_t* abort;
 };
 
 // Tiles per wave of the two instances: kTraceSingle (whole-image launches) and
@@ -1766,6 +1771,14 @@ __device__ __forceinline__ void single_body(
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t tiles_x = (a_width + 7u) >> 3;
+    // frame chains: a segment whose go wait gave up drops its image stores (the frames must
+    // not run before the caller's stream reached them; rt_chain_go_kernel)
+    // (a system-scope load: no cache between it and the go kernel's store; waited for only
+    // at the stores)
+    const uint32_t aborted =
+        kChain ? __builtin_amdgcn_readfirstlane(
+                     __hip_atomic_load(p.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+               : 0u;
     // workgroups by decreasing candidate-list load (wg_order, launch_wg_order): the
     // costliest are dispatched first and the cheap ones fill the tail
     uint32_t gx = blockIdx.x, lband = (p.lbands & 0xFFFFu) + blockIdx.y * (p.lbands >> 16);
@@ -2000,8 +2013,9 @@ __device__ __forceinline__ void single_body(
             // RT_SINGLE_MASKS: no branch — a pixel past the image edge stores to an offset
             // past the band's buffer record, which the buffer unit drops
             const uint32_t off = ((lane >> 3) * a_width + tc[s].x) * 16u;
-            __builtin_amdgcn_raw_buffer_store_b128(
-                v, rsrc, (int)((RT_SINGLE_MASKS && !tc[s].valid) ? 0x7FFFFFF0u : off), 0, 16);
+            const bool drop = (RT_SINGLE_MASKS && !tc[s].valid) || (kChain && aborted != 0u);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, (int)(drop ? 0x7FFFFFF0u : off), 0,
+                                                   16);
         }
 #else
 #pragma unroll
@@ -2048,30 +2062,36 @@ __global__ __launch_bounds__(64 * kSingleWg, RT_SINGLE_MIN_WAVES) void rt_chain_
     const uint32_t* __restrict__ a_order, const SingleParams p) {
     single_body<kPix, true, true>(a_cand, a_hx, a_in, a_width, a_height, a_bands, a_order, p);
 }
-// 10 s at s_memrealtime's 100 MHz: the caller's stream work queued ahead of a chain
-constexpr uint64_t kChainGoTicks = 1000000000ull;
 // A chain's first packet: wait until the caller's stream has reached the chain (its
-// hipStreamWriteValue32 of `want` into *go, signal memory).  Bounded (s_memrealtime, 100
-// MHz): a wait that gives up counts in *err and the call reports an error.
+// hipStreamWriteValue32 of `want` into *go, signal memory).  Bounded by `ticks` of
+// s_memrealtime (100 MHz; rt_chain.cpp, default 10 s): a wait that gives up sets *abort
+// (device memory: every later chain frame drops its image stores, so no frame runs before
+// the caller's stream has reached it) and *gave_up (coherent host memory: the host fails the
+// chain on its next call, rt_abi.cpp, and runs HIP launches from then on).  Vector stores.
 __global__ __launch_bounds__(64) void rt_chain_go_kernel(const uint32_t* go, uint32_t want,
-                                                         uint32_t* err) {
+                                                         uint32_t* abort, uint32_t* gave_up,
+                                                         uint64_t ticks) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (true) {
         const uint32_t v = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
         if ((int32_t)(v - want) >= 0) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kChainGoTicks) {
-            if (threadIdx.x == 0u) atomicAdd(err, 1u);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+            if (threadIdx.x == 0u) {
+                __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(gave_up, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             break;
         }
         __builtin_amdgcn_s_sleep(2);
     }
 }
 // A chain's last packet (barrier bit: after every frame): the caller's stream, waiting in
-// hipStreamWaitValue32 for `value`, continues.
+// hipStreamWaitValue32 for `value`, continues.  A release store at system scope: the frames'
+// stores are written back before the stream (or a copy engine, or RCCL over xGMI) reads on.
 __global__ __launch_bounds__(64) void rt_chain_done_kernel(uint32_t* done, uint32_t value) {
     if (threadIdx.x == 0u)
-        __hip_atomic_store(done, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(done, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---- Bounce paths with workgroup-wide compaction (kTraceBounce) -----------------------
@@ -2391,8 +2411,10 @@ rt_bounce_kernel(const TraceParams p) {
                 }
                 // the images of the launch's last two frames survive (wgsl:362-363): frame
                 // fj's image belongs to out for even fj, out2 (the input buffer) for odd fj
-                // (store_each); otherwise only the last frame's, to out
-                if (valid && (fj + 1u == p.frames || (p.store_each && fj + 2u == p.frames))) {
+                // (store_each; 2: every frame's image is stored); otherwise only the last
+                // frame's, to out
+                if (valid && (fj + 1u == p.frames ||
+                              (p.store_each && (p.store_each == 2u || fj + 2u == p.frames)))) {
                     float4* dst = (p.store_each && (fj & 1u)) ? p.out2 : p.out;
                     dst[tc.idx] = make_float4(c.x, c.y, c.z, (float)(n < spp ? n + 1u : n));
                 }
@@ -3009,13 +3031,14 @@ const char* chain_kernel_symbol(int which) {
 // chain kernels read none of them — the workgroups per row come in SingleParams::grid_x).
 // Returns the bytes written (0: the part has no workgroup), the grid in workgroups and the
 // chain kernel (kChain*).
-uint32_t chain_args(const TraceParams& p, int kernel, unsigned char* out, uint32_t cap,
-                    uint32_t grid[2], uint32_t* group_threads, int* which) {
+uint32_t chain_args(const TraceParams& p, int kernel, const uint32_t* abort, unsigned char* out,
+                    uint32_t cap, uint32_t grid[2], uint32_t* group_threads, int* which) {
     SingleArgs args;
     dim3 g;
     const bool one = kernel == kTraceSingleOne;
     const bool any = one ? single_args<1>(p, args, g) : single_args<(int)kSinglePix>(p, args, g);
     if (!any) return 0;
+    args.q.abort = abort;
     const uint32_t hb = (uint32_t)((sizeof(args) + 7u) & ~(size_t)7u);
     const uint32_t total = hb + kHiddenArgsBytes;
     if (total > cap) return 0;

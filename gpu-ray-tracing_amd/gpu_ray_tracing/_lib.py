@@ -121,6 +121,7 @@ _SIGS = {
     "rt_set_tile_order": (ctypes.c_int, [P, ctypes.c_int]),
     "rt_set_update_queues": (ctypes.c_int, [P, U32]),
     "rt_set_update_submit": (ctypes.c_int, [P, ctypes.c_int]),
+    "rt_set_frame_images": (ctypes.c_int, [P, ctypes.c_int]),
     "rt_update_submit_status": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(U32),
                                                ctypes.POINTER(ctypes.c_uint64)]),
     "rt_last_launch_info": (ctypes.c_int, [P, P]),

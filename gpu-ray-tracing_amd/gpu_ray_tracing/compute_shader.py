@@ -74,6 +74,13 @@ class ComputeShaderPipeline:
         _lib.call("rt_set_frame_pairs", self._ctx,
                   {"auto": 0, "off": 1, "on": 2, "quad": 3}[mode])
 
+    def set_frame_images(self, mode: str) -> None:
+        """rt_set_frame_images: the images a fused multi-frame launch writes — "last_two"
+        (default: the two that survive the call) or "every" (every frame's image to the
+        ping-pong buffer its chained update writes, as the reference's dispatches do);
+        identical pixels."""
+        _lib.call("rt_set_frame_images", self._ctx, {"last_two": 0, "every": 1}[mode])
+
     def set_tile_order(self, mode: str) -> None:
         """rt_set_tile_order: "auto" (costliest tiles first, from the first launch's
         per-tile durations) or "off" (raster order)."""
@@ -85,10 +92,10 @@ class ComputeShaderPipeline:
         _lib.call("rt_set_update_queues", self._ctx, int(queues))
 
     def set_update_submit(self, mode: str) -> None:
-        """rt_set_update_submit: how update_frames submits one-frame updates — "auto" (AQL
-        packets for launches of 6 000 to 11 999 tiles, HIP launches otherwise), "hip" or
-        "aql" (AQL packets on the context's own HSA queues, an error if unavailable);
-        identical pixels."""
+        """rt_set_update_submit: how update_frames submits one-frame updates — "auto" (HIP
+        launches; AQL is opt-in), "hip" or "aql" (AQL packets on the context's own HSA
+        queues, an error if unavailable; after a failed AQL segment, reported once as an
+        error, the context runs HIP launches); identical pixels."""
         _lib.call("rt_set_update_submit", self._ctx, {"auto": 0, "hip": 1, "aql": 2}[mode])
 
     def submit_status(self) -> dict:

@@ -158,7 +158,7 @@ typedef struct rt_ctx rt_ctx;
 
 /* Version / introspection ------------------------------------------------------------ */
 RT_API uint32_t rt_abi_version(void); /* RT_ABI_VERSION */
-#define RT_ABI_VERSION 3u
+#define RT_ABI_VERSION 4u
 /* Text of the last error on this thread (never NULL). */
 RT_API const char* rt_last_error(void);
 /* Trace-kernel instances (rt_launch_info.kernel) and their names as rocprofv3 lists them
@@ -276,6 +276,22 @@ RT_API rt_status rt_render(rt_ctx* ctx, const float* in_rgba, float* out_rgba, u
  * `update` dispatch per frame, exactly the reference's dispatch structure, n = up to n (at
  * most 128).  The cap applies to the camera-ray-only and the bounce launches. */
 RT_API rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launch);
+/* Images of fused multi-frame launches (rt_set_frames_per_launch above 1).  The reference
+ * writes every frame's image to the texture its dispatch binds as output (lib.rs:218-227,
+ * 366-374; wgsl:362-363).
+ *   RT_FRAME_IMAGES_LAST_TWO  (default) a launch writes the images of its last two frames
+ *                             only: each earlier frame's image would be overwritten two
+ *                             frames later, unread, so both buffers end up the same.
+ *   RT_FRAME_IMAGES_EVERY     every frame's image is written to the buffer its chained
+ *                             update writes (frame f of a call: image_b for even f, image_a
+ *                             for odd f) — the reference's per-frame memory traffic, with
+ *                             only the launch boundary between the frames removed.  Used for
+ *                             the per-frame steps of small rank shares (bench.py, DESIGN.md
+ *                             §6), where one launch per frame is bound by the launch itself.
+ * The camera-ray-only and the bounce instances; pixel results are identical. */
+#define RT_FRAME_IMAGES_LAST_TWO 0
+#define RT_FRAME_IMAGES_EVERY 1
+RT_API rt_status rt_set_frame_images(rt_ctx* ctx, int mode);
 /* rt_update_frames at max_depth <= 1 traces with several waves per 8x8 tile, each taking
  * a different frame of each group of frames (the others hand their colours to wave 0,
  * which accumulates every frame in order: the same bits), whenever every pixel
@@ -327,19 +343,25 @@ RT_API rt_status rt_set_update_queues(rt_ctx* ctx, uint32_t queues);
  *                   shares (a 4-rank K3 share 6.76 against 7.54-7.68 µs), slower on small
  *                   ones (an 8-rank share 5.8 against 5.0); four HSA queues beside HIP's are
  *                   oversubscribed.
- *   RT_SUBMIT_AUTO  (default) AQL for launches of 6 000 to 11 999 tiles when the machine
- *                   offers it (HSA queues, host-visible VRAM or host memory for the
- *                   arguments, the code object's chain kernels), else HIP.
+ *   RT_SUBMIT_AUTO  (default) HIP launches: AQL submission is opt-in (it needs HSA queues,
+ *                   host-visible VRAM or host memory for the arguments and the code object's
+ *                   chain kernels, and has no multi-GPU record yet).
  * Parts under AQL (rt_set_update_queues 0): 2 for launches of 2 000 tiles or more, else 1.
+ * Every wait of the AQL path is bounded: a segment whose caller's stream has not reached it
+ * after RT_CHAIN_GO_MS milliseconds (environment, default 10 000) drops its frames instead
+ * of running them early; that, an HSA queue error or a segment that does not complete in
+ * time is returned as RT_ERR_HIP by the context's next call (rt_update_frames, rt_destroy,
+ * rt_update_submit_status), and the context runs HIP launches from then on.
  * Pixel results are identical in every mode. */
 #define RT_SUBMIT_AUTO 0
 #define RT_SUBMIT_HIP 1
 #define RT_SUBMIT_AQL 2
 RT_API rt_status rt_set_update_submit(rt_ctx* ctx, int mode);
 /* Whether AQL submission is available on the context's device (*aql_available; if not,
- * rt_last_error() says why), the go waits that gave up so far (*go_give_ups: a chain whose
- * caller's stream had not reached it after 10 s ran early; 0 in a correct run) and the AQL
- * packets submitted so far.  Synchronous: waits for the context's AQL work in flight. */
+ * rt_last_error() says why), whether a go wait gave up (*go_give_ups, 0 or 1: a segment
+ * whose caller's stream had not reached it within the bound; its frames were dropped; 0 in
+ * a correct run) and the AQL packets submitted so far.  Synchronous: waits (bounded) for
+ * the context's AQL work in flight.  Creates no HSA queue. */
 RT_API rt_status rt_update_submit_status(rt_ctx* ctx, int* aql_available, uint32_t* go_give_ups,
                                          uint64_t* packets);
 /* Bounce paths (max_depth >= 2): RT_PATHS_PER_WAVE keeps every path in the wave of its

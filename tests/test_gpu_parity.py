@@ -198,24 +198,27 @@ def test_bench_dispatch_chain_matches_fixture(rt, cfg, single, submit):
 @pytest.mark.parametrize("submit", ["auto", "aql"])
 def test_update_queues_match_one_launch(rt, single, order, submit):
     """rt_set_update_queues: one-frame updates as 2-4 concurrent parts on their own streams
-    or HSA queues (rt_set_update_submit; each part every queues-th workgroup of the cost order, or every queues-th band when
-    the order is off) leave both ping-pong images bit-identical to one launch per update —
-    whole image and a rank share, across the reset frame, the order's first build and a
-    second call — and match the oracle's sampled pixels (tests/golden/bench_k3.npz)."""
+    or HSA queues (rt_set_update_submit; each part every queues-th workgroup of the cost
+    order, or every queues-th band when the order is off) leave both ping-pong images
+    bit-identical to one launch per update — whole image and a rank share, across the reset
+    frame, the order's first build and a second call — and match the oracle's sampled pixels
+    (tests/golden/bench_k3.npz).  Every part count runs on a fresh context, so the cost
+    order is first built inside a call that already has parts in flight (frame 1 in raster
+    bands, frame 2 in the new order: the parts are joined before the order is built)."""
     g = load_golden("bench_k3.npz")
     w, h = int(g["width"]), int(g["height"])
     cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
     cam_t = cam.with_fields(camera_has_moved=0.0)
-    p = rt.ComputeShaderPipeline(0)
-    p.set_frames_per_launch(1)
-    p.set_single_kernel(single)
-    p.set_tile_order(order)
-    p.set_update_submit(submit)
-    try:
-        for rank, nranks in ((0, 1), (3, 8)):
-            rows = rt.stripe_local_rows(h, rank, nranks)
-            ref = None
-            for q in (1, 2, 3, 4):
+    for rank, nranks in ((0, 1), (3, 8)):
+        rows = rt.stripe_local_rows(h, rank, nranks)
+        ref = None
+        for q in (1, 2, 3, 4):
+            p = rt.ComputeShaderPipeline(0)
+            try:
+                p.set_frames_per_launch(1)
+                p.set_single_kernel(single)
+                p.set_tile_order(order)
+                p.set_update_submit(submit)
                 p.set_update_queues(q)
                 a, b = p.new_image(w, rows), p.new_image(w, rows)
                 n0 = p.update_frames(a, b, w, h, cam, sc, g["seeds"][:5], rank, nranks)
@@ -225,16 +228,16 @@ def test_update_queues_match_one_launch(rt, single, order, submit):
                 info = p.last_launch_info()
                 assert info["queues"] == q and info["launches"] == 20 * q, (q, info)
                 imgs = (host(b if newest == 1 else a), host(a if newest == 1 else b))
-                if ref is None:
-                    ref = imgs
-                    if nranks == 1:
-                        k = list(g["frame_counts"]).index(25)
-                        assert_same(imgs[0][g["py"], g["px"]], g["pixels"][k])
-                else:
-                    for x, y in zip(imgs, ref):
-                        assert_same(x, y)
-    finally:
-        p.close()
+            finally:
+                p.close()
+            if ref is None:
+                ref = imgs
+                if nranks == 1:
+                    k = list(g["frame_counts"]).index(25)
+                    assert_same(imgs[0][g["py"], g["px"]], g["pixels"][k])
+            else:
+                for x, y in zip(imgs, ref):
+                    assert_same(x, y)
 
 
 @pytest.mark.parametrize("single", ["auto", "one"])
@@ -245,7 +248,7 @@ def test_update_submit_aql_matches_hip(rt, single):
     frame, the workgroup order's first build and a second call; the first call starts on an
     idle stream (no go packet), the second is issued while the stream still waits for the
     first (the go packet path) — and match the oracle's sampled pixels; no go wait gave up.
-    AUTO picks AQL for the 4-rank share (6 000 to 11 999 tiles) and HIP for the others."""
+    AUTO submits HIP launches at every size (AQL is opt-in since round 4)."""
     g = load_golden("bench_k3.npz")
     w, h = int(g["width"]), int(g["height"])
     cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
@@ -258,7 +261,6 @@ def test_update_submit_aql_matches_hip(rt, single):
     try:
         for rank, nranks in ((0, 1), (5, 8), (1, 4)):
             rows = rt.stripe_local_rows(h, rank, nranks)
-            tiles = ((w + 7) // 8) * ((rows + 7) // 8)
             ref = None
             for mode, q in (("hip", 1), ("aql", 1), ("aql", 2), ("aql", 3), ("aql", 4),
                             ("aql", 0), ("auto", 0)):
@@ -271,7 +273,7 @@ def test_update_submit_aql_matches_hip(rt, single):
                     a, b = b, a
                 newest = p.update_frames(a, b, w, h, cam_t, sc, g["seeds"][5:25], rank, nranks)
                 info = p.last_launch_info()
-                want = mode if mode != "auto" else ("aql" if 6000 <= tiles < 12000 else "hip")
+                want = mode if mode != "auto" else "hip"
                 assert info["submit"] == want and info["frames"] == 20, (mode, q, info)
                 if q:
                     assert info["queues"] == q, (mode, q, info)
@@ -287,6 +289,92 @@ def test_update_submit_aql_matches_hip(rt, single):
         st = p.submit_status()
         assert st["go_give_ups"] == 0 and st["packets"] > 0, st
     finally:
+        p.close()
+
+
+class _HipStreamGate:
+    """Holds a HIP stream at a hipStreamWaitValue32 on a signal-memory word until release()
+    (hipStreamWriteValue32 from a second stream): the stream is busy, and whatever is queued
+    behind the wait cannot start — a caller's stream that never reaches an AQL segment."""
+
+    def __init__(self, stream):
+        import ctypes
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.word = ctypes.c_void_p()
+        assert self.hip.hipExtMallocWithFlags(ctypes.byref(self.word), ctypes.c_size_t(8),
+                                              ctypes.c_uint(2)) == 0   # hipMallocSignalMemory
+        assert self.hip.hipMemset(self.word, 0, ctypes.c_size_t(8)) == 0
+        assert self.hip.hipDeviceSynchronize() == 0
+        self.other = torch.cuda.Stream()
+        self.ctypes = ctypes
+        # wait until *word >= 1 (hipStreamWaitValueGte = 0), full mask
+        assert self.hip.hipStreamWaitValue32(ctypes.c_void_p(stream.cuda_stream), self.word,
+                                             ctypes.c_uint32(1), ctypes.c_uint(0),
+                                             ctypes.c_uint32(0xFFFFFFFF)) == 0
+
+    def release(self):
+        c = self.ctypes
+        assert self.hip.hipStreamWriteValue32(c.c_void_p(self.other.cuda_stream), self.word,
+                                              c.c_uint32(1), c.c_uint(0)) == 0
+
+    def close(self):
+        torch.cuda.synchronize()
+        self.hip.hipFree(self.word)
+
+
+def test_aql_go_wait_gives_up_and_falls_back(rt, monkeypatch):
+    """The AQL path's bounded go wait (rt_chain.cpp): a segment submitted while the caller's
+    stream is held (a hipStreamWaitValue32 nobody satisfies within RT_CHAIN_GO_MS = 300 ms)
+    gives up without running its frames early (their stores are dropped: the images keep
+    what they held), the context's next call returns RT_ERR_HIP with the reason, and the calls
+    after it run on HIP launches — bit-exact against tests/golden/bench_k3.npz from a reset."""
+    import time
+    monkeypatch.setenv("RT_CHAIN_GO_MS", "300")
+    g = load_golden("bench_k3.npz")
+    w, h = int(g["width"]), int(g["height"])
+    cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
+    cam_t = cam.with_fields(camera_has_moved=0.0)
+    p = rt.ComputeShaderPipeline(0)
+    gate = None
+    try:
+        st = p.submit_status()
+        assert st["aql_available"], st["why"]
+        p.set_frames_per_launch(1)
+        p.set_update_submit("aql")
+        a, b = p.new_image(w, h), p.new_image(w, h)
+        p.update_frames(a, b, w, h, cam, sc, g["seeds"][:3])      # a working segment
+        assert p.last_launch_info()["submit"] == "aql"
+        torch.cuda.synchronize()
+        before = (host(a).copy(), host(b).copy())
+        stream = torch.cuda.current_stream()
+        gate = _HipStreamGate(stream)                              # the stream is held
+        p.update_frames(a, b, w, h, cam_t, sc, g["seeds"][3:7])   # go wait: never satisfied
+        assert p.last_launch_info()["submit"] == "aql"
+        time.sleep(1.5)                                            # > the 300-ms bound
+        gate.release()
+        torch.cuda.synchronize()
+        # the segment's frames did not run: both images hold what they held before
+        after = (host(a), host(b))
+        for x, y in zip(after, before):
+            assert_same(x, y)
+        with pytest.raises(rt.RtError, match="go wait gave up"):
+            p.update_frames(a, b, w, h, cam_t, sc, g["seeds"][3:7])
+        st = p.submit_status()
+        assert not st["aql_available"] and st["go_give_ups"] == 1, st
+        # from now on HIP launches: the driver's 5 + 20 frames from a reset, bit-exact
+        n0 = p.update_frames(a, b, w, h, cam, sc, g["seeds"][:5])
+        assert p.last_launch_info()["submit"] == "hip"
+        if n0 == 1:
+            a, b = b, a
+        newest = p.update_frames(a, b, w, h, cam_t, sc, g["seeds"][5:25])
+        assert p.last_launch_info()["submit"] == "hip"
+        img = host(b if newest == 1 else a)
+        k = list(g["frame_counts"]).index(25)
+        assert_same(img[g["py"], g["px"]], g["pixels"][k])
+    finally:
+        if gate is not None:
+            gate.release()
+            gate.close()
         p.close()
 
 
@@ -647,9 +735,12 @@ def test_candidate_list_overflow_falls_back(rt, depth):
                                                   (5, 8, 500, 4), (9, 2, 3, 3), (14, 1, 500, 4),
                                                   (11, 1, 6, 3)])
 @pytest.mark.parametrize("pairs", ["off", "on", "quad"])
-def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, spp, per, pairs):
-    """rt_update_frames (frames fused per launch, every frame's image stored to the
-    ping-pong buffers; or one dispatch per frame) leaves BOTH buffers exactly as chained
+@pytest.mark.parametrize("images", ["last_two", "every"])
+def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, spp, per, pairs,
+                                              images):
+    """rt_update_frames (frames fused per launch, the last two or every frame's image stored
+    to the ping-pong buffers, rt_set_frame_images; or one dispatch per frame) leaves BOTH
+    buffers exactly as chained
     rt_update calls do: the newest frame and the one before, for the whole image and for
     stripe ranks (compact local buffers), across launch boundaries and the spp cap, with
     and without frame groups (several waves per tile on alternate frames); the depth-1
@@ -671,6 +762,7 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, s
     got_prev = np.zeros((h, w, 4), np.float32)
     pipe.set_frames_per_launch(per)
     pipe.set_frame_pairs(pairs)
+    pipe.set_frame_images(images)
     try:
         for r in range(nranks):
             a, b = pipe.new_image(w, rows0), pipe.new_image(w, rows0)
@@ -685,6 +777,7 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, s
     finally:
         pipe.set_frames_per_launch(0)
         pipe.set_frame_pairs("auto")
+        pipe.set_frame_images("last_two")
     assert (newest == 0) == (frames % 2 == 0)
     assert_same(got_new, want_new)
     if frames >= 2:
@@ -694,7 +787,8 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, s
 BOUNCE_PATH_KERNEL = {"per_wave": 0, "compact": 1, "pair": 2, "auto": 0}
 
 
-def _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks, fpl):
+def _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks, fpl,
+                           images="last_two"):
     sc = {"n120": rt.synthetic_scene(120), "default": rt.create_default_spheres(seed=3),
           "three": rt.three_spheres()}[scene]
     seeds = rt.frame_seeds(33, frames)
@@ -706,6 +800,7 @@ def _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks
                                         yy.ravel(), cam.blob, sc.spheres, seeds[:frames - 1])
     p = rt.ComputeShaderPipeline(0)
     p.set_path_compaction(paths)
+    p.set_frame_images(images)
     if fpl:
         p.set_frames_per_launch(fpl)
     rows0 = rt.stripe_local_rows(h, 0, nranks)
@@ -747,12 +842,14 @@ def test_bounce_launches_match_oracle(rt, oracle, paths, w, h, depth, frames, sc
 @pytest.mark.parametrize("paths", ["per_wave", "compact", "pair"])
 @pytest.mark.parametrize("w,h,depth,frames,scene,nranks", [
     (56, 40, 2, 5, "n120", 1), (50, 37, 8, 6, "default", 3), (72, 48, 5, 4, "three", 2)])
-def test_bounce_launches_in_tile_order(rt, oracle, paths, w, h, depth, frames, scene, nranks):
+@pytest.mark.parametrize("images", ["last_two", "every"])
+def test_bounce_launches_in_tile_order(rt, oracle, paths, w, h, depth, frames, scene, nranks,
+                                       images):
     """Two frames per launch (rt_set_frames_per_launch(2)): the first launch records the
     per-tile (compact mode: per-workgroup) costs, every later launch runs the measured
     cost order (tile_order) — both ping-pong buffers still equal the oracle's chain, in
-    every path mode."""
-    _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks, 2)
+    every path mode, with the last two or every frame's image stored."""
+    _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks, 2, images)
 
 
 def test_accumulator_written_outside_the_library(rt, oracle, pipe):

@@ -1,7 +1,7 @@
 """Per-rank frame time of the stripe partition on ONE GPU (diagnostic, not the bench): times
 rank 0's share of a W x H progressive render for world sizes 1, 2, 4, 8, i.e. what each rank
 of `bench.py --gpus N` computes per step, to predict strong-scaling efficiency without an
-8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] [RT_QUEUES=q] [RT_SUBMIT=auto|hip|aql] [RT_REPS=r] [RT_WARM_MS=50] [RT_PATHS=auto|per_wave|pair|compact] python tools/rank_sim.py [K3|K2|K5] [steps]"""
+8-GPU node.  usage: [RT_FRAME_PAIRS=auto|off|on] [RT_TILE_ORDER=auto|off] [RT_FPL=n] [RT_IMAGES=last_two|every] [RT_QUEUES=q] [RT_SUBMIT=auto|hip|aql] [RT_REPS=r] [RT_WARM_MS=50] [RT_PATHS=auto|per_wave|pair|compact] python tools/rank_sim.py [K3|K2|K5] [steps]"""
 import json
 import os
 import sys
@@ -32,6 +32,8 @@ def main(cfg="K3", steps=50):
     # RT_FPL=1: one launch per frame (the reference's dispatch structure)
     pipe.set_frames_per_launch(int(os.environ.get("RT_FPL", "0")))
     pipe.set_path_compaction(os.environ.get("RT_PATHS", "auto"))   # bounce launches
+    if hasattr(rt._lib.lib(), "rt_set_frame_images"):
+        pipe.set_frame_images(os.environ.get("RT_IMAGES", "last_two"))
     if hasattr(rt._lib.lib(), "rt_set_single_kernel"):
         pipe.set_single_kernel(os.environ.get("RT_SINGLE", "auto"))
     if hasattr(rt._lib.lib(), "rt_set_tile_order"):
@@ -76,6 +78,8 @@ def main(cfg="K3", steps=50):
                           "host_issue_us_per_step": round(host_us, 2),
                           "runs_us": [round(x, 2) for x in runs],
                           "queues": pipe.last_launch_info().get("queues"),
+                          "kernel": pipe.last_launch_info().get("kernel_name"),
+                          "frames_per_launch": pipe.last_launch_info().get("max_frames_per_launch"),
                           "submit": pipe.last_launch_info().get("submit")}), flush=True)
     pipe.close()
 
