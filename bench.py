@@ -201,6 +201,15 @@ def cpu_baseline(cam, spheres, w, h, seconds):
     for _ in range(frames):
         O.update_parallel(img, cam.blob, spheres.spheres, T)
     dt = time.perf_counter() - t0
+    # every host core the process may use (SURVEY §8d5 "all nproc cores"): ~seconds/4 of
+    # whole frames on affinity-many threads (the reported value stays the per-GPU share)
+    A = host_cpus()[1]
+    fa = max(1, int(round(seconds / 4 / (w * h / (single * 1e6 * A)))))
+    band = max(1, min(8, h // (2 * A)))        # at least two bands per thread
+    t0 = time.perf_counter()
+    for _ in range(fa):
+        O.update_parallel(img, cam.blob, spheres.spheres, A, band=band)
+    dta = time.perf_counter() - t0
     return {"value": round(w * h * frames / dt / 1e6, 3), "unit": "Mrays/s", "cores": T,
             "kind": "port",
             "sample": f"{frames} full {w}x{h} update(s) on {T} threads (8-row bands from a "
@@ -208,9 +217,13 @@ def cpu_baseline(cam, spheres, w, h, seconds):
                       f"max_depth {int(cam.max_depth)}",
             "single_thread": {"value": round(single, 3), "cores": 1,
                               "sample": f"{w}x{rows1} rows of one update"},
+            "all_cores": {"value": round(w * h * fa / dta / 1e6, 3), "cores": A,
+                          "sample": f"{fa} full {w}x{h} update(s) on {A} threads "
+                                    f"({band}-row bands from a queue), {dta:.1f} s"},
             "cpu_model": cpu_model(),
             "nproc": host_cpus()[0], "affinity_cpus": host_cpus()[1],
-            "cores_rule": "min(16, affinity): the per-GPU share of the box's host cores"}
+            "cores_rule": "value: min(16, affinity) threads, the per-GPU share of the box's host "
+                          "cores; all_cores: every core of the affinity set"}
 
 
 def load_pmc(config, kernel, frames_per_launch):

@@ -101,6 +101,10 @@ struct rt_ctx {
     // Images of fused multi-frame launches (rt_set_frame_images): the last two frames' only,
     // or every frame's (TraceParams::store_each 1 / 2)
     int frame_images = RT_FRAME_IMAGES_LAST_TWO;
+    // split bounce launches (TraceParams::split_col / split_cnt, plan_split)
+    float4* split_col = nullptr;
+    uint32_t* split_cnt = nullptr;
+    uint64_t split_col_bytes = 0, split_cnt_tiles = 0;
 };
 
 namespace {
@@ -632,6 +636,67 @@ rt_status plan_wg_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_
     return RT_OK;
 }
 
+// Split bounce launches (rt_kernels.hip kBounceSplit; RT_PATHS_SPLIT, or AUTO for small
+// launches): each tile's frames in S chunks traced by separate waves.  A share of a few
+// waves per SIMD in per-wave mode ends with SIMDs idle behind its costliest tiles' 64-frame
+// chains (an 8-rank K5 share's longest waves last 0.91-1.0 of the launch, 4.75
+// waves resident per SIMD on average); S times as many, S times shorter waves keep them
+// busy to the end.  S = 4 up to kSplit4MaxTiles tiles per launch, 2 up to kSplit2MaxTiles,
+// else 1 (per wave; RT_PATHS_SPLIT forces at least 2); never more chunks than frames.
+// RT_BOUNCE_SPLIT (environment, diagnostic) overrides S.
+#ifndef RT_SPLIT4_MAX_TILES
+#define RT_SPLIT4_MAX_TILES 20000
+#endif
+#ifndef RT_SPLIT2_MAX_TILES
+#define RT_SPLIT2_MAX_TILES 40000
+#endif
+constexpr uint64_t kSplit4MaxTiles = RT_SPLIT4_MAX_TILES, kSplit2MaxTiles = RT_SPLIT2_MAX_TILES;
+rt_status plan_split(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t stream) {
+    p.split = 1;
+    p.split_col = nullptr;
+    p.split_cnt = nullptr;
+    const int mode = ctx->path_compaction;
+    if (kernel != rtk::kTraceBounce || (mode != RT_PATHS_AUTO && mode != RT_PATHS_SPLIT))
+        return RT_OK;
+    const uint64_t tiles = (uint64_t)((p.width + 7u) >> 3) * p.local_bands;
+    uint32_t S = tiles <= kSplit4MaxTiles ? 4u : tiles <= kSplit2MaxTiles ? 2u : 1u;
+    if (mode == RT_PATHS_SPLIT) S = std::max(S, 2u);
+    if (const char* e = std::getenv("RT_BOUNCE_SPLIT")) S = (uint32_t)std::max(1L, std::atol(e));
+    S = std::min(S, p.frames);
+    if (S <= 1u || tiles == 0) {
+        p.compact = 0u;
+        return RT_OK;
+    }
+    const uint64_t bytes = tiles * p.frames * 1024ull;
+    if (bytes > ctx->split_col_bytes || tiles > ctx->split_cnt_tiles) {
+        hipError_t e = hipStreamSynchronize(stream);    // the old buffers may be in use
+        if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+        if (bytes > ctx->split_col_bytes) {
+            (void)hipFree(ctx->split_col);
+            ctx->split_col = nullptr;
+            ctx->split_col_bytes = 0;
+            e = hipMalloc(&ctx->split_col, bytes);
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc(split colours)");
+            ctx->split_col_bytes = bytes;
+        }
+        if (tiles > ctx->split_cnt_tiles) {
+            (void)hipFree(ctx->split_cnt);
+            ctx->split_cnt = nullptr;
+            ctx->split_cnt_tiles = 0;
+            e = hipMalloc(&ctx->split_cnt, tiles * sizeof(uint32_t));
+            // (zero once: every launch leaves the arrival counters at zero)
+            if (e == hipSuccess) e = hipMemsetAsync(ctx->split_cnt, 0, tiles * sizeof(uint32_t), stream);
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc(split counters)");
+            ctx->split_cnt_tiles = tiles;
+        }
+    }
+    p.compact = 3u;
+    p.split = S;
+    p.split_col = ctx->split_col;
+    p.split_cnt = ctx->split_cnt;
+    return RT_OK;
+}
+
 // After a launch that recorded tile costs.
 void finish_tile_order(rt_ctx* ctx, const rtk::TraceParams& p) {
     if (!p.tile_cost) return;
@@ -910,7 +975,9 @@ void note_launch(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t fr
     ctx->last.submit = aql ? RT_SUBMIT_AQL : RT_SUBMIT_HIP;
     ctx->last.frames += frames;
     ctx->last.max_frames_per_launch = std::max(ctx->last.max_frames_per_launch, frames);
-    ctx->last.kernel = kernel != rtk::kTraceBounce ? kernel : RT_KERNEL_BOUNCE + (int)p.compact;
+    ctx->last.kernel = kernel != rtk::kTraceBounce ? kernel
+                       : p.compact == 3u             ? RT_KERNEL_BOUNCE_SPLIT
+                                                     : RT_KERNEL_BOUNCE + (int)p.compact;
 }
 
 // A chain failure (a go wait that gave up, so a segment's frames were dropped; a queue
@@ -1012,6 +1079,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         const int kernel = single_or(ctx, p, trace_kernel_for(ctx, p));
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         if (rt_status s = plan_wg_order(ctx, p, kernel, stream)) return s;
+        if (rt_status s = plan_split(ctx, p, kernel, stream)) return s;
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         finish_tile_order(ctx, p);
@@ -1035,7 +1103,8 @@ const char* rt_kernel_name(int which) {
                                         "rt_trace_kernel<4>",      "rt_bounce_kernel<0>",
                                         "rt_bounce_kernel<1>",     "rt_bounce_kernel<2>",
                                         rtk::single_kernel_name(0),
-                                        rtk::single_kernel_name(1)};
+                                        rtk::single_kernel_name(1),
+                                        "rt_bounce_kernel<3>"};
     if (which >= 0 && which < (int)(sizeof(names) / sizeof(names[0]))) return names[which];
     return rtk::trace_kernel_name();
 }
@@ -1102,6 +1171,8 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->tile_order);
         (void)hipFree(ctx->d_grid);
         (void)hipFree(ctx->wg_buf);
+        (void)hipFree(ctx->split_col);
+        (void)hipFree(ctx->split_cnt);
         free_candidates(ctx);
         for (uint32_t k = 0; k + 1 < RT_MAX_UPDATE_QUEUES; ++k) {
             if (ctx->aux[k]) (void)hipStreamDestroy(ctx->aux[k]);
@@ -1142,7 +1213,7 @@ rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode) {
 rt_status rt_set_path_compaction(rt_ctx* ctx, int mode) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     if (mode != RT_PATHS_AUTO && mode != RT_PATHS_PER_WAVE && mode != RT_PATHS_COMPACT &&
-        mode != RT_PATHS_PAIR)
+        mode != RT_PATHS_PAIR && mode != RT_PATHS_SPLIT)
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown path-compaction mode");
     ctx->path_compaction = mode;
     return RT_OK;
@@ -1334,9 +1405,8 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         if (known) {
             n_last = fill_hint(p, p.reset_first ? 0u : n_in);
             // the frame before the last: what the other buffer holds when nf >= 2
-            rtk::TraceParams q = p;
-            q.frames = nf - 1;
-            n_prev = fill_hint(q, p.reset_first ? 0u : n_in);
+            n_prev = p.reset_first ? 0u : n_in;
+            for (uint32_t f = 0; f + 1u < nf; ++f) n_prev = next_count(n_prev, p.spp);
         } else {
             p.hint_frames = 0;
         }
@@ -1374,6 +1444,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         }
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         if (rt_status s = plan_wg_order(ctx, p, kernel, stream)) return s;
+        if (rt_status s = plan_split(ctx, p, kernel, stream)) return s;
         if (aql) {
             // frame f of part k is a packet on the chain's queue k, after part k's frame f - 1
             if (!fl.seg_open) {

@@ -106,8 +106,15 @@ struct TraceParams {
     // table (rt_kernels.hip disk_unit), computed on the host
     double disk_rcp[8];
     // bounce instance (kTraceBounce): compact live paths across the workgroup's waves
-    // after every bounce (1) or let each wave keep its own paths (0)
+    // after every bounce (1), let each wave keep its own paths (0), frame pairs (2), or
+    // split each tile's frames into `split` chunks traced by separate waves (3)
     uint32_t compact;
+    // compact == 3: chunks per tile, each chunk's per-frame colours in split_col (one 1-KB
+    // row of 64 float4 per tile and frame, [tile][frame][lane]), arrivals per tile in
+    // split_cnt (zero between launches: the last arriver resets it)
+    uint32_t split;
+    float4* split_col;
+    uint32_t* split_cnt;
     uint32_t hint_frames;  // 0 = no hint
     uint32_t hint_n[kHintFrames];
     // RN64(1 / (hint_n[f] + 1)): the accumulator's division by f32(n + 1) as one f64

@@ -2221,8 +2221,15 @@ __device__ __forceinline__ const kconst TraceParams* karg_bounce_params() {
 // barriers; kBounceCompact — four-wave workgroups exchanging paths through LDS (above);
 // kBouncePair — two waves per tile on alternate frames, wave 1 handing its colours to wave
 // 0 through LDS, which accumulates both in order (the frame groups of the camera-ray
-// instance, trace_pair): half as long a chain per wave, for small per-rank shares.
-constexpr int kBounceWave = 0, kBounceCompact = 1, kBouncePair = 2;
+// instance, trace_pair): half as long a chain per wave, for small per-rank shares;
+// kBounceSplit — one-wave workgroups, each tile's frames split into p.split consecutive
+// chunks traced by separate waves (units (tile, chunk), the costliest tiles' chunks first):
+// a chunk stores its frames' colours write-through, the wave whose arrival is the tile's
+// last accumulates all of them in frame order (wgsl:352-363) and stores the images.  Small
+// rank shares (a few waves per SIMD in per-wave mode) then run S times as many, S times
+// shorter waves, so the launch no longer ends with SIMDs idle behind the costliest tiles'
+// 64-frame chains.
+constexpr int kBounceWave = 0, kBounceCompact = 1, kBouncePair = 2, kBounceSplit = 3;
 template <int kMode>
 constexpr uint32_t bounce_waves() {
     return kMode == kBounceCompact ? kBounceWaves : kMode == kBouncePair ? 2u : 1u;
@@ -2233,14 +2240,24 @@ __global__ __launch_bounds__(64 * bounce_waves<kMode>(), RT_BOUNCE_MIN_WAVES) vo
 rt_bounce_kernel(const TraceParams p) {
     WAVE_TRACE(0);
     constexpr bool kCompact = kMode == kBounceCompact, kPair = kMode == kBouncePair;
+    constexpr bool kSplit = kMode == kBounceSplit;
     constexpr uint32_t kW = bounce_waves<kMode>();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = kW == 1u ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t me = threadIdx.x;                    // lane in the workgroup
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     uint32_t gx = blockIdx.x, lband = blockIdx.y;       // group of kW tiles
+    // kSplit: workgroup u = unit (tile slot u / S, chunk u % S); grid (tiles_x * S, bands)
+    const uint32_t S = kSplit ? p.split : 1u;
+    const uint32_t unit = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t chunk = kSplit ? unit % S : 0u;
+    if (kSplit) {
+        const uint32_t slot = unit / S;
+        gx = slot % tiles_x;
+        lband = slot / tiles_x;
+    }
     if (p.tile_order) {                                 // costliest groups first
-        const uint32_t pos = blockIdx.y * gridDim.x + blockIdx.x;
+        const uint32_t pos = kSplit ? unit / S : unit;
         const uint32_t t = __builtin_amdgcn_readfirstlane(p.tile_order[pos]);
         gx = t & 0xFFFFu;
         lband = t >> 16;
@@ -2260,7 +2277,8 @@ rt_bounce_kernel(const TraceParams p) {
     }
     constexpr uint32_t kTiles = kPair ? 1u : kW;        // tiles per workgroup
     const uint32_t group = lband * ((tiles_x + kTiles - 1u) / kTiles) + gx;
-    if (p.tile_cost && threadIdx.x == 0u)
+    // (kSplit: chunk 0's duration stands for its tile's: the chunks carry equal frames)
+    if (p.tile_cost && threadIdx.x == 0u && chunk == 0u)
         p.tile_cost[group] = (uint32_t)__builtin_amdgcn_s_memtime();
     if (p.lds_records || kW > 1u) __syncthreads();
     const uint32_t tile = lband * tiles_x + (wave_in ? tx : 0u);
@@ -2280,7 +2298,23 @@ rt_bounce_kernel(const TraceParams p) {
         n = f2u(acc.w);
     }
     constexpr uint32_t kStep = kPair ? 2u : 1u;               // frames per iteration
-    for (uint32_t f0 = 0; f0 < p.frames; f0 += kStep) {
+    // kSplit: this chunk's frames [f_lo, f_hi), and the pixel's count before f_lo (the
+    // count arithmetic of wgsl:345-362 over the frames before it, f32 round trip included)
+    uint32_t f_lo = 0u, f_hi = p.frames;
+    if (kSplit) {
+        const uint32_t cs = (p.frames + S - 1u) / S;
+        f_lo = min(chunk * cs, p.frames);
+        f_hi = min(f_lo + cs, p.frames);
+        for (uint32_t f = 0; f < f_lo; ++f) {
+            if (f == 0u && p.reset_first) n = 0u;
+            n = f2u((float)(n < spp ? n + 1u : n));
+        }
+    }
+    // (kSplit: this tile's colour rows, one 1-KB row per frame)
+    const __amdgpu_buffer_rsrc_t col_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        p.split_col + ((size_t)lband * tiles_x + (wave_in ? tx : 0u)) * p.frames * 64u, 0,
+        (int)(p.frames * 1024u), 0x00020000);
+    for (uint32_t f0 = f_lo; f0 < f_hi; f0 += kStep) {
         if (f0 == 0 && p.reset_first) {                           // wgsl:345-350
             c = mk(0.0f, 0.0f, 0.0f);
             n = 0u;
@@ -2393,6 +2427,16 @@ rt_bounce_kernel(const TraceParams p) {
             if (wave == 1u) s_pair_col[lane] = make_float4(res.x, res.y, res.z, 0.0f);
             __syncthreads();
         }
+        if (kSplit) {
+            // the frame's colour, write-through (sc1): the tile's last arriver reads it
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 v = {__float_as_uint(res.x), __float_as_uint(res.y),
+                             __float_as_uint(res.z), 0u};
+            __builtin_amdgcn_raw_buffer_store_b128(v, col_rsrc, (int)((f0 * 64u + lane) * 16u),
+                                                   0, 16);
+            n = f2u((float)(n < spp ? n + 1u : n));
+            continue;
+        }
         // accumulate this iteration's frames in order (pairs: wave 0 does both; wave 1 only
         // follows the count)
         for (uint32_t j = 0; j < kStep; ++j) {
@@ -2423,7 +2467,65 @@ rt_bounce_kernel(const TraceParams p) {
         }
         if (kCompact || kPair) __syncthreads();                   // LDS reused next frame
     }
-    if (p.tile_cost && threadIdx.x == 0u)
+    if (kSplit) {
+        // arrival: every colour of this chunk has left the CU (sc1 stores, drained), then one
+        // agent-scope add; the tile's last arriver (told by the add's value) reads the other
+        // chunks' colours with sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility,
+        // first row of the hand-off table) and accumulates every frame in order
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t* cnt = p.split_cnt + (size_t)lband * tiles_x + (wave_in ? tx : 0u);
+        uint32_t old = 0u;
+        if (lane == 0u) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        old = __builtin_amdgcn_readlane(old, 0);
+        if (old + 1u == S) {
+            if (lane == 0u)    // (the next launch starts after this one ends)
+                __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            c = mk(0.0f, 0.0f, 0.0f);
+            n = 0u;
+            if (!p.reset_first && valid) {
+                const float4 acc = p.in[tc.idx];
+                c = mk(acc.x, acc.y, acc.z);
+                n = f2u(acc.w);
+            }
+            // the colours in batches of kMergeBatch frames, all of a batch's loads in flight
+            // before its accumulation (one dependent load per frame made the merge as long as
+            // 64 load latencies)
+            constexpr uint32_t kMergeBatch = 8;
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            for (uint32_t f0 = 0; f0 < p.frames; f0 += kMergeBatch) {
+                u32x4 v[kMergeBatch];
+#pragma unroll
+                for (uint32_t j = 0; j < kMergeBatch; ++j)   // (rows past the last frame:
+                    v[j] = __builtin_amdgcn_raw_buffer_load_b128(   // dropped by the buffer)
+                        col_rsrc, (int)(((f0 + j) * 64u + lane) * 16u), 0, 16);
+#pragma unroll
+                for (uint32_t j = 0; j < kMergeBatch; ++j) {
+                    const uint32_t fj = f0 + j;
+                    if (fj >= p.frames) break;
+                    if (fj == 0u && p.reset_first) {              // wgsl:345-350
+                        c = mk(0.0f, 0.0f, 0.0f);
+                        n = 0u;
+                    }
+                    const v3 col = mk(__uint_as_float(v[j].x), __uint_as_float(v[j].y),
+                                      __uint_as_float(v[j].z));
+                    if (valid && n < spp) {                       // wgsl:352, 356-357
+                        const float k = (float)(n + 1u);
+                        c = mk(c.x + (col.x - c.x) / k, c.y + (col.y - c.y) / k,
+                               c.z + (col.z - c.z) / k);
+                    }
+                    // wgsl:362-363, the same images as the per-wave mode
+                    if (valid && (fj + 1u == p.frames ||
+                                  (p.store_each && (p.store_each == 2u || fj + 2u == p.frames)))) {
+                        float4* dst = (p.store_each && (fj & 1u)) ? p.out2 : p.out;
+                        dst[tc.idx] = make_float4(c.x, c.y, c.z, (float)(n < spp ? n + 1u : n));
+                    }
+                    n = f2u((float)(n < spp ? n + 1u : n));
+                }
+            }
+        }
+    }
+    if (p.tile_cost && threadIdx.x == 0u && chunk == 0u)
         p.tile_cost[group] = (uint32_t)__builtin_amdgcn_s_memtime() - p.tile_cost[group];
     WAVE_TRACE(1);
 }
@@ -2850,30 +2952,84 @@ static dim3 tile_grid(const TraceParams& p, uint32_t waves = 4) {
     return dim3((tiles_x + waves - 1u) / waves, p.local_bands);
 }
 
+// Launches through hipModuleLaunchKernel with the arguments packed in the kernel's layout and
+// a function handle cached per device and kernel (the launch_single path below): no
+// per-launch symbol lookup or per-argument marshalling of the 2.6-KB TraceParams block.
+// Slots: 0-4 rt_trace_kernel<k>, 5-8 rt_bounce_kernel<m>.
+constexpr int kLaunchSlots = 9;
+static hipError_t launch_packed(int slot, const void* sym, dim3 grid, dim3 block, size_t lds,
+                                hipStream_t stream, void* args, size_t bytes) {
+    constexpr int kMaxDevices = 64;
+    static hipFunction_t fn[kMaxDevices][kLaunchSlots] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDevices || slot < 0 || slot >= kLaunchSlots)
+        return hipErrorInvalidValue;
+    if (!fn[dev][slot]) {
+        e = hipGetFuncBySymbol(&fn[dev][slot], sym);
+        if (e != hipSuccess) {
+            fn[dev][slot] = nullptr;
+            return e;
+        }
+    }
+    void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes,
+                     HIP_LAUNCH_PARAM_END};
+    return hipModuleLaunchKernel(fn[dev][slot], grid.x, grid.y, grid.z, block.x, block.y,
+                                 block.z, (unsigned)lds, stream, nullptr, extra);
+}
+
+// rt_trace_kernel's explicit arguments in its layout (the preloaded leading dwords, then
+// TraceParams at kParamsOff)
+struct TraceArgs {
+    const float4* cand;
+    const uint32_t* hx;
+    const float4* in;
+    uint32_t width, height, bands;
+    TraceParams p;
+};
+static_assert(offsetof(TraceArgs, p) == kParamsOff, "rt_trace_kernel's argument layout");
+
 template <int kScan>
-static void launch_trace_as(const TraceParams& p, size_t lds, hipStream_t stream) {
+static hipError_t launch_trace_as(const TraceParams& p, size_t lds, hipStream_t stream) {
     constexpr uint32_t w = wg_waves<kScan>();
     const dim3 grid = tile_grid(p, is_group_kernel(kScan) ? 1u : w);
-    if (grid.x == 0 || grid.y == 0) return;
-    hipLaunchKernelGGL(rt_trace_kernel<kScan>, grid, dim3(64 * w), lds, stream, p.cand,
-                       p.hx, p.in, p.width, p.height,
-                       pack_bands(p.band_first, p.band_step, p.tile_order != nullptr), p);
+    if (grid.x == 0 || grid.y == 0) return hipSuccess;
+    TraceArgs args;
+    std::memset(&args, 0, offsetof(TraceArgs, p));
+    args.cand = p.cand;
+    args.hx = p.hx;
+    args.in = p.in;
+    args.width = p.width;
+    args.height = p.height;
+    args.bands = pack_bands(p.band_first, p.band_step, p.tile_order != nullptr);
+    args.p = p;
+    return launch_packed(kScan, reinterpret_cast<const void*>(&rt_trace_kernel<kScan>), grid,
+                         dim3(64 * w), lds, stream, &args, sizeof(args));
 }
 
 // Workgroups of kBounceWaves tiles along a stripe band: grid (column groups, bands).
-static void launch_bounce(const TraceParams& p, hipStream_t stream) {
+static hipError_t launch_bounce(const TraceParams& p, hipStream_t stream) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     const uint32_t w = p.compact == 1u ? kBounceWaves : 1u;   // tiles per workgroup
-    const dim3 grid((tiles_x + w - 1u) / w, p.local_bands);
-    if (grid.x == 0 || grid.y == 0) return;
+    dim3 grid((tiles_x + w - 1u) / w, p.local_bands);
+    if (grid.x == 0 || grid.y == 0) return hipSuccess;
     const size_t lds = (size_t)p.lds_records * sizeof(float4);
-    if (p.compact == 1u)
-        hipLaunchKernelGGL(rt_bounce_kernel<kBounceCompact>, grid, dim3(64 * kBounceWaves), lds,
-                           stream, p);
-    else if (p.compact == 2u)
-        hipLaunchKernelGGL(rt_bounce_kernel<kBouncePair>, grid, dim3(128), lds, stream, p);
-    else
-        hipLaunchKernelGGL(rt_bounce_kernel<kBounceWave>, grid, dim3(64), lds, stream, p);
+    TraceParams args = p;
+    const void* sym = reinterpret_cast<const void*>(&rt_bounce_kernel<kBounceWave>);
+    uint32_t threads = 64;
+    if (p.compact == 3u) {                                    // (tile, chunk) units
+        grid.x = tiles_x * p.split;
+        sym = reinterpret_cast<const void*>(&rt_bounce_kernel<kBounceSplit>);
+    } else if (p.compact == 1u) {
+        sym = reinterpret_cast<const void*>(&rt_bounce_kernel<kBounceCompact>);
+        threads = 64 * kBounceWaves;
+    } else if (p.compact == 2u) {
+        sym = reinterpret_cast<const void*>(&rt_bounce_kernel<kBouncePair>);
+        threads = 128;
+    }
+    return launch_packed(5 + (int)p.compact, sym, grid, dim3(threads), lds, stream, &args,
+                         sizeof(args));
 }
 
 // The explicit arguments of rt_single_kernel / rt_chain_kernel, in the kernels' layout.
@@ -3061,20 +3217,16 @@ hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
     if (kernel == kTraceSingle) return launch_single<(int)kSinglePix>(p, stream);
     if (kernel == kTraceSingleOne) return launch_single<1>(p, stream);
     if (kernel == kTraceCulled)
-        launch_trace_as<kTraceCulled>(p, (size_t)p.lds_records * sizeof(float4), stream);
-    else if (kernel == kTraceList)
-        launch_trace_as<kTraceList>(p, 0, stream);
-    else if (kernel == kTraceListPair)
-        launch_trace_as<kTraceListPair>(p, 2 * (frame_group<kTraceListPair>() - 1) * 64 *
-                                               sizeof(float4), stream);
-    else if (kernel == kTraceBounce)
-        launch_bounce(p, stream);
-    else if (kernel == kTraceListQuad)
-        launch_trace_as<kTraceListQuad>(p, 2 * (frame_group<kTraceListQuad>() - 1) * 64 *
-                                               sizeof(float4), stream);
-    else
-        launch_trace_as<kTraceExhaustive>(p, 0, stream);
-    return hipGetLastError();
+        return launch_trace_as<kTraceCulled>(p, (size_t)p.lds_records * sizeof(float4), stream);
+    if (kernel == kTraceList) return launch_trace_as<kTraceList>(p, 0, stream);
+    if (kernel == kTraceListPair)
+        return launch_trace_as<kTraceListPair>(
+            p, 2 * (frame_group<kTraceListPair>() - 1) * 64 * sizeof(float4), stream);
+    if (kernel == kTraceBounce) return launch_bounce(p, stream);
+    if (kernel == kTraceListQuad)
+        return launch_trace_as<kTraceListQuad>(
+            p, 2 * (frame_group<kTraceListQuad>() - 1) * 64 * sizeof(float4), stream);
+    return launch_trace_as<kTraceExhaustive>(p, 0, stream);
 }
 
 hipError_t launch_candidates(const TraceParams& p, float4* cand, hipStream_t stream) {

@@ -74,7 +74,7 @@ class SceneCamera:
         return SceneCamera(a)
 
     def to_c(self) -> _lib.SceneCameraC:
-        return _lib.SceneCameraC.from_buffer_copy(self.blob.astype(np.float32).tobytes())
+        return _lib.SceneCameraC.from_buffer_copy(np.ascontiguousarray(self.blob, np.float32))
 
     def with_fields(self, **kw) -> "SceneCamera":
         c = self.to_c()

@@ -30,6 +30,16 @@ def _ptr(t: torch.Tensor) -> ctypes.c_void_p:
     return ctypes.c_void_p(t.data_ptr())
 
 
+def _np_ptr(a: np.ndarray) -> ctypes.c_void_p:
+    # (the array interface's address: ndarray.ctypes builds a helper object per access,
+    # several microseconds of host time on every call)
+    return ctypes.c_void_p(a.__array_interface__["data"][0])
+
+
+# torch's current stream as a raw handle without building a Stream object per call
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _check_image(t: torch.Tensor, width: int, height: int, name: str) -> None:
     if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
         raise ValueError(f"{name} must be a CUDA (HIP) tensor")
@@ -109,11 +119,12 @@ class ComputeShaderPipeline:
                 "packets": int(packets.value), "why": why}
 
     def set_path_compaction(self, mode: str) -> None:
-        """rt_set_path_compaction for bounce launches: "auto" (default), "per_wave",
-        "compact" (paths repacked across four waves after every bounce) or "pair" (two waves
-        per tile on alternate frames)."""
+        """rt_set_path_compaction for bounce launches: "auto" (default: "split" for small
+        launches, else "per_wave"), "per_wave", "compact" (paths repacked across four waves
+        after every bounce), "pair" (two waves per tile on alternate frames) or "split" (each
+        tile's frames in 2-4 chunks on separate waves, the last finisher accumulating)."""
         _lib.call("rt_set_path_compaction", self._ctx,
-                  {"auto": 0, "per_wave": 1, "compact": 2, "pair": 3}[mode])
+                  {"auto": 0, "per_wave": 1, "compact": 2, "pair": 3, "split": 4}[mode])
 
     def set_single_kernel(self, mode: str) -> None:
         """rt_set_single_kernel: "auto" (one-frame launches of the camera-ray-only case run
@@ -175,12 +186,14 @@ class ComputeShaderPipeline:
 
     # ---- helpers ----------------------------------------------------------------------
     def _stream(self) -> ctypes.c_void_p:
+        if _raw_stream is not None:
+            return ctypes.c_void_p(_raw_stream(self.device))
         return ctypes.c_void_p(torch.cuda.current_stream(self.torch_device).cuda_stream)
 
     def _spheres(self, spheres: SphereCollection):
         arr = np.ascontiguousarray(spheres.spheres, np.float32)
         self._sphere_keep = arr
-        return arr.ctypes.data_as(ctypes.c_void_p), arr.shape[0]
+        return _np_ptr(arr), arr.shape[0]
 
     def new_image(self, width: int, height: int) -> torch.Tensor:
         return torch.zeros((height, width, 4), dtype=torch.float32, device=self.torch_device)
@@ -217,7 +230,7 @@ class ComputeShaderPipeline:
         p, n = self._spheres(spheres)
         s = np.ascontiguousarray(seeds, np.float32)
         _lib.call("rt_render", self._ctx, _ptr(inp), _ptr(out), width, height,
-                  ctypes.byref(cam), p, n, s.size, s.ctypes.data_as(ctypes.c_void_p),
+                  ctypes.byref(cam), p, n, s.size, _np_ptr(s),
                   self._stream())
 
     def render_stripes(self, inp: torch.Tensor, out: torch.Tensor, width: int, height: int,
@@ -230,7 +243,7 @@ class ComputeShaderPipeline:
         p, n = self._spheres(spheres)
         s = np.ascontiguousarray(seeds, np.float32)
         _lib.call("rt_render_stripes", self._ctx, _ptr(inp), _ptr(out), width, height, rank,
-                  nranks, ctypes.byref(cam), p, n, s.size, s.ctypes.data_as(ctypes.c_void_p),
+                  nranks, ctypes.byref(cam), p, n, s.size, _np_ptr(s),
                   self._stream())
 
     def update_frames(self, image_a: torch.Tensor, image_b: torch.Tensor, width: int,
@@ -247,8 +260,8 @@ class ComputeShaderPipeline:
         s = np.ascontiguousarray(seeds, np.float32)
         newest = ctypes.c_int(-1)
         _lib.call("rt_update_frames", self._ctx, _ptr(image_a), _ptr(image_b), width, height,
-                  rank, nranks, ctypes.byref(cam), p, n, s.size,
-                  s.ctypes.data_as(ctypes.c_void_p), self._stream(), ctypes.byref(newest))
+                  rank, nranks, ctypes.byref(cam), p, n, s.size, _np_ptr(s), self._stream(),
+                  ctypes.byref(newest))
         return newest.value
 
     def deinterleave(self, gathered: torch.Tensor, out: torch.Tensor, width: int, height: int,

@@ -181,6 +181,9 @@ RT_API const char* rt_last_error(void);
 #define RT_KERNEL_SINGLE 8
 /* the same with one tile per wave, for small per-rank shares */
 #define RT_KERNEL_SINGLE_ONE 9
+/* bounce rays, each tile's frames split into chunks traced by separate waves, the last
+ * finisher accumulating them in order (RT_PATHS_SPLIT) */
+#define RT_KERNEL_BOUNCE_SPLIT 10
 /* The instance's name as rocprofv3 lists it ("rt_trace_kernel<k>", "rt_bounce_kernel<m>",
  * "rt_single_kernel<p>"), "rt_trace_kernel" for an unknown id. */
 RT_API const char* rt_kernel_name(int which);
@@ -369,13 +372,17 @@ RT_API rt_status rt_update_submit_status(rt_ctx* ctx, int* aql_available, uint32
  * frames, the second handing its colours to the first through LDS (shorter chains for
  * small per-rank shares); RT_PATHS_COMPACT repacks the live paths of a workgroup's four
  * waves into the fewest waves after every bounce (ballot + mbcnt prefix, path state through
- * LDS).  RT_PATHS_AUTO (default) = RT_PATHS_PER_WAVE, the fastest at every rank count
- * measured (profiles/r02_rank_sim_k5_paths_*.jsonl).  Pixel results are identical in
- * every mode. */
+ * LDS); RT_PATHS_SPLIT splits each tile's frames into 2 or 4 consecutive chunks, each traced
+ * by its own wave, which stores its frames' colours (device scratch the context keeps: 1 KB
+ * per tile and frame); the tile's last finishing chunk accumulates every frame in order and
+ * writes the images.  RT_PATHS_AUTO (default): RT_PATHS_SPLIT with 4 chunks for launches of
+ * at most 20 000 tiles, 2 chunks up to 40 000 (small per-rank shares: a few waves per SIMD),
+ * else RT_PATHS_PER_WAVE.  Pixel results are identical in every mode. */
 #define RT_PATHS_AUTO 0
 #define RT_PATHS_PER_WAVE 1
 #define RT_PATHS_COMPACT 2
 #define RT_PATHS_PAIR 3
+#define RT_PATHS_SPLIT 4
 RT_API rt_status rt_set_path_compaction(rt_ctx* ctx, int mode);
 /* One-frame launches of the camera-ray-only case (rt_update, rt_render / rt_update_frames
  * launches carrying one frame): AUTO (default) runs RT_KERNEL_SINGLE (two tiles per wave),

@@ -397,6 +397,38 @@ def test_bench_k5_launches_match_golden(rt):
         p.close()
 
 
+@pytest.mark.parametrize("world,paths", [(1, "split"), (4, "auto"), (8, "auto"), (8, "per_wave")])
+def test_bench_k5_shares_match_golden(rt, world, paths):
+    """bench.py --config K5 per rank: rank 0's stripe share of the 64-spp 3840x2160 depth-8
+    render (one 64-frame bounce launch), AUTO splitting each tile's frames into chunks on
+    separate waves for small shares (2 chunks at 4 ranks, 4 at 8; forced on the whole
+    image), per wave otherwise — the fixture's sampled pixels that fall in rank 0's bands,
+    bit for bit, on two consecutive steps (the second runs the cost order the first
+    measured; the arrival counters are reused)."""
+    g = load_golden("k5.npz")
+    w, h = int(g["width"]), int(g["height"])
+    p = rt.ComputeShaderPipeline(0)
+    p.set_path_compaction(paths)
+    try:
+        rows = rt.stripe_local_rows(h, 0, world)
+        a, b = p.new_image(w, rows), p.new_image(w, rows)
+        py, px = g["py"], g["px"]
+        mine = (py // 8) % world == 0
+        ly = (py[mine] // 8 // world) * 8 + py[mine] % 8
+        for step in range(2):
+            newest = p.update_frames(a, b, w, h, rt.SceneCamera(g["camera"]),
+                                     rt.SphereCollection(g["spheres"]), g["seeds"], 0, world)
+            info = p.last_launch_info()
+            split = paths == "split" or (paths == "auto" and world >= 4)
+            assert info["kernel_name"] == ("rt_bounce_kernel<3>" if split
+                                           else "rt_bounce_kernel<0>"), info
+            img = host(b if newest == 1 else a)
+            assert_same(img[ly, px[mine]], g["pixels"][mine])
+            assert np.all(img[:rows, :, 3] == 64)
+    finally:
+        p.close()
+
+
 def test_golden_k5_sampled(rt, pipe):
     """configs[4] shape on one GPU: 3840x2160, 500 spheres, 64 spp, depth 8 (sampled)."""
     g = load_golden("k5.npz")
@@ -784,7 +816,14 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, s
         assert_same(got_prev, want_prev)
 
 
-BOUNCE_PATH_KERNEL = {"per_wave": 0, "compact": 1, "pair": 2, "auto": 0}
+BOUNCE_PATH_KERNEL = {"per_wave": 0, "compact": 1, "pair": 2, "auto": 3, "split": 3}
+
+
+def bounce_kernel(paths, frames_per_launch):
+    """The instance a bounce launch runs: AUTO / split at these small sizes split each tile's
+    frames into chunks (rt_bounce_kernel<3>) when the launch carries two frames or more."""
+    k = BOUNCE_PATH_KERNEL[paths]
+    return 0 if k == 3 and frames_per_launch < 2 else k
 
 
 def _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks, fpl,
@@ -812,7 +851,8 @@ def _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks
             newest = p.update_frames(a, b, w, h, cam, sc, seeds, r, nranks)
             info = p.last_launch_info()
             if depth >= 2:
-                assert info["kernel_name"] == "rt_bounce_kernel<%d>" % BOUNCE_PATH_KERNEL[paths]
+                per = (frames % fpl or fpl) if fpl else frames   # the call's last launch
+                assert info["kernel_name"] == "rt_bounce_kernel<%d>" % bounce_kernel(paths, per)
                 if fpl and rt.stripe_local_rows(h, r, nranks):
                     assert info["launches"] == -(-frames // fpl)
             img_new, img_prev = (host(a), host(b)) if newest == 0 else (host(b), host(a))
@@ -827,7 +867,7 @@ def _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks
         assert_same(got_prev, want_prev.reshape(h, w, 4))
 
 
-@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "auto"])
+@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "split", "auto"])
 @pytest.mark.parametrize("w,h,depth,frames,scene,nranks", [
     (56, 40, 2, 5, "n120", 1), (67, 45, 8, 3, "default", 1), (64, 48, 3, 1, "n120", 1),
     (50, 37, 8, 6, "default", 3), (40, 32, 0, 2, "n120", 1), (72, 48, 5, 4, "three", 2)])
@@ -839,7 +879,7 @@ def test_bounce_launches_match_oracle(rt, oracle, paths, w, h, depth, frames, sc
     _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks, 0)
 
 
-@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair"])
+@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "split"])
 @pytest.mark.parametrize("w,h,depth,frames,scene,nranks", [
     (56, 40, 2, 5, "n120", 1), (50, 37, 8, 6, "default", 3), (72, 48, 5, 4, "three", 2)])
 @pytest.mark.parametrize("images", ["last_two", "every"])
