@@ -65,7 +65,7 @@ PEAK_FP32_TFLOPS = 157.3      # MI355X FP32 vector peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0         # MI355X HBM3E peak
 # Practical floor of one progressive update's memory pattern (read + write 16 B per pixel,
 # one dependent launch per frame, no tracing), measured by tools/rmw_floor.hip at 1920x1080:
-# 10.18 us per launch = 0.815 of the 8 TB/s peak (profiles/r02_rmw_floor.jsonl)
+# 10.18 us per launch = 0.815 of the 8 TB/s peak (profiles/archive/r02_rmw_floor.jsonl)
 RMW_FLOOR_GBS = 6518.0
 CLOCK_GHZ = 2.4               # MI355X max engine clock
 SIMDS = 1024                  # 256 CUs x 4 SIMDs
@@ -593,7 +593,7 @@ def main():
             # the same bytes against the measured streaming floor of the pattern (no tracing)
             "practical_hbm": {"floor_GBs": RMW_FLOOR_GBS,
                               "frac": round(bytes_launch / launch_s / 1e9 / RMW_FLOOR_GBS, 4),
-                              "source": "tools/rmw_floor.hip, profiles/r02_rmw_floor.jsonl"}}
+                              "source": "tools/rmw_floor.hip, profiles/archive/r02_rmw_floor.jsonl"}}
     if pmc and pmc.get("valu_insts_per_launch"):
         insts = pmc["valu_insts_per_launch"]
         avail = SIMDS * CLOCK_GHZ * 1e9 * launch_s

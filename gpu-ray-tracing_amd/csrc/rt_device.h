@@ -199,6 +199,17 @@ __device__ __forceinline__ float sqrt_core(float x) {
     const float g = x * y, h = 0.5f * y;
     return fmaf(fmaf(-g, g, x), h, g);
 }
+// sqrt_core(x) and, from the same rsq(x), a refined reciprocal of the result (one Newton
+// step, no v_rcp): y is within the accuracy rcp_refined gives (rsq(x) is within ~1.5 ulp of
+// 1 / sqrt_core(x), the step squares that), so div_core(a, len, y) is the IEEE a / len on
+// div_core's domain (rt_selftest_fastmath replays it: out[1]).
+__device__ __forceinline__ float sqrt_core_rcp(float x, float& y) {
+    const float r = __builtin_amdgcn_rsqf(x);
+    const float g = x * r, h = 0.5f * r;
+    const float len = fmaf(fmaf(-g, g, x), h, g);
+    y = fmaf(fmaf(-len, r, 1.0f), r, r);
+    return len;
+}
 // |x| as its bit pattern (domain checks on the integer view)
 __device__ __forceinline__ uint32_t abs_bits(float x) { return __float_as_uint(x) & 0x7FFFFFFFu; }
 constexpr uint32_t kBits2m100 = 0x0D800000u;   // 2^-100

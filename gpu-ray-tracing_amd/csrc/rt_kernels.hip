@@ -1478,6 +1478,10 @@ constexpr uint32_t kSingleWg = RT_SINGLE_WG;
 #ifndef RT_SINGLE_SCAN
 #define RT_SINGLE_SCAN 0
 #endif
+// records per tile and step of the joint list walk (both tiles' lists in one loop)
+#ifndef RT_SINGLE_CHUNK
+#define RT_SINGLE_CHUNK RT_LIST_CHUNK
+#endif
 // skip the hit shading of a tile none of whose rays hit
 #ifndef RT_SINGLE_GATE
 #define RT_SINGLE_GATE 0
@@ -1574,12 +1578,23 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
 }
 
 // normalize(d).y of the sky (wgsl:293-296) and its colour times cf
+// RT_SKY_RSQ: the reciprocal of |d| from the square root's own rsq (sqrt_core_rcp) instead
+// of a second transcendental (v_rcp)
+#ifndef RT_SKY_RSQ
+#define RT_SKY_RSQ 0
+#endif
 __device__ __forceinline__ v3 sky_w(v3 cf, v3 d) {
     const float dd = dot(d, d);
     float uy;
     if (rt_ballot(__float_as_uint(dd) - kBits2m20 >= kBits2p40 - kBits2m20) == 0ull) {
-        const float len = sqrt_core(dd);
-        uy = div_core(d.y, len, rcp_refined(len));
+        if (RT_SKY_RSQ) {
+            float y;
+            const float len = sqrt_core_rcp(dd, y);
+            uy = div_core(d.y, len, y);
+        } else {
+            const float len = sqrt_core(dd);
+            uy = div_core(d.y, len, rcp_refined(len));
+        }
     } else {
         uy = d.y / sqrtf(dd);
     }
@@ -1605,7 +1620,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                                               const uint64_t (&live_m)[S],
                                               const float4 (&bv)[S], float4* lblk,
                                               v3 (&col)[S]) {
-    constexpr int K = RT_LIST_CHUNK;
+    constexpr int K = RT_SINGLE_CHUNK;
     v3 o[S], d[S];
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {                            // wgsl:311, 305-325
@@ -2919,6 +2934,15 @@ __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cn
         if ((r2 & 0x380000u) == 0)                    // n + 1 counts, n < 2^32 - 1
             b = (float)((r2 & 0x400000u) ? 1u + (r1 & 0xFFFFFFu) : max(r1, 1u));
         bad1 += !same_bits(div_core_signed(a, b, rcp_refined(b)), a / b);
+        {   // the sky's d.y / |d| with |d| and its reciprocal from one rsq (sqrt_core_rcp):
+            // |d|^2 in [2^-20, 2^40], |d.y| <= |d| (and >= 2^-100 or zero)
+            const float dd = with_exp(r1 & 0x7FFFFFu, -20 + (int)(r2 % 60u));
+            float y;
+            const float len = sqrt_core_rcp(dd, y);
+            const float dy = (r0 & 0x1000u) ? 0.0f : unit_rand(r0) * len;
+            if (dd <= 0x1p40f && (dy == 0.0f || fabsf(dy) >= 0x1p-100f))
+                bad1 += !same_bits(div_core(dy, len, y), dy / sqrtf(dd));
+        }
         // the accumulator's f64-reciprocal division: any f32 numerator (r0's bits: zeros,
         // subnormals, inf, NaN included), k = f32(n + 1) for n + 1 in [1, 2^24]
         const uint32_t kk = (r2 & 0x800000u) ? 1u + (r1 & 0xFFFFFFu)
