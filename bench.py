@@ -398,6 +398,12 @@ def driver_record_sides(device, stream, main_cfg, main_us):
     return out
 
 
+def _unserializable(o):
+    """json default: a value the line cannot hold is named, not fatal (the line still
+    prints; the bad path shows in its place)."""
+    return f"<{type(o).__name__} {getattr(o, '__name__', '')}>"
+
+
 def timed(stream, fn):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -433,7 +439,7 @@ def main():
     if dispatch:
         # progressive frames: frame 0 resets, one seed per frame
         spheres = rt.SphereCollection.generate(kind, nsph, 1)
-        seeds = rt.frame_seeds(FRAME_SEED, args.warmup + args.steps + 3 * args.side)
+        seeds = rt.frame_seeds(FRAME_SEED, args.warmup + args.steps + 5 * args.side)
         settings = rt.CameraSettings(max_depth=depth, samples_per_pixel=BENCH_SPP)
         cam0 = rt.SceneCamera.from_settings(settings, w, h, float(seeds[0]))
         cam_t = cam0.with_fields(camera_has_moved=0.0)
@@ -676,17 +682,32 @@ def main():
                 "unit": "TFLOP/s", "frac": round(flops / t_exh / 1e12 / PEAK_FP32_TFLOPS, 4),
                 "flop_per_frame": flops}
             # the same frames fused (up to 64 per launch; K4's launches, the last two
-            # frames' images written)
+            # frames' images written), after one untimed fused call that records the tile
+            # costs the fused instances order by (the dispatch steps record none); then as a
+            # frame chain writing every frame's image (what rank shares run)
             set_frame_launch(pipe, "dispatch")
             pipe.set_frames_per_launch(0)
             s1 = base + args.side
+            r.frames(cam_t, spheres, seeds[s1:s1 + args.side])
+            s1 += args.side
             t_f = timed(stream, lambda: r.frames(cam_t, spheres, seeds[s1:s1 + args.side]))
             fi = pipe.last_launch_info()
+            set_frame_launch(pipe, "chain")
+            s2 = s1 + args.side
+            t_c = timed(stream, lambda: r.frames(cam_t, spheres, seeds[s2:s2 + args.side]))
+            ci = pipe.last_launch_info()
             set_frame_launch(pipe, launch_mode)
             side["fused_frames"] = {"kernel": fi["kernel_name"],
                                     "frames_per_launch": fi["max_frames_per_launch"],
                                     "us_per_frame": round(t_f / args.side * 1e6, 2),
-                                    "Mrays_per_s": round(local_px * args.side / t_f / 1e6, 1)}
+                                    "Mrays_per_s": round(local_px * args.side / t_f / 1e6, 1),
+                                    "what": "the last two frames' images written per launch"}
+            side["chain_frames"] = {"kernel": ci["kernel_name"],
+                                    "frames_per_launch": ci["max_frames_per_launch"],
+                                    "us_per_frame": round(t_c / args.side * 1e6, 2),
+                                    "Mrays_per_s": round(local_px * args.side / t_c / 1e6, 1),
+                                    "what": "every frame's image written (rt_set_frame_images "
+                                            "EVERY): the structure of the rank shares' steps"}
             # moving camera: every frame a new camera (the reference's WASD movement resets
             # the accumulator, camera.rs:243-252, wgsl:345-350): candidate lists rebuilt
             # every frame, one update dispatch each
@@ -731,7 +752,7 @@ def main():
     if rank == 0:
         if world == 1 and args.cpu_seconds > 0:
             line["cpu_baseline"] = cpu_baseline(cam0, spheres, w, h, args.cpu_seconds)
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line, default=_unserializable), flush=True)
     if comm is not None:
         torch.cuda.synchronize()
         comm.close()

@@ -643,12 +643,16 @@ rt_status plan_wg_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_
 // waves resident per SIMD on average); S times as many, S times shorter waves keep them
 // busy to the end.  S = 4 up to kSplit4MaxTiles tiles per launch, 2 up to kSplit2MaxTiles,
 // else 1 (per wave; RT_PATHS_SPLIT forces at least 2); never more chunks than frames.
-// RT_BOUNCE_SPLIT (environment, diagnostic) overrides S.
+// RT_BOUNCE_SPLIT (environment, diagnostic) overrides S.  Measured (tools/k5_ab.py, 64-frame
+// K5 launches, the modes interleaved launch by launch, 7 each; profiles/r04/k5_ab_r04e.jsonl):
+// 8-rank share per wave 4 635 µs, S = 2 4 422, S = 4 4 821, S = 8 4 970; 4-rank share per
+// wave 8 010, S = 2 8 388, S = 4 9 490 — the chunks' scratch traffic, merges and extra wave
+// starts cost more than the shorter tail saves except for two chunks at 8 ranks.
 #ifndef RT_SPLIT4_MAX_TILES
-#define RT_SPLIT4_MAX_TILES 20000
+#define RT_SPLIT4_MAX_TILES 0
 #endif
 #ifndef RT_SPLIT2_MAX_TILES
-#define RT_SPLIT2_MAX_TILES 40000
+#define RT_SPLIT2_MAX_TILES 20000
 #endif
 constexpr uint64_t kSplit4MaxTiles = RT_SPLIT4_MAX_TILES, kSplit2MaxTiles = RT_SPLIT2_MAX_TILES;
 rt_status plan_split(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t stream) {

@@ -849,6 +849,11 @@ __device__ __forceinline__ v3 sel3(bool c, v3 a, v3 b) {
     return mk(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z);
 }
 
+// RT_SKY_RSQ: the reciprocal of |v| in the sky's normalize(d).y and in normalize_w from the
+// square root's own rsq (sqrt_core_rcp) instead of a second transcendental (v_rcp)
+#ifndef RT_SKY_RSQ
+#define RT_SKY_RSQ 0
+#endif
 // normalize(v) = v / sqrt(v.v) (WGSL normalize).  kFast: when every active lane's |v|^2 is
 // in [2^-20, 2^40] (NaN, 0 and inf are not) and its components are >= 2^-100 in
 // magnitude, sqrt_core and div_core with the shared reciprocal of |v| in [2^-10, 2^20]
@@ -862,8 +867,9 @@ __device__ __forceinline__ v3 normalize_w(v3 v) {
         const bool in = span < kBits2p40 - kBits2m20 && vmin >= kBits2m100;
         if ((RT_SINGLE_MASKS ? (mask_uge(span, kBits2p40 - kBits2m20) | mask_ult(vmin, kBits2m100))
                              : rt_ballot(!in)) == 0ull) {
-            const float len = sqrt_core(dd);
-            const float y = rcp_refined(len);
+            float y;
+            const float len = RT_SKY_RSQ ? sqrt_core_rcp(dd, y) : sqrt_core(dd);
+            if (!RT_SKY_RSQ) y = rcp_refined(len);
             return mk(div_core(v.x, len, y), div_core(v.y, len, y), div_core(v.z, len, y));
         }
     }
@@ -1578,11 +1584,6 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
 }
 
 // normalize(d).y of the sky (wgsl:293-296) and its colour times cf
-// RT_SKY_RSQ: the reciprocal of |d| from the square root's own rsq (sqrt_core_rcp) instead
-// of a second transcendental (v_rcp)
-#ifndef RT_SKY_RSQ
-#define RT_SKY_RSQ 0
-#endif
 __device__ __forceinline__ v3 sky_w(v3 cf, v3 d) {
     const float dd = dot(d, d);
     float uy;

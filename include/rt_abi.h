@@ -375,9 +375,9 @@ RT_API rt_status rt_update_submit_status(rt_ctx* ctx, int* aql_available, uint32
  * LDS); RT_PATHS_SPLIT splits each tile's frames into 2 or 4 consecutive chunks, each traced
  * by its own wave, which stores its frames' colours (device scratch the context keeps: 1 KB
  * per tile and frame); the tile's last finishing chunk accumulates every frame in order and
- * writes the images.  RT_PATHS_AUTO (default): RT_PATHS_SPLIT with 4 chunks for launches of
- * at most 20 000 tiles, 2 chunks up to 40 000 (small per-rank shares: a few waves per SIMD),
- * else RT_PATHS_PER_WAVE.  Pixel results are identical in every mode. */
+ * writes the images.  RT_PATHS_AUTO (default): RT_PATHS_SPLIT with 2 chunks for launches of
+ * at most 20 000 tiles (small per-rank shares: a few waves per SIMD), else RT_PATHS_PER_WAVE
+ * (DESIGN.md §5).  Pixel results are identical in every mode. */
 #define RT_PATHS_AUTO 0
 #define RT_PATHS_PER_WAVE 1
 #define RT_PATHS_COMPACT 2

@@ -397,12 +397,13 @@ def test_bench_k5_launches_match_golden(rt):
         p.close()
 
 
-@pytest.mark.parametrize("world,paths", [(1, "split"), (4, "auto"), (8, "auto"), (8, "per_wave")])
+@pytest.mark.parametrize("world,paths", [(1, "split"), (4, "split"), (4, "auto"), (8, "auto"),
+                                         (8, "per_wave")])
 def test_bench_k5_shares_match_golden(rt, world, paths):
     """bench.py --config K5 per rank: rank 0's stripe share of the 64-spp 3840x2160 depth-8
-    render (one 64-frame bounce launch), AUTO splitting each tile's frames into chunks on
-    separate waves for small shares (2 chunks at 4 ranks, 4 at 8; forced on the whole
-    image), per wave otherwise — the fixture's sampled pixels that fall in rank 0's bands,
+    render (one 64-frame bounce launch), AUTO splitting each tile's frames into two chunks on
+    separate waves for 8-rank shares (forced on the whole image and a 4-rank share), per wave
+    otherwise — the fixture's sampled pixels that fall in rank 0's bands,
     bit for bit, on two consecutive steps (the second runs the cost order the first
     measured; the arrival counters are reused)."""
     g = load_golden("k5.npz")
@@ -419,7 +420,7 @@ def test_bench_k5_shares_match_golden(rt, world, paths):
             newest = p.update_frames(a, b, w, h, rt.SceneCamera(g["camera"]),
                                      rt.SphereCollection(g["spheres"]), g["seeds"], 0, world)
             info = p.last_launch_info()
-            split = paths == "split" or (paths == "auto" and world >= 4)
+            split = paths == "split" or (paths == "auto" and world >= 8)
             assert info["kernel_name"] == ("rt_bounce_kernel<3>" if split
                                            else "rt_bounce_kernel<0>"), info
             img = host(b if newest == 1 else a)
