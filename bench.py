@@ -179,10 +179,11 @@ def cpu_model():
 
 
 def cpu_baseline(cam, spheres, w, h, seconds):
-    """The scalar C oracle on one update of the same camera and scene: (i) one
-    thread on a row band sized to ~seconds/3, (ii) host_threads() threads over 8-row bands
-    of whole frames for ~2*seconds/3 (at least one frame).  The threaded run is the
-    reported value."""
+    """The scalar C oracle on one update of the same camera and scene, on
+    native threads (oracle_update_threads: 8-row bands claimed from a shared counter):
+    (i) one thread on a row band (~seconds/5), (ii) host_threads() threads over whole frames
+    (~2*seconds/5, at least one frame; the reported value: a GPU's share of the host), (iii)
+    every core of the process's affinity set (~seconds/5, 2-row bands)."""
     from oracle import oracle as O
     img = np.zeros((h, w, 4), np.float32)
     O.lib()
@@ -190,36 +191,38 @@ def cpu_baseline(cam, spheres, w, h, seconds):
     t0 = time.perf_counter()
     O.update(img, cam.blob, spheres.spheres, rows=(mid, mid + 8))
     per_row = (time.perf_counter() - t0) / 8
-    rows1 = int(min(h, max(8, seconds / 3 / max(per_row, 1e-9)))) & ~7 or 8
+    rows1 = int(min(h, max(8, seconds / 5 / max(per_row, 1e-9)))) & ~7 or 8
     y0 = max(0, (h - rows1) // 2) & ~7
     t0 = time.perf_counter()
     O.update(img, cam.blob, spheres.spheres, rows=(y0, y0 + rows1))
     single = rows1 * w / (time.perf_counter() - t0) / 1e6
+
+    def threaded(threads, share, band):
+        # one frame first (its time sizes the sample), then enough frames for ~share s
+        t0 = time.perf_counter()
+        O.update_threads(img, cam.blob, spheres.spheres, threads, band)
+        one = time.perf_counter() - t0
+        frames = max(1, int(round(share / max(one, 1e-6))) - 1)
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            O.update_threads(img, cam.blob, spheres.spheres, threads, band)
+        return frames, time.perf_counter() - t0
+
     T = host_threads()
-    frames = max(1, int(round(2 * seconds / 3 / (w * h / (single * 1e6 * T)))))
-    t0 = time.perf_counter()
-    for _ in range(frames):
-        O.update_parallel(img, cam.blob, spheres.spheres, T)
-    dt = time.perf_counter() - t0
-    # every host core the process may use (SURVEY §8d5 "all nproc cores"): ~seconds/4 of
-    # whole frames on affinity-many threads (the reported value stays the per-GPU share)
+    frames, dt = threaded(T, 2 * seconds / 5, 8)
     A = host_cpus()[1]
-    fa = max(1, int(round(seconds / 4 / (w * h / (single * 1e6 * A)))))
     band = max(1, min(8, h // (2 * A)))        # at least two bands per thread
-    t0 = time.perf_counter()
-    for _ in range(fa):
-        O.update_parallel(img, cam.blob, spheres.spheres, A, band=band)
-    dta = time.perf_counter() - t0
+    fa, dta = threaded(A, seconds / 5, band)
     return {"value": round(w * h * frames / dt / 1e6, 3), "unit": "Mrays/s", "cores": T,
             "kind": "port",
             "sample": f"{frames} full {w}x{h} update(s) on {T} threads (8-row bands from a "
-                      f"queue), {dt:.1f} s; scalar C oracle (oracle/rt_oracle.c, gcc -O3), "
+                      f"shared counter), {dt:.1f} s; scalar C oracle (oracle/rt_oracle.c, gcc -O3), "
                       f"max_depth {int(cam.max_depth)}",
             "single_thread": {"value": round(single, 3), "cores": 1,
                               "sample": f"{w}x{rows1} rows of one update"},
             "all_cores": {"value": round(w * h * fa / dta / 1e6, 3), "cores": A,
                           "sample": f"{fa} full {w}x{h} update(s) on {A} threads "
-                                    f"({band}-row bands from a queue), {dta:.1f} s"},
+                                    f"({band}-row bands from a shared counter), {dta:.1f} s"},
             "cpu_model": cpu_model(),
             "nproc": host_cpus()[0], "affinity_cpus": host_cpus()[1],
             "cores_rule": "value: min(16, affinity) threads, the per-GPU share of the box's host "
@@ -483,7 +486,7 @@ def main():
     # Cold start (N=1 side line, before anything else ran on the GPU in this process): the
     # same W + K frames on scratch images, timed the same way — what the line's value would
     # be without the warm-up below.
-    cold = None
+    cold_start = None
     if args.side > 0 and world == 1 and dispatch:
         cr = StripeRenderer(pipe, w, h, rank, world, comm=None)
         torch.cuda.synchronize()
@@ -496,7 +499,7 @@ def main():
             seeds[args.warmup:args.warmup + args.steps]))
         dt_cold = time.perf_counter() - tc0
         ok, what = image_check(cfg, cr.local, args.warmup + args.steps, cam0, w, h)
-        cold = {"us_per_step_events": round(t_cold / args.steps * 1e6, 2),
+        cold_start = {"us_per_step_events": round(t_cold / args.steps * 1e6, 2),
                 "us_per_step_wall": round(dt_cold / args.steps * 1e6, 2),
                 "Mrays_per_s": round(w * h * args.steps / dt_cold / 1e6, 1),
                 "image_ok": ok, "image_check": what,
@@ -742,8 +745,8 @@ def main():
                                      "achieved": round(w * h * 20 / t_p / 1e9, 1),
                                      "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                      "frac": round(w * h * 20 / t_p / 1e9 / PEAK_HBM_GBS, 4)}
-        if cold is not None:
-            side["cold_start"] = cold
+        if cold_start is not None:
+            side["cold_start"] = cold_start
         if dispatch and depth == 1:
             # K2 / K5 / rank shares: each with its image check
             side.update(driver_record_sides(device, stream, cfg, render_s / args.steps * 1e6))

@@ -41,6 +41,8 @@ def lib() -> ctypes.CDLL:
         h.oracle_update_rows.argtypes = [_P, _P, _U32, _U32, _U32, _U32, _P, _P, _U32]
         h.oracle_update.restype = ctypes.c_uint64
         h.oracle_update.argtypes = [_P, _P, _U32, _U32, _P, _P, _U32]
+        h.oracle_update_threads.restype = ctypes.c_uint64
+        h.oracle_update_threads.argtypes = [_P, _P, _U32, _U32, _P, _P, _U32, _U32, _U32]
         h.oracle_render_pixels.restype = ctypes.c_uint64
         h.oracle_render_pixels.argtypes = [_P, _P, _P, ctypes.c_uint64, _P, _P, _U32, _U32, _P]
         h.oracle_init.restype = None
@@ -97,6 +99,20 @@ def update(inp: np.ndarray, camera: np.ndarray, spheres: np.ndarray,
     y0, y1 = rows if rows else (0, h)
     segs = lib().oracle_update_rows(_p(inp), _p(out), w, h, y0, y1, _p(cam), _p(sph),
                                     sph.shape[0])
+    return out, int(segs)
+
+
+def update_threads(inp: np.ndarray, camera: np.ndarray, spheres: np.ndarray, threads: int,
+                   band: int = 8) -> tuple[np.ndarray, int]:
+    """`update` over the whole image on `threads` native threads (oracle_update_threads:
+    bands claimed from a shared counter, no Python between them).  Same image as update()."""
+    inp = _f32(inp)
+    h, w, _ = inp.shape
+    out = inp.copy()
+    cam = _f32(camera).reshape(44)
+    sph = _f32(spheres).reshape(-1, 8)
+    segs = lib().oracle_update_threads(_p(inp), _p(out), w, h, _p(cam), _p(sph), sph.shape[0],
+                                       max(1, threads), max(1, band))
     return out, int(segs)
 
 

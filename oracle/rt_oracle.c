@@ -26,6 +26,8 @@
  * bit for bit (the parity tests require it).
  */
 #include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -322,6 +324,56 @@ EXPORT uint64_t oracle_update_rows(const float* in, float* out, uint32_t width,
 EXPORT uint64_t oracle_update(const float* in, float* out, uint32_t width, uint32_t height,
                               const float* camera, const float* spheres, uint32_t count) {
     return oracle_update_rows(in, out, width, height, 0, height, camera, spheres, count);
+}
+
+/* The same update on `threads` POSIX threads, each claiming `band`-row bands from a shared
+ * counter (the CPU baseline on all host cores, SURVEY §8d5: no Python between the bands). */
+typedef struct {
+    const float *in, *camera, *spheres;
+    float* out;
+    uint32_t width, height, count, band;
+    atomic_uint next;
+    atomic_ullong segs;
+} pool_t;
+
+static void* pool_run(void* arg) {
+    pool_t* p = (pool_t*)arg;
+    uint64_t segs = 0;
+    for (;;) {
+        const uint32_t y0 = atomic_fetch_add(&p->next, p->band);
+        if (y0 >= p->height) break;
+        const uint32_t y1 = y0 + p->band < p->height ? y0 + p->band : p->height;
+        segs += oracle_update_rows(p->in, p->out, p->width, p->height, y0, y1, p->camera,
+                                   p->spheres, p->count);
+    }
+    atomic_fetch_add(&p->segs, segs);
+    return NULL;
+}
+
+EXPORT uint64_t oracle_update_threads(const float* in, float* out, uint32_t width,
+                                      uint32_t height, const float* camera,
+                                      const float* spheres, uint32_t count, uint32_t threads,
+                                      uint32_t band) {
+    pool_t p;
+    p.in = in;
+    p.out = out;
+    p.camera = camera;
+    p.spheres = spheres;
+    p.width = width;
+    p.height = height;
+    p.count = count;
+    p.band = band ? band : 1u;
+    atomic_init(&p.next, 0u);
+    atomic_init(&p.segs, 0ull);
+    if (threads < 1u) threads = 1u;
+    if (threads > 1024u) threads = 1024u;
+    pthread_t tid[1024];
+    uint32_t started = 0;
+    for (uint32_t t = 1; t < threads; ++t)
+        if (pthread_create(&tid[started], NULL, pool_run, &p) == 0) ++started;
+    pool_run(&p);                       /* the caller's thread works too */
+    for (uint32_t t = 0; t < started; ++t) pthread_join(tid[t], NULL);
+    return (uint64_t)atomic_load(&p.segs);
 }
 
 /* `frames` chained updates on a list of pixels (px[i], py[i]); state[i] holds the
