@@ -168,6 +168,18 @@ def host_threads():
     return max(1, min(16, host_cpus()[1]))
 
 
+def cgroup_cpus():
+    """The CPU bandwidth limit of this process's cgroup (cgroup v2 cpu.max: quota / period)
+    in CPUs, or None when unlimited or unreadable.  (A box may show every host core in nproc
+    and the affinity set while its cgroup allows far fewer: the all-cores sample then runs
+    more threads than the quota schedules at once.)"""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_model():
     try:
         for line in Path("/proc/cpuinfo").read_text().splitlines():
@@ -225,6 +237,7 @@ def cpu_baseline(cam, spheres, w, h, seconds):
                                     f"({band}-row bands from a shared counter), {dta:.1f} s"},
             "cpu_model": cpu_model(),
             "nproc": host_cpus()[0], "affinity_cpus": host_cpus()[1],
+            "cgroup_cpu_quota": cgroup_cpus(),
             "cores_rule": "value: min(16, affinity) threads, the per-GPU share of the box's host "
                           "cores; all_cores: every core of the affinity set"}
 
@@ -346,9 +359,12 @@ def driver_record_sides(device, stream, main_cfg, main_us):
             pipe.set_frame_images("last_two")
             r = StripeRenderer(pipe, w, h, 0, world)
             r.frames(cam, sc, seeds)                   # records the tile costs
-            t = timed(stream, lambda: r.frames(cam, sc, seeds))
+            # (each call restarts from the camera's reset; the median of three launches)
+            runs = sorted(timed(stream, lambda: r.frames(cam, sc, seeds)) for _ in range(3))
+            t = runs[1]
             info = pipe.last_launch_info()
             return {"us_per_step": round(t * 1e6, 1), "us_per_spp": round(t / 64 * 1e6, 2),
+                    "runs_us": [round(x * 1e6, 1) for x in runs],
                     "kernel": info["kernel_name"],
                     "image_ok": share_pixels_ok("K5", r.local, 64, world)}
 

@@ -2317,8 +2317,13 @@ rt_bounce_kernel(const TraceParams p) {
     // kSplit: this chunk's frames [f_lo, f_hi), and the pixel's count before f_lo (the
     // count arithmetic of wgsl:345-362 over the frames before it, f32 round trip included)
     uint32_t f_lo = 0u, f_hi = p.frames;
+    // kSplit: chunk 0 accumulates its frames in registers when none of them stores an image
+    // (an image store of an early frame may go to the input buffer, p.out2, which the later
+    // chunks read at their start); otherwise it stores colours like the others
+    const uint32_t cs = kSplit ? (p.frames + S - 1u) / S : p.frames;
+    const bool c0_regs = kSplit && cs < p.frames && p.store_each != 2u &&
+                         !(p.store_each && p.frames - 2u < cs);
     if (kSplit) {
-        const uint32_t cs = (p.frames + S - 1u) / S;
         f_lo = min(chunk * cs, p.frames);
         f_hi = min(f_lo + cs, p.frames);
         for (uint32_t f = 0; f < f_lo; ++f) {
@@ -2443,8 +2448,9 @@ rt_bounce_kernel(const TraceParams p) {
             if (wave == 1u) s_pair_col[lane] = make_float4(res.x, res.y, res.z, 0.0f);
             __syncthreads();
         }
-        if (kSplit) {
+        if (kSplit && (chunk != 0u || !c0_regs)) {
             // the frame's colour, write-through (sc1): the tile's last arriver reads it
+            // (chunk 0 accumulates its frames in registers, as the per-wave mode does)
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
             const u32x4 v = {__float_as_uint(res.x), __float_as_uint(res.y),
                              __float_as_uint(res.z), 0u};
@@ -2484,10 +2490,18 @@ rt_bounce_kernel(const TraceParams p) {
         if (kCompact || kPair) __syncthreads();                   // LDS reused next frame
     }
     if (kSplit) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        // chunk 0 leaves its accumulator after its frames (colour and count: the state every
+        // later frame starts from) in row 0, which holds no colour of its own
+        if (chunk == 0u && c0_regs) {
+            const u32x4 v = {__float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z), n};
+            __builtin_amdgcn_raw_buffer_store_b128(v, col_rsrc, (int)(lane * 16u), 0, 16);
+        }
         // arrival: every colour of this chunk has left the CU (sc1 stores, drained), then one
         // agent-scope add; the tile's last arriver (told by the add's value) reads the other
         // chunks' colours with sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility,
-        // first row of the hand-off table) and accumulates every frame in order
+        // first row of the hand-off table) and accumulates their frames in order after chunk
+        // 0's state
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t* cnt = p.split_cnt + (size_t)lband * tiles_x + (wave_in ? tx : 0u);
         uint32_t old = 0u;
@@ -2497,19 +2511,25 @@ rt_bounce_kernel(const TraceParams p) {
         if (old + 1u == S) {
             if (lane == 0u)    // (the next launch starts after this one ends)
                 __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            c = mk(0.0f, 0.0f, 0.0f);
-            n = 0u;
-            if (!p.reset_first && valid) {
-                const float4 acc = p.in[tc.idx];
-                c = mk(acc.x, acc.y, acc.z);
-                n = f2u(acc.w);
+            if (!c0_regs) {      // every frame's colour is in the buffer
+                c = mk(0.0f, 0.0f, 0.0f);
+                n = 0u;
+                if (!p.reset_first && valid) {
+                    const float4 acc = p.in[tc.idx];
+                    c = mk(acc.x, acc.y, acc.z);
+                    n = f2u(acc.w);
+                }
+            } else if (chunk != 0u) {   // (chunk 0 arriving last holds its state in registers)
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(col_rsrc, (int)(lane * 16u),
+                                                                      0, 16);
+                c = mk(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z));
+                n = v.w;
             }
-            // the colours in batches of kMergeBatch frames, all of a batch's loads in flight
-            // before its accumulation (one dependent load per frame made the merge as long as
-            // 64 load latencies)
+            // the colours of the frames after chunk 0's state in batches of kMergeBatch
+            // frames, all of a batch's loads in flight before its accumulation (one dependent
+            // load per frame made the merge as long as 64 load latencies)
             constexpr uint32_t kMergeBatch = 8;
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            for (uint32_t f0 = 0; f0 < p.frames; f0 += kMergeBatch) {
+            for (uint32_t f0 = c0_regs ? cs : 0u; f0 < p.frames; f0 += kMergeBatch) {
                 u32x4 v[kMergeBatch];
 #pragma unroll
                 for (uint32_t j = 0; j < kMergeBatch; ++j)   // (rows past the last frame:
