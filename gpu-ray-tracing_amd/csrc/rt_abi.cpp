@@ -655,8 +655,15 @@ rt_status plan_wg_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_
 #define RT_SPLIT2_MAX_TILES 20000
 #endif
 constexpr uint64_t kSplit4MaxTiles = RT_SPLIT4_MAX_TILES, kSplit2MaxTiles = RT_SPLIT2_MAX_TILES;
+// Only the costliest tiles split: the first ceil(tiles * kSplitFrac) slots of the cost order
+// (a launch without an order: its first slots in raster order).  RT_SPLIT_FRAC (environment,
+// diagnostic) overrides the fraction.
+#ifndef RT_SPLIT_FRAC
+#define RT_SPLIT_FRAC 1.0
+#endif
 rt_status plan_split(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t stream) {
     p.split = 1;
+    p.split_tiles = 0;
     p.split_col = nullptr;
     p.split_cnt = nullptr;
     const int mode = ctx->path_compaction;
@@ -694,8 +701,16 @@ rt_status plan_split(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t s
             ctx->split_cnt_tiles = tiles;
         }
     }
+    double frac = RT_SPLIT_FRAC;
+    if (const char* e = std::getenv("RT_SPLIT_FRAC")) frac = std::atof(e);
+    const uint64_t st = std::min<uint64_t>(tiles, (uint64_t)std::ceil(tiles * std::max(0.0, frac)));
+    if (st == 0) {
+        p.compact = 0u;
+        return RT_OK;
+    }
     p.compact = 3u;
     p.split = S;
+    p.split_tiles = (uint32_t)st;
     p.split_col = ctx->split_col;
     p.split_cnt = ctx->split_cnt;
     return RT_OK;

@@ -113,6 +113,7 @@ struct TraceParams {
     // row of 64 float4 per tile and frame, [tile][frame][lane]), arrivals per tile in
     // split_cnt (zero between launches: the last arriver resets it)
     uint32_t split;
+    uint32_t split_tiles;  // the leading slots of the order that split (the rest: one unit)
     float4* split_col;
     uint32_t* split_cnt;
     uint32_t hint_frames;  // 0 = no hint

@@ -1537,12 +1537,27 @@ constexpr int kSingleDisk = RT_SINGLE_DISK;
 #endif
 
 
+// RT_SINGLE_UNIF: the one-frame kernel's per-lane selects after the hit shading (hit /
+// miss, the degenerate scatter direction, metal absorption) only in waves whose lanes
+// differ — a wave-uniform branch on a lane mask skips them otherwise
+#ifndef RT_SINGLE_UNIF
+#define RT_SINGLE_UNIF 0
+#endif
+// RT_SINGLE_AND: "some discriminant of the chunk is not negative" as the sign of the AND of
+// their bit patterns (one 2-cycle v_and per record instead of a 4-cycle v_max_i32).  Exact
+// on the camera-ray domain the host proves for these instances: every discriminant is
+// finite (|h|, sqrt(D) <= 2^53, consider_fast) and never -0 (max_bits above), so its sign bit
+// is set exactly when it is < 0.
+#ifndef RT_SINGLE_AND
+#define RT_SINGLE_AND 0
+#endif
+
 // Shading of a camera ray's hit at depth 1 (ray_color's loop body at i = 0, wgsl:266-286):
 // sets the scattered direction and attenuation, or black (metal absorbed).  r_sb / ruv are
 // the scatter's random numbers.  Lanes with !hit compute garbage that the caller drops.
 __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, v3 d,
                                           float r_sb, v3 ruv, bool hit, uint64_t hm, v3& nd,
-                                          v3& att, bool& black) {
+                                          v3& att, bool& black, bool& took_other) {
     const v3 hp = fmas(t, d, o);
     const v3 rel = sub(hp, mk(pr.x, pr.y, pr.z));
     v3 outward;                                                   // wgsl:209
@@ -1559,11 +1574,21 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
     const v3 n = front ? outward : neg(outward);
     // lambertian (wgsl:84-93), computed for every lane; the other materials below
     v3 dir = add(n, ruv);
-    if (dot(dir, dir) < 0x1.0c6f7ap-20f) dir = n;
+    const float ddir = dot(dir, dir);
+    if (!RT_SINGLE_UNIF ||
+        (__builtin_amdgcn_fcmpf(ddir, 0x1.0c6f7ap-20f, 4) & hm) != 0ull) {   // (FCMP_OLT)
+        // (the degenerate scatter direction, wgsl:89-91: per-lane selects only in a wave
+        // that has one)
+        if (RT_SINGLE_UNIF) asm volatile("");
+        if (ddir < 0x1.0c6f7ap-20f) dir = n;
+    }
     nd = dir;
     att = mk(mat.x, mat.y, mat.z);
     black = false;
+    took_other = false;
     const bool other = hit && !(mat.w < -1.0f);
+    if ((RT_SINGLE_MASKS ? (mask_not_lt(mat.w, -1.0f) & hm) : rt_ballot(other)) != 0ull)
+        took_other = true;
     if ((RT_SINGLE_MASKS ? (mask_not_lt(mat.w, -1.0f) & hm) : rt_ballot(other)) != 0ull &&
         other) {
         if (mat.w <= 1.0f) {                                      // metal wgsl:95-100
@@ -1642,12 +1667,13 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
         for (uint32_t s = 0; s < S; ++s) lblk[s * kCandStride + lane] = bv[s];
     }
     v3 cf[S], dsky[S];
-    bool black[S];
+    bool black[S], any_other[S];      // (any_other: wave-uniform, a metal / dielectric hit)
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
         cf[s] = mk(1.0f, 1.0f, 1.0f);
         dsky[s] = d[s];
         black[s] = false;
+        any_other[s] = false;
     }
     if (p.depth != 0u && !(RT_SKO & 2)) {                         // wgsl:264
         // sphere_list_hit over each tile's list, the tiles' chunks interleaved
@@ -1668,6 +1694,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
             for (uint32_t i = 0; i < m; i += K) {
                 float hh[S][K], dd[S][K];
                 int mx = (int)0x80000000;
+                uint32_t an = 0xFFFFFFFFu;   // (RT_SINGLE_AND: the AND of the bit patterns)
 #pragma unroll
                 for (uint32_t s = 0; s < S; ++s)
 #pragma unroll
@@ -1676,9 +1703,12 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                             kSingleLds<S> ? lblk[s * kCandStride + kCandRecOff + i + k]
                                           : load_rec<true>(blk[s] + kCandRecOff, i + k);
                         dd[s][k] = discriminant(g, o[s], d[s], a[s], hh[s][k]);
-                        mx = max(mx, __float_as_int(dd[s][k]));
+                        if (RT_SINGLE_AND)
+                            an &= __float_as_uint(dd[s][k]);
+                        else
+                            mx = max(mx, __float_as_int(dd[s][k]));
                     }
-                if (__builtin_expect(mx > (int)0xFF800000, 0)) {
+                if (__builtin_expect(RT_SINGLE_AND ? (int)an >= 0 : mx > (int)0xFF800000, 0)) {
 #pragma unroll
                     for (uint32_t s = 0; s < S; ++s)
 #pragma unroll
@@ -1747,10 +1777,17 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                     ruv = random_unit_vector(r_sb, sb);
                 }
                 v3 nd, att;
-                bool blk_s;
+                bool blk_s, other_s;
                 shade_hit(pr[s], mat[s], tmax[s], o[s], d[s], r_sb, ruv, hit[s], hm[s], nd,
-                          att, blk_s);
-                if (hit[s]) {                                     // wgsl:285-286
+                          att, blk_s, other_s);
+                any_other[s] = other_s;
+                if (RT_SINGLE_UNIF && RT_SINGLE_MASKS && hm[s] == live_m[s]) {
+                    // every live lane hit (a tile inside a sphere's image): no selects
+                    asm volatile("");
+                    cf[s] = att;
+                    dsky[s] = nd;
+                    black[s] = blk_s;
+                } else if (hit[s]) {                              // wgsl:285-286
                     cf[s] = att;
                     dsky[s] = nd;
                     black[s] = blk_s;
@@ -1761,7 +1798,13 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
         const v3 c = sky_w(cf[s], dsky[s]);                       // wgsl:293-296
-        col[s] = black[s] ? mk(0.0f, 0.0f, 0.0f) : c;             // wgsl:277-279
+        // (black: only metal hits absorb, so only a wave that shaded one selects)
+        if (RT_SINGLE_UNIF && !any_other[s]) {
+            asm volatile("");
+            col[s] = c;
+        } else {
+            col[s] = black[s] ? mk(0.0f, 0.0f, 0.0f) : c;         // wgsl:277-279
+        }
     }
     SST_V(5, col[S - 1].x);
 }
@@ -2263,17 +2306,27 @@ rt_bounce_kernel(const TraceParams p) {
     const uint32_t me = threadIdx.x;                    // lane in the workgroup
     const uint32_t tiles_x = (p.width + 7u) >> 3;
     uint32_t gx = blockIdx.x, lband = blockIdx.y;       // group of kW tiles
-    // kSplit: workgroup u = unit (tile slot u / S, chunk u % S); grid (tiles_x * S, bands)
-    const uint32_t S = kSplit ? p.split : 1u;
+    // kSplit: workgroup u = unit; the first p.split_tiles slots of the order (the costliest
+    // tiles) run as p.split chunks each (slot u / S, chunk u % S), every later slot as one
+    // unit (S = 1: the per-wave schedule); a one-dimensional grid of tiles + split_tiles *
+    // (S - 1) units
     const uint32_t unit = blockIdx.y * gridDim.x + blockIdx.x;
-    const uint32_t chunk = kSplit ? unit % S : 0u;
+    uint32_t S = 1u, chunk = 0u, slot = unit;
     if (kSplit) {
-        const uint32_t slot = unit / S;
+        const uint32_t su = p.split_tiles * p.split;
+        if (unit < su) {
+            S = p.split;
+            slot = unit / S;
+            chunk = unit % S;
+        } else {
+            slot = unit - su + p.split_tiles;
+        }
         gx = slot % tiles_x;
         lband = slot / tiles_x;
     }
+    const bool sp = kSplit && S > 1u;                   // (wave-uniform)
     if (p.tile_order) {                                 // costliest groups first
-        const uint32_t pos = kSplit ? unit / S : unit;
+        const uint32_t pos = slot;
         const uint32_t t = __builtin_amdgcn_readfirstlane(p.tile_order[pos]);
         gx = t & 0xFFFFu;
         lband = t >> 16;
@@ -2293,7 +2346,6 @@ rt_bounce_kernel(const TraceParams p) {
     }
     constexpr uint32_t kTiles = kPair ? 1u : kW;        // tiles per workgroup
     const uint32_t group = lband * ((tiles_x + kTiles - 1u) / kTiles) + gx;
-    // (kSplit: chunk 0's duration stands for its tile's: the chunks carry equal frames)
     if (p.tile_cost && threadIdx.x == 0u && chunk == 0u)
         p.tile_cost[group] = (uint32_t)__builtin_amdgcn_s_memtime();
     if (p.lds_records || kW > 1u) __syncthreads();
@@ -2320,10 +2372,10 @@ rt_bounce_kernel(const TraceParams p) {
     // kSplit: chunk 0 accumulates its frames in registers when none of them stores an image
     // (an image store of an early frame may go to the input buffer, p.out2, which the later
     // chunks read at their start); otherwise it stores colours like the others
-    const uint32_t cs = kSplit ? (p.frames + S - 1u) / S : p.frames;
-    const bool c0_regs = kSplit && cs < p.frames && p.store_each != 2u &&
+    const uint32_t cs = sp ? (p.frames + S - 1u) / S : p.frames;
+    const bool c0_regs = sp && cs < p.frames && p.store_each != 2u &&
                          !(p.store_each && p.frames - 2u < cs);
-    if (kSplit) {
+    if (sp) {
         f_lo = min(chunk * cs, p.frames);
         f_hi = min(f_lo + cs, p.frames);
         for (uint32_t f = 0; f < f_lo; ++f) {
@@ -2448,7 +2500,7 @@ rt_bounce_kernel(const TraceParams p) {
             if (wave == 1u) s_pair_col[lane] = make_float4(res.x, res.y, res.z, 0.0f);
             __syncthreads();
         }
-        if (kSplit && (chunk != 0u || !c0_regs)) {
+        if (sp && (chunk != 0u || !c0_regs)) {
             // the frame's colour, write-through (sc1): the tile's last arriver reads it
             // (chunk 0 accumulates its frames in registers, as the per-wave mode does)
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -2489,7 +2541,7 @@ rt_bounce_kernel(const TraceParams p) {
         }
         if (kCompact || kPair) __syncthreads();                   // LDS reused next frame
     }
-    if (kSplit) {
+    if (sp) {
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         // chunk 0 leaves its accumulator after its frames (colour and count: the state every
         // later frame starts from) in row 0, which holds no colour of its own
@@ -2561,8 +2613,11 @@ rt_bounce_kernel(const TraceParams p) {
             }
         }
     }
+    // (a split tile's cost: its chunk 0's duration times S, the chunks carrying equal frames,
+    // so that the next launch's order ranks it with the unsplit tiles)
     if (p.tile_cost && threadIdx.x == 0u && chunk == 0u)
-        p.tile_cost[group] = (uint32_t)__builtin_amdgcn_s_memtime() - p.tile_cost[group];
+        p.tile_cost[group] =
+            ((uint32_t)__builtin_amdgcn_s_memtime() - p.tile_cost[group]) * S;
     WAVE_TRACE(1);
 }
 
@@ -3064,7 +3119,7 @@ static hipError_t launch_bounce(const TraceParams& p, hipStream_t stream) {
     const void* sym = reinterpret_cast<const void*>(&rt_bounce_kernel<kBounceWave>);
     uint32_t threads = 64;
     if (p.compact == 3u) {                                    // (tile, chunk) units
-        grid.x = tiles_x * p.split;
+        grid = dim3(tiles_x * p.local_bands + p.split_tiles * (p.split - 1u), 1);
         sym = reinterpret_cast<const void*>(&rt_bounce_kernel<kBounceSplit>);
     } else if (p.compact == 1u) {
         sym = reinterpret_cast<const void*>(&rt_bounce_kernel<kBounceCompact>);

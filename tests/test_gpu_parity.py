@@ -1,6 +1,7 @@
 """GPU parity tests: the HIP path (through the C ABI) against the CPU oracle and the
 committed golden fixtures, bit for bit (NaN == NaN).  Run on a real MI355X with -m gpu."""
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -817,7 +818,11 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, s
         assert_same(got_prev, want_prev)
 
 
-BOUNCE_PATH_KERNEL = {"per_wave": 0, "compact": 1, "pair": 2, "auto": 3, "split": 3}
+BOUNCE_PATH_KERNEL = {"per_wave": 0, "compact": 1, "pair": 2, "auto": 3, "split": 3,
+                      "split_part": 3}
+# split_part: three chunks for the costliest 30 % of the tiles (the order's first slots), one
+# unit for every other tile (rt_abi.cpp plan_split, RT_BOUNCE_SPLIT / RT_SPLIT_FRAC)
+SPLIT_PART_ENV = {"RT_BOUNCE_SPLIT": "3", "RT_SPLIT_FRAC": "0.3"}
 
 
 def bounce_kernel(paths, frames_per_launch):
@@ -839,13 +844,16 @@ def _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks
     want_prev, _ = oracle.render_pixels(np.zeros((h * w, 4), np.float32), xx.ravel(),
                                         yy.ravel(), cam.blob, sc.spheres, seeds[:frames - 1])
     p = rt.ComputeShaderPipeline(0)
-    p.set_path_compaction(paths)
+    p.set_path_compaction("split" if paths == "split_part" else paths)
     p.set_frame_images(images)
     if fpl:
         p.set_frames_per_launch(fpl)
     rows0 = rt.stripe_local_rows(h, 0, nranks)
     got_new = np.zeros((h, w, 4), np.float32)
     got_prev = np.zeros((h, w, 4), np.float32)
+    saved = {k: os.environ.get(k) for k in SPLIT_PART_ENV}
+    if paths == "split_part":
+        os.environ.update(SPLIT_PART_ENV)
     try:
         for r in range(nranks):
             a, b = p.new_image(w, rows0), p.new_image(w, rows0)
@@ -863,12 +871,17 @@ def _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks
                     got_new[y], got_prev[y] = img_new[lr], img_prev[lr]
     finally:
         p.close()
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     assert_same(got_new, want_new.reshape(h, w, 4))
     if frames >= 2:
         assert_same(got_prev, want_prev.reshape(h, w, 4))
 
 
-@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "split", "auto"])
+@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "split", "split_part", "auto"])
 @pytest.mark.parametrize("w,h,depth,frames,scene,nranks", [
     (56, 40, 2, 5, "n120", 1), (67, 45, 8, 3, "default", 1), (64, 48, 3, 1, "n120", 1),
     (50, 37, 8, 6, "default", 3), (40, 32, 0, 2, "n120", 1), (72, 48, 5, 4, "three", 2)])
@@ -880,7 +893,7 @@ def test_bounce_launches_match_oracle(rt, oracle, paths, w, h, depth, frames, sc
     _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks, 0)
 
 
-@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "split"])
+@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "split", "split_part"])
 @pytest.mark.parametrize("w,h,depth,frames,scene,nranks", [
     (56, 40, 2, 5, "n120", 1), (50, 37, 8, 6, "default", 3), (72, 48, 5, 4, "three", 2)])
 @pytest.mark.parametrize("images", ["last_two", "every"])

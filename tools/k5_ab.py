@@ -2,7 +2,8 @@
 size, rank 0's share of the 3840x2160 depth-8 64-spp render, one 64-frame launch per
 measurement, the modes alternating launch by launch (so clock and power drift hits every
 mode alike); reports each mode's median and min us per step.
-usage: python tools/k5_ab.py [reps] [worlds, e.g. 4,8] [modes, e.g. per_wave,split4]"""
+usage: python tools/k5_ab.py [reps] [worlds, e.g. 4,8] [modes, e.g. per_wave,split4,split2f25]
+(split<S>f<P>: S chunks for the costliest P % of the tiles)"""
 import json
 import os
 import sys
@@ -28,8 +29,13 @@ pipe.set_spheres(sc)
 
 
 def set_mode(m):
+    # split<S>[f<percent>]: S chunks for the costliest <percent> % of the tiles (default all)
+    os.environ.pop("RT_SPLIT_FRAC", None)
     if m.startswith("split"):
-        os.environ["RT_BOUNCE_SPLIT"] = m[5:] or "4"
+        s, _, f = m[5:].partition("f")
+        os.environ["RT_BOUNCE_SPLIT"] = s or "4"
+        if f:
+            os.environ["RT_SPLIT_FRAC"] = str(int(f) / 100)
         pipe.set_path_compaction("split")
     else:
         os.environ.pop("RT_BOUNCE_SPLIT", None)
