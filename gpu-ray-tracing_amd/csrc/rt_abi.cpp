@@ -105,6 +105,10 @@ struct rt_ctx {
     float4* split_col = nullptr;
     uint32_t* split_cnt = nullptr;
     uint64_t split_col_bytes = 0, split_cnt_tiles = 0;
+    // their unit order (launch_unit_order) and its count, rebuilt when unit_key changes
+    uint32_t* unit_order = nullptr;     // unit_cap entries, then the count
+    uint64_t unit_cap = 0;
+    uint64_t unit_key[5] = {~0ull, 0, 0, 0, 0};
 };
 
 namespace {
@@ -661,9 +665,14 @@ constexpr uint64_t kSplit4MaxTiles = RT_SPLIT4_MAX_TILES, kSplit2MaxTiles = RT_S
 #ifndef RT_SPLIT_FRAC
 #define RT_SPLIT_FRAC 1.0
 #endif
+#ifndef RT_SPLIT_ALPHA
+#define RT_SPLIT_ALPHA 0.25
+#endif
 rt_status plan_split(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t stream) {
     p.split = 1;
     p.split_tiles = 0;
+    p.unit_order = nullptr;
+    p.unit_count = nullptr;
     p.split_col = nullptr;
     p.split_cnt = nullptr;
     const int mode = ctx->path_compaction;
@@ -701,8 +710,56 @@ rt_status plan_split(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t s
             ctx->split_cnt_tiles = tiles;
         }
     }
+    // With a measured tile order: the unit order (longest-processing-time-first over the
+    // units; tiles above alpha times the launch's ideal span split).  RT_SPLIT_FRAC (the
+    // first fraction of the tile order splits, no unit order) and RT_SPLIT_ALPHA: diagnostic.
+    const char* frac_env = std::getenv("RT_SPLIT_FRAC");
+    if (p.tile_order && !frac_env && p.local_bands < 4096u && ((p.width + 7u) >> 3) < 65536u) {
+        double alpha = RT_SPLIT_ALPHA;
+        if (const char* e = std::getenv("RT_SPLIT_ALPHA")) alpha = std::atof(e);
+        const uint64_t cap = tiles * S;
+        if (cap + 1 > ctx->unit_cap) {
+            hipError_t e = hipStreamSynchronize(stream);   // the old order may be in use
+            if (e == hipSuccess) {
+                (void)hipFree(ctx->unit_order);
+                ctx->unit_order = nullptr;
+                ctx->unit_cap = 0;
+                e = hipMalloc(&ctx->unit_order, (cap + 1) * sizeof(uint32_t));
+            }
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc(unit order)");
+            ctx->unit_cap = cap + 1;
+            ctx->unit_key[0] = ~0ull;
+        }
+        // (resident waves of the launch: every SIMD of the device at 8 waves)
+        static const int cus = [] {
+            int n = 0, dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                n = 256;
+            return n > 0 ? n : 256;
+        }();
+        const float k_thr = (float)(alpha / (cus * 4.0 * 8.0));
+        uint32_t kbits;
+        std::memcpy(&kbits, &k_thr, 4);
+        const uint64_t key[5] = {ctx->order_gen, ctx->order_frames, tiles, S, kbits};
+        if (!std::equal(key, key + 5, ctx->unit_key)) {
+            hipError_t e = rtk::launch_unit_order(ctx->tile_cost, ctx->unit_order,
+                                                  ctx->unit_order + cap, (uint32_t)tiles,
+                                                  (p.width + 7u) >> 3, S, k_thr, stream);
+            if (e != hipSuccess) return hip_fail(e, "rt_unit_order_kernel launch");
+            std::copy(key, key + 5, ctx->unit_key);
+        }
+        p.compact = 3u;
+        p.split = S;
+        p.split_tiles = 0;
+        p.split_col = ctx->split_col;
+        p.split_cnt = ctx->split_cnt;
+        p.unit_order = ctx->unit_order;
+        p.unit_count = ctx->unit_order + cap;
+        return RT_OK;
+    }
     double frac = RT_SPLIT_FRAC;
-    if (const char* e = std::getenv("RT_SPLIT_FRAC")) frac = std::atof(e);
+    if (frac_env) frac = std::atof(frac_env);
     const uint64_t st = std::min<uint64_t>(tiles, (uint64_t)std::ceil(tiles * std::max(0.0, frac)));
     if (st == 0) {
         p.compact = 0u;
@@ -1192,6 +1249,7 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->wg_buf);
         (void)hipFree(ctx->split_col);
         (void)hipFree(ctx->split_cnt);
+        (void)hipFree(ctx->unit_order);
         free_candidates(ctx);
         for (uint32_t k = 0; k + 1 < RT_MAX_UPDATE_QUEUES; ++k) {
             if (ctx->aux[k]) (void)hipStreamDestroy(ctx->aux[k]);

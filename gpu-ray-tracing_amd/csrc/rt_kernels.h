@@ -116,6 +116,11 @@ struct TraceParams {
     uint32_t split_tiles;  // the leading slots of the order that split (the rest: one unit)
     float4* split_col;
     uint32_t* split_cnt;
+    // compact == 3 with a measured order: the launch's units costliest first (launch_unit_order:
+    // entry = split << 31 | chunk << 28 | band << 16 | column), *unit_count of them; the grid
+    // has tiles * split workgroups and those past the count exit at once
+    const uint32_t* unit_order;
+    const uint32_t* unit_count;
     uint32_t hint_frames;  // 0 = no hint
     uint32_t hint_n[kHintFrames];
     // RN64(1 / (hint_n[f] + 1)): the accumulator's division by f32(n + 1) as one f64
@@ -230,6 +235,12 @@ const char* single_kernel_name(uint32_t pix);
 hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, uint32_t tiles,
                              uint32_t tiles_x, hipStream_t stream, uint32_t snake = 0,
                              uint32_t parts = 1);
+// The bounce split schedule's unit order (rt_kernels.hip rt_unit_order_kernel): a tile whose
+// recorded cost exceeds k_thr times the sum of all costs runs as `split` chunks of a
+// 1/split share each, and all units are ordered by their own cost, costliest first.
+hipError_t launch_unit_order(const uint32_t* tile_cost, uint32_t* unit_order,
+                             uint32_t* unit_count, uint32_t tiles, uint32_t tiles_x,
+                             uint32_t split, float k_thr, hipStream_t stream);
 // Exact fast-path self-test (rt_selftest_fastmath): cnt[5] device counters, zeroed.
 hipError_t launch_selftest(unsigned long long* cnt, uint64_t n_rand, hipStream_t stream);
 

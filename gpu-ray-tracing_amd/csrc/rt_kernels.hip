@@ -2312,7 +2312,18 @@ rt_bounce_kernel(const TraceParams p) {
     // (S - 1) units
     const uint32_t unit = blockIdx.y * gridDim.x + blockIdx.x;
     uint32_t S = 1u, chunk = 0u, slot = unit;
-    if (kSplit) {
+    bool ordered_units = false;
+    if (kSplit && p.unit_order) {
+        // the measured unit order (launch_unit_order): the costliest tiles split, every unit
+        // placed by its own cost; the grid's units past the count exit at once
+        if (unit >= __builtin_amdgcn_readfirstlane(*p.unit_count)) return;
+        const uint32_t e = __builtin_amdgcn_readfirstlane(p.unit_order[unit]);
+        gx = e & 0xFFFFu;
+        lband = (e >> 16) & 0xFFFu;
+        chunk = (e >> 28) & 7u;
+        S = (e >> 31) ? p.split : 1u;
+        ordered_units = true;
+    } else if (kSplit) {
         const uint32_t su = p.split_tiles * p.split;
         if (unit < su) {
             S = p.split;
@@ -2325,7 +2336,7 @@ rt_bounce_kernel(const TraceParams p) {
         lband = slot / tiles_x;
     }
     const bool sp = kSplit && S > 1u;                   // (wave-uniform)
-    if (p.tile_order) {                                 // costliest groups first
+    if (p.tile_order && !ordered_units) {               // costliest groups first
         const uint32_t pos = slot;
         const uint32_t t = __builtin_amdgcn_readfirstlane(p.tile_order[pos]);
         gx = t & 0xFFFFu;
@@ -2717,6 +2728,88 @@ hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, ui
     if (tiles == 0) return hipSuccess;
     hipLaunchKernelGGL(rt_tile_order_kernel, dim3(1), dim3(1024), 0, stream, tile_cost,
                        tile_order, tiles, tiles_x, snake, parts);
+    return hipGetLastError();
+}
+
+// launch_unit_order: the split bounce schedule's units by their own recorded cost (one
+// 1024-thread workgroup, the buckets of rt_tile_order_kernel).  A tile whose cost exceeds
+// thr = k_thr * (sum of all costs) — k_thr = alpha / (resident waves of the launch), i.e. alpha
+// times the launch's ideal span — becomes S chunk units of cost / S (its bucket moves 4 * log2 S
+// places: four per octave), every other tile one unit; the units are then placed costliest
+// first, a split tile's chunks side by side, so the tail after the last dispatch is bounded by
+// the costliest unit rather than by the costliest tile (longest-processing-time-first on the
+// units).  *count = the number of units.
+__global__ __launch_bounds__(1024) void rt_unit_order_kernel(const uint32_t* __restrict__ cost,
+                                                             uint32_t* __restrict__ order,
+                                                             uint32_t* __restrict__ count,
+                                                             uint32_t tiles, uint32_t tiles_x,
+                                                             uint32_t S, float k_thr) {
+    constexpr uint32_t kBuckets = 128, kWaves = 16;
+    __shared__ uint32_t hist[kBuckets * kWaves];       // [bucket][wave]
+    __shared__ uint32_t scan[1024];
+    __shared__ unsigned long long total;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6;
+    const uint32_t shift = 4u * (31u - (uint32_t)__builtin_clz(S));   // 4 * log2 S (S = 2^k)
+    auto bucket = [](uint32_t c) -> uint32_t {
+        if (c == 0u) return kBuckets - 1u;
+        const uint32_t lz = (uint32_t)__builtin_clz(c);
+        const uint32_t e = 31u - lz;
+        const uint32_t m = e >= 2u ? (c >> (e - 2u)) & 3u : (c << (2u - e)) & 3u;
+        return kBuckets - 1u - (e * 4u + m);          // descending cost
+    };
+    hist[2 * tid] = 0u;
+    hist[2 * tid + 1] = 0u;
+    if (tid == 0u) total = 0ull;
+    __syncthreads();
+    unsigned long long mine = 0ull;
+    for (uint32_t t = tid; t < tiles; t += 1024u) mine += cost[t];
+    atomicAdd(&total, mine);
+    __syncthreads();
+    const double thr_d = (double)total * (double)k_thr;
+    const uint32_t thr = thr_d >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)thr_d;
+    auto unit_bucket = [&](uint32_t c, bool& split) -> uint32_t {
+        split = S > 1u && c > thr;
+        const uint32_t b = bucket(c);
+        return split ? min(b + shift, kBuckets - 1u) : b;
+    };
+    for (uint32_t t = tid; t < tiles; t += 1024u) {
+        bool split;
+        const uint32_t b = unit_bucket(cost[t], split);
+        atomicAdd(&hist[b * kWaves + wave], split ? S : 1u);
+    }
+    __syncthreads();
+    const uint32_t a0 = hist[2 * tid], a1 = hist[2 * tid + 1];
+    uint32_t v = a0 + a1;
+    scan[tid] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024u; d <<= 1) {
+        const uint32_t add = tid >= d ? scan[tid - d] : 0u;
+        __syncthreads();
+        v += add;
+        scan[tid] = v;
+        __syncthreads();
+    }
+    const uint32_t before = v - a0 - a1;
+    hist[2 * tid] = before;
+    hist[2 * tid + 1] = before + a0;
+    if (tid == 1023u) *count = v;                      // (the inclusive total)
+    __syncthreads();
+    for (uint32_t t = tid; t < tiles; t += 1024u) {
+        bool split;
+        const uint32_t b = unit_bucket(cost[t], split);
+        const uint32_t n = split ? S : 1u;
+        const uint32_t pos = atomicAdd(&hist[b * kWaves + wave], n);
+        const uint32_t e = (split ? 0x80000000u : 0u) | ((t / tiles_x) << 16) | (t % tiles_x);
+        for (uint32_t k = 0; k < n; ++k) order[pos + k] = e | (k << 28);
+    }
+}
+
+hipError_t launch_unit_order(const uint32_t* tile_cost, uint32_t* unit_order,
+                             uint32_t* unit_count, uint32_t tiles, uint32_t tiles_x,
+                             uint32_t split, float k_thr, hipStream_t stream) {
+    if (tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(rt_unit_order_kernel, dim3(1), dim3(1024), 0, stream, tile_cost,
+                       unit_order, unit_count, tiles, tiles_x, split, k_thr);
     return hipGetLastError();
 }
 
@@ -3119,7 +3212,8 @@ static hipError_t launch_bounce(const TraceParams& p, hipStream_t stream) {
     const void* sym = reinterpret_cast<const void*>(&rt_bounce_kernel<kBounceWave>);
     uint32_t threads = 64;
     if (p.compact == 3u) {                                    // (tile, chunk) units
-        grid = dim3(tiles_x * p.local_bands + p.split_tiles * (p.split - 1u), 1);
+        grid = dim3(p.unit_order ? tiles_x * p.local_bands * p.split
+                                 : tiles_x * p.local_bands + p.split_tiles * (p.split - 1u), 1);
         sym = reinterpret_cast<const void*>(&rt_bounce_kernel<kBounceSplit>);
     } else if (p.compact == 1u) {
         sym = reinterpret_cast<const void*>(&rt_bounce_kernel<kBounceCompact>);

@@ -819,10 +819,15 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, s
 
 
 BOUNCE_PATH_KERNEL = {"per_wave": 0, "compact": 1, "pair": 2, "auto": 3, "split": 3,
-                      "split_part": 3}
+                      "split_part": 3, "split_lpt": 3}
 # split_part: three chunks for the costliest 30 % of the tiles (the order's first slots), one
-# unit for every other tile (rt_abi.cpp plan_split, RT_BOUNCE_SPLIT / RT_SPLIT_FRAC)
-SPLIT_PART_ENV = {"RT_BOUNCE_SPLIT": "3", "RT_SPLIT_FRAC": "0.3"}
+# unit for every other tile; split_lpt: once an order is measured, the unit order with a
+# threshold that splits only the costlier tiles of these small images (alpha 150: tiles above
+# ~1.8 % of the launch's total cost) — rt_abi.cpp plan_split, RT_BOUNCE_SPLIT / RT_SPLIT_FRAC /
+# RT_SPLIT_ALPHA
+SPLIT_ENV = {"split_part": {"RT_BOUNCE_SPLIT": "3", "RT_SPLIT_FRAC": "0.3"},
+             "split_lpt": {"RT_BOUNCE_SPLIT": "2", "RT_SPLIT_ALPHA": "150"}}
+SPLIT_ENV_KEYS = ("RT_BOUNCE_SPLIT", "RT_SPLIT_FRAC", "RT_SPLIT_ALPHA")
 
 
 def bounce_kernel(paths, frames_per_launch):
@@ -844,16 +849,17 @@ def _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks
     want_prev, _ = oracle.render_pixels(np.zeros((h * w, 4), np.float32), xx.ravel(),
                                         yy.ravel(), cam.blob, sc.spheres, seeds[:frames - 1])
     p = rt.ComputeShaderPipeline(0)
-    p.set_path_compaction("split" if paths == "split_part" else paths)
+    p.set_path_compaction("split" if paths in SPLIT_ENV else paths)
     p.set_frame_images(images)
     if fpl:
         p.set_frames_per_launch(fpl)
     rows0 = rt.stripe_local_rows(h, 0, nranks)
     got_new = np.zeros((h, w, 4), np.float32)
     got_prev = np.zeros((h, w, 4), np.float32)
-    saved = {k: os.environ.get(k) for k in SPLIT_PART_ENV}
-    if paths == "split_part":
-        os.environ.update(SPLIT_PART_ENV)
+    saved = {k: os.environ.get(k) for k in SPLIT_ENV_KEYS}
+    for k in SPLIT_ENV_KEYS:
+        os.environ.pop(k, None)
+    os.environ.update(SPLIT_ENV.get(paths, {}))
     try:
         for r in range(nranks):
             a, b = p.new_image(w, rows0), p.new_image(w, rows0)
@@ -881,7 +887,8 @@ def _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks
         assert_same(got_prev, want_prev.reshape(h, w, 4))
 
 
-@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "split", "split_part", "auto"])
+@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "split", "split_part",
+                                   "split_lpt", "auto"])
 @pytest.mark.parametrize("w,h,depth,frames,scene,nranks", [
     (56, 40, 2, 5, "n120", 1), (67, 45, 8, 3, "default", 1), (64, 48, 3, 1, "n120", 1),
     (50, 37, 8, 6, "default", 3), (40, 32, 0, 2, "n120", 1), (72, 48, 5, 4, "three", 2)])
@@ -893,7 +900,8 @@ def test_bounce_launches_match_oracle(rt, oracle, paths, w, h, depth, frames, sc
     _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks, 0)
 
 
-@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "split", "split_part"])
+@pytest.mark.parametrize("paths", ["per_wave", "compact", "pair", "split", "split_part",
+                                   "split_lpt"])
 @pytest.mark.parametrize("w,h,depth,frames,scene,nranks", [
     (56, 40, 2, 5, "n120", 1), (50, 37, 8, 6, "default", 3), (72, 48, 5, 4, "three", 2)])
 @pytest.mark.parametrize("images", ["last_two", "every"])

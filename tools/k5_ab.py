@@ -3,7 +3,8 @@ size, rank 0's share of the 3840x2160 depth-8 64-spp render, one 64-frame launch
 measurement, the modes alternating launch by launch (so clock and power drift hits every
 mode alike); reports each mode's median and min us per step.
 usage: python tools/k5_ab.py [reps] [worlds, e.g. 4,8] [modes, e.g. per_wave,split4,split2f25]
-(split<S>f<P>: S chunks for the costliest P % of the tiles)"""
+(split<S>f<P>: S chunks for the costliest P % of the tiles; split<S>a<P>: the unit order
+with alpha = P / 100)"""
 import json
 import os
 import sys
@@ -29,13 +30,17 @@ pipe.set_spheres(sc)
 
 
 def set_mode(m):
-    # split<S>[f<percent>]: S chunks for the costliest <percent> % of the tiles (default all)
+    # split<S>[f<P> | a<P>]: S chunks for the costliest P % of the tiles of the tile order
+    # (f), or the unit order with alpha = P / 100 (a; default: the library's alpha)
     os.environ.pop("RT_SPLIT_FRAC", None)
+    os.environ.pop("RT_SPLIT_ALPHA", None)
     if m.startswith("split"):
-        s, _, f = m[5:].partition("f")
+        rest = m[5:]
+        key = "f" if "f" in rest else "a" if "a" in rest else None
+        s, _, f = rest.partition(key) if key else (rest, "", "")
         os.environ["RT_BOUNCE_SPLIT"] = s or "4"
-        if f:
-            os.environ["RT_SPLIT_FRAC"] = str(int(f) / 100)
+        if key:
+            os.environ["RT_SPLIT_FRAC" if key == "f" else "RT_SPLIT_ALPHA"] = str(int(f) / 100)
         pipe.set_path_compaction("split")
     else:
         os.environ.pop("RT_BOUNCE_SPLIT", None)
