@@ -451,7 +451,22 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
         hipError_t e = hipMemcpyAsync(ctx->d_geom, geom.data(), geom.size() * sizeof(float4),
                                       hipMemcpyHostToDevice, stream);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(sphere geometry)");
-        e = hipMemcpyAsync(ctx->d_sph, spheres, count * sizeof(rt_sphere),
+        // The device records carry, in a dielectric's unused colour channels (wgsl:102-135
+        // reads only color[0] = ri), RN(1 / ri) and the front face's Schlick r0 =
+        // RN(RN((1 - y) / (1 + y))^2) with y = RN(1 / ri): the one-frame kernel's
+        // RT_SINGLE_DIEL reads them instead of two divisions (the same IEEE f32 operations
+        // as wgsl:104 and wgsl:137-141, so the same bits).  Dielectric = neither
+        // color[3] < -1 nor color[3] <= 1, the kernels' test (NaN included).
+        std::vector<rt_sphere> dev(spheres, spheres + count);
+        for (rt_sphere& d : dev)
+            if (!(d.color[3] < -1.0f) && !(d.color[3] <= 1.0f)) {
+                const float y = 1.0f / d.color[0];
+                float r0 = (1.0f - y) / (1.0f + y);
+                r0 = r0 * r0;
+                d.color[1] = y;
+                d.color[2] = r0;
+            }
+        e = hipMemcpyAsync(ctx->d_sph, dev.data(), count * sizeof(rt_sphere),
                            hipMemcpyHostToDevice, stream);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(sphere records)");
         e = hipStreamSynchronize(stream);

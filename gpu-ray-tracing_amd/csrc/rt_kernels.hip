@@ -1552,6 +1552,33 @@ constexpr int kSingleDisk = RT_SINGLE_DISK;
 #define RT_SINGLE_AND 0
 #endif
 
+// RT_SINGLE_DIEL: the one-frame kernel's dielectric scatter with the sphere's precomputed
+// RN(1 / ri) and front-face r0 (rt_abi.cpp upload_spheres) and checked fast square roots
+#ifndef RT_SINGLE_DIEL
+#define RT_SINGLE_DIEL 0
+#endif
+// sqrtf(x) through sqrt_core when every active lane's x is finite and >= 2^-96 (or
+// negative: both give NaN there), the IEEE operation otherwise
+constexpr uint32_t kBits2m96 = 0x0F800000u;   // 2^-96
+__device__ __forceinline__ float sqrt_checked(float x) {
+    const uint32_t b = __float_as_uint(x);
+    // out of the domain: +-0, [0, 2^-96) and +inf / NaN of either sign ... as an unsigned range
+    // on the magnitude bits: |x| < 2^-96 or |x| >= +inf
+    const uint32_t m = b & 0x7FFFFFFFu;
+    if (__builtin_amdgcn_uicmp(m - kBits2m96, 0x7F800000u - kBits2m96, 35) == 0ull)   // UGE
+        return sqrt_core(x);
+    return sqrtf(x);
+}
+// WGSL refract (rt_device.h) with sqrt_checked
+__device__ __forceinline__ v3 refract_checked(v3 e1, v3 e2, float eta) {
+    const float d = dot(e2, e1);
+    const float k = fmaf(-(eta * eta), fmaf(-d, d, 1.0f), 1.0f);
+    if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
+    const float m = fmaf(eta, d, sqrt_checked(k));
+    return mk(fmaf(eta, e1.x, -(m * e2.x)), fmaf(eta, e1.y, -(m * e2.y)),
+              fmaf(eta, e1.z, -(m * e2.z)));
+}
+
 // Shading of a camera ray's hit at depth 1 (ray_color's loop body at i = 0, wgsl:266-286):
 // sets the scattered direction and attenuation, or black (metal absorbed).  r_sb / ruv are
 // the scatter's random numbers.  Lanes with !hit compute garbage that the caller drops.
@@ -1595,6 +1622,30 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
             const v3 refl = fmas(mat.w, ruv, normalize_w<true>(reflect(d, n)));
             black = !(dot(refl, n) > 0.0f);                       // wgsl:277-279
             nd = normalize_w<true>(refl);
+        } else if (RT_SINGLE_DIEL) {                              // dielectric wgsl:102-135
+            // the sphere's RN(1 / ri) and the front face's r0 from its record (upload_spheres
+            // fills the unused colour channels of a dielectric: the same IEEE operations on
+            // the host); the square roots through sqrt_core when every lane's operand is in
+            // its domain
+            att = mk(1.0f, 1.0f, 1.0f);
+            const float ratio = front ? mat.y : mat.x;
+            const v3 u = normalize_w<true>(d);
+            const float cos_t = fminf(dot(neg(u), n), 1.0f);
+            const float s2 = fmaf(-cos_t, cos_t, 1.0f);
+            const float sin_t = sqrt_checked(s2);
+            const bool cannot = ratio * sin_t > 1.0f;
+            float r0 = mat.z;
+            if (__builtin_amdgcn_ballot_w64(!front) != 0ull) {   // (back faces: wgsl:138)
+                asm volatile("");
+                if (!front) {
+                    r0 = (1.0f - ratio) / (1.0f + ratio);
+                    r0 = r0 * r0;
+                }
+            }
+            const float x = 1.0f - cos_t;
+            const float x2 = x * x;
+            const bool refl = cannot || fmaf(1.0f - r0, (x2 * x2) * x, r0) > r_sb;
+            nd = normalize_w<true>(refl ? reflect(u, n) : refract_checked(u, n, ratio));
         } else {                                                  // dielectric wgsl:102-135
             att = mk(1.0f, 1.0f, 1.0f);
             const float ratio = front ? 1.0f / mat.x : mat.x;

@@ -246,6 +246,18 @@ def test_parallel_update_is_the_same_image(oracle):
     assert segs == 256 * 256
 
 
+@pytest.mark.parametrize("threads,band", [(1, 8), (5, 2), (64, 1)])
+def test_native_threaded_update_is_the_same_image(oracle, threads, band):
+    """bench.py's CPU baseline (oracle_update_threads: pthreads claiming row bands from a
+    shared counter, more threads than bands included) computes the golden image's bits."""
+    g = load_golden("k1.npz")
+    out, segs = oracle.update_threads(np.zeros((256, 256, 4), np.float32), g["camera"],
+                                      g["spheres"], threads, band)
+    ok, bad = bits_equal(out, g["image"])
+    assert ok, bad
+    assert segs == 256 * 256
+
+
 def test_golden_accumulator(oracle):
     g = load_golden("accum_default.npz")
     cur = g["state0"]
