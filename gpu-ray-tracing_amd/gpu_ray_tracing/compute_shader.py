@@ -265,6 +265,35 @@ class ComputeShaderPipeline:
                   ctypes.byref(newest))
         return newest.value
 
+    def bind_update_frames(self, image_a: torch.Tensor, image_b: torch.Tensor, width: int,
+                           height: int, rank: int = 0, nranks: int = 1):
+        """update_frames with the images, size and stripe fixed: the images are checked once
+        here, and the returned run(camera, spheres, seeds) -> newest issues the call with no
+        per-call validation or lookups (the host time before a call's first launch is part of
+        a short timed region).  The images must stay allocated while run is used."""
+        rows = stripe_local_rows(height, rank, nranks) if nranks > 1 else height
+        _check_image(image_a, width, rows, "image_a")
+        _check_image(image_b, width, rows, "image_b")
+        fn = _lib.lib().rt_update_frames
+        ctx, pa, pb = self._ctx, _ptr(image_a), _ptr(image_b)
+        newest = ctypes.c_int(-1)
+        pnew = ctypes.byref(newest)
+        stream = self._stream
+        spheres_of = self._spheres
+
+        def run(camera: SceneCamera, spheres: SphereCollection, seeds) -> int:
+            cam = camera.to_c()
+            p, n = spheres_of(spheres)
+            s = np.ascontiguousarray(seeds, np.float32)
+            rc = fn(ctx, pa, pb, width, height, rank, nranks, ctypes.byref(cam), p, n, s.size,
+                    _np_ptr(s), stream(), pnew)
+            if rc:
+                _lib.check(rc, "rt_update_frames")
+            return newest.value
+
+        run.images = (image_a, image_b)
+        return run
+
     def deinterleave(self, gathered: torch.Tensor, out: torch.Tensor, width: int, height: int,
                      nranks: int) -> None:
         rows = stripe_local_rows(height, 0, nranks)

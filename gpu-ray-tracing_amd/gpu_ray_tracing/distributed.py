@@ -139,6 +139,7 @@ class StripeRenderer:
         # ping-pong local accumulators, padded to rows0 so the gather is uniform
         self.buf = [pipeline.new_image(width, self.rows0), pipeline.new_image(width, self.rows0)]
         self.cur = 0
+        self._runs = None   # bound update_frames calls, per ping-pong direction
         # the root's gather and output buffers, allocated up front (finish() then runs only
         # the collective and the de-interleave kernel)
         self._gathered = self._image = None
@@ -159,9 +160,21 @@ class StripeRenderer:
     def frames(self, camera, spheres, seeds) -> None:
         """len(seeds) progressive frames, one `update` dispatch each, from a single call."""
         if self.rows:
-            a, b = self.buf[self.cur], self.buf[1 - self.cur]
-            newest = self.pipe.update_frames(a, b, self.width, self.height, camera, spheres,
-                                             seeds, self.rank, self.world)
+            run = self._runs[self.cur] if self._runs else None
+            bind = getattr(self.pipe, "bind_update_frames", None)
+            if run is None and bind is not None:
+                # (bound once per ping-pong direction: the buffers are this renderer's own)
+                run = bind(self.buf[self.cur], self.buf[1 - self.cur], self.width, self.height,
+                           self.rank, self.world)
+                if self._runs is None:
+                    self._runs = [None, None]
+                self._runs[self.cur] = run
+            if run is not None:
+                newest = run(camera, spheres, seeds)
+            else:
+                newest = self.pipe.update_frames(self.buf[self.cur], self.buf[1 - self.cur],
+                                                 self.width, self.height, camera, spheres,
+                                                 seeds, self.rank, self.world)
             if newest == 1:
                 self.cur = 1 - self.cur
         elif len(seeds) % 2:

@@ -1,5 +1,6 @@
 """Host cost of one rt_update_frames call (diagnostic): the Python wrapper
-(ComputeShaderPipeline.update_frames) against the bare ctypes call with its arguments built
+(ComputeShaderPipeline.update_frames), the bound call (bind_update_frames, what
+StripeRenderer.frames issues) and the bare ctypes call with its arguments built
 once, per K3 rank share and launch structure; the GPU is idle at each call (synchronised
 before), so the wall time is what the call costs the host before the stream runs.
 usage: python tools/host_call.py [frames]"""
@@ -42,6 +43,14 @@ for mode in ("dispatch", "chain"):
             t0 = time.perf_counter()
             pipe.update_frames(a, b, w, h, cam_t, sc, seeds[:frames], 0, world)
             py.append((time.perf_counter() - t0) * 1e6)
+        # the bound call (bind_update_frames: what StripeRenderer.frames issues)
+        run = pipe.bind_update_frames(a, b, w, h, 0, world)
+        bound = []
+        for k in range(30):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run(cam_t, sc, seeds[:frames])
+            bound.append((time.perf_counter() - t0) * 1e6)
         # the bare C call, arguments built once
         c_cam = cam_t.to_c()
         p, n = pipe._spheres(sc)
@@ -60,6 +69,7 @@ for mode in ("dispatch", "chain"):
         torch.cuda.synchronize()
         print(json.dumps({"mode": mode, "world": world, "frames": frames,
                           "python_call_us": round(sorted(py)[15], 2),
+                          "bound_call_us": round(sorted(bound)[15], 2),
                           "c_call_us": round(sorted(cc)[15], 2),
                           "launches": pipe.last_launch_info()["launches"]}), flush=True)
 pipe.close()
