@@ -246,7 +246,7 @@ def load_pmc(config, kernel, frames_per_launch):
     """The newest committed rocprofv3 PMC summary of the timed kernel (tools/pmc_bench.sh),
     if it was taken for the same kernel instance at the same frames per launch, and its
     path."""
-    for rnd in ("r03", "r02"):
+    for rnd in ("r04", "r03", "r02"):
         p = ROOT / "profiles" / f"pmc_{rnd}_{config}.json"
         if not p.exists():
             continue
@@ -259,11 +259,14 @@ def load_pmc(config, kernel, frames_per_launch):
 def load_weighted(config, kernel):
     """The weighted VALU cycles per launch of the timed kernel (tools/valu_weighted.py over
     the PMC instruction classes and the instance's disassembly), if committed."""
-    p = ROOT / "profiles" / f"valu_weighted_r03_{config}.json"
-    if not p.exists():
-        return None, None
-    d = json.loads(p.read_text())
-    return (d, p.relative_to(ROOT).as_posix()) if d.get("kernel") == kernel else (None, None)
+    for rnd in ("r04", "r03"):
+        p = ROOT / "profiles" / f"valu_weighted_{rnd}_{config}.json"
+        if not p.exists():
+            continue
+        d = json.loads(p.read_text())
+        if d.get("kernel") == kernel:
+            return d, p.relative_to(ROOT).as_posix()
+    return None, None
 
 
 def image_check(config, image, frames, cam, w, h):

@@ -2,11 +2,11 @@
 # PMC summaries of the timed trace kernel of `bench.py --config CFG` (the kernel instance and
 # frames per launch the bench line reports): FETCH_SIZE and WRITE_SIZE in separate passes
 # (MI355X_MICROARCH.md §HBM), then SQ/GRBM groups and the VALU instruction classes (two
-# passes of 8 SQ counters, read by tools/valu_weighted.py).  Writes gpurun_out/TAG/pmc_r03_CFG.json
+# passes of 8 SQ counters, read by tools/valu_weighted.py).  Writes gpurun_out/TAG/pmc_${PMC_ROUND}_CFG.json
 # (copy to profiles/ to have bench.py report `traffic` and `roofline.valu` from it).
-# Usage: bash tools/pmc_bench.sh TAG "K3 K2 K4 K5"
+# Usage: [PMC_ROUND=r04] bash tools/pmc_bench.sh TAG "K3 K2 K4 K5"
 set -o pipefail
-TAG=$1; CFGS=$2
+TAG=$1; CFGS=$2; PMC_ROUND=${PMC_ROUND:-r04}
 cd $GRAFT_REPO_ROOT; O=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
 for c in $CFGS; do
@@ -26,7 +26,7 @@ for c in $CFGS; do
       > $O/pmc_${c}_p$i.log 2>&1 || { echo "pmc $c pass $i failed"; tail -5 $O/pmc_${c}_p$i.log; exit 1; }
   done
   U=$(python3 -c "import json; print(json.loads(open('$O/pmc_bench_$c.json').read())['roofline']['kernel_avg_us'])")
-  python3 tools/pmc_bench_summary.py $O/pmc_r03_$c.json "$K" "$F" $O/raw/${c}_p*_counter_collection.csv \
+  python3 tools/pmc_bench_summary.py $O/pmc_${PMC_ROUND}_$c.json "$K" "$F" $O/raw/${c}_p*_counter_collection.csv \
     || exit 1
-  python3 -c "import json; d=json.load(open('$O/pmc_r03_$c.json')); d['kernel_avg_us']=$U; json.dump(d, open('$O/pmc_r03_$c.json','w'), indent=1)"
+  python3 -c "import json; d=json.load(open('$O/pmc_${PMC_ROUND}_$c.json')); d['kernel_avg_us']=$U; json.dump(d, open('$O/pmc_${PMC_ROUND}_$c.json','w'), indent=1)"
 done
