@@ -1686,6 +1686,14 @@ __device__ __forceinline__ v3 sky_w(v3 cf, v3 d) {
 // ncand[s] its count (kCandNone: the full list; 0 for a tile past the image edge).
 template <uint32_t S>
 constexpr bool kSingleLds = RT_SINGLE_LDS == 2 || (RT_SINGLE_LDS == 1 && S == 1);
+// RT_SINGLE_LDS_HIT: the multi-tile instance stages its tiles' candidate blocks in LDS too,
+// but for the hit records only (the scan keeps its scalar record loads): the hit sphere's
+// record is then an LDS read instead of a dependent L2 round trip before the shading
+#ifndef RT_SINGLE_LDS_HIT
+#define RT_SINGLE_LDS_HIT 0
+#endif
+template <uint32_t S>
+constexpr bool kSingleLdsHit = kSingleLds<S> || (RT_SINGLE_LDS_HIT && S > 1);
 template <uint32_t S, bool kUniRs>
 __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& cam,
                                               const TileCoord (&tc)[S],
@@ -1712,7 +1720,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
     }
     SST_V(3, d[S - 1].x);
     const uint32_t lane = threadIdx.x & 63u;
-    if (kSingleLds<S>) {
+    if (kSingleLdsHit<S>) {
         // (this wave's own LDS slots: written and read by this wave only, in order)
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s) lblk[s * kCandStride + lane] = bv[s];
@@ -1804,7 +1812,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
                 const uint32_t j = hit[s] ? (uint32_t)idx[s] : 0u;
-                if (kSingleLds<S> && ncand[s] != kCandNone) {
+                if (kSingleLdsHit<S> && ncand[s] != kCandNone) {
                     pr[s] = lblk[s * kCandStride + kCandSphOff + 2u * j];
                     mat[s] = lblk[s * kCandStride + kCandSphOff + 2u * j + 1u];
                 } else {
@@ -1948,7 +1956,7 @@ __device__ __forceinline__ void single_body(
     // need the seeds long before the scan and the accumulation need these)
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s)
-        bv[s] = (kSingleLds<S> && tx0 + s < tiles_x) ? blk[s][lane]
+        bv[s] = (kSingleLdsHit<S> && tx0 + s < tiles_x) ? blk[s][lane]
                                                       : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     // Frame chains (rt_chain.cpp): consecutive frames of a part are AQL packets with no
     // cache acquire between them, so the accumulator the previous frame stored (write-

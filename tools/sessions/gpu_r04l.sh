@@ -22,6 +22,6 @@ timeout -k 10 400 python tools/k5_ab.py 7 1,4,8 \
   || { echo k5_ab failed; exit 1; }
 cat $O/k5_ab.jsonl | python -c "import json,sys; [print(' ', d['world'], d['mode'], d['median_us'], d['min_us']) for d in map(json.loads, sys.stdin)]"
 bash tools/gpu_ab_bench.sh ${TAG}_ab "K3" 3 default $V/librt_hip_all3.so $V/librt_hip_all4.so \
-  $V/librt_hip_all5.so || exit 1
+  $V/librt_hip_all5.so $V/librt_hip_ldshit.so $V/librt_hip_all6.so || exit 1
 timeout -k 10 120 python tools/host_call.py 20 > $O/host_call.jsonl || { echo host_call failed; exit 1; }
 cat $O/host_call.jsonl
