@@ -852,7 +852,7 @@ __device__ __forceinline__ v3 sel3(bool c, v3 a, v3 b) {
 // RT_SKY_RSQ: the reciprocal of |v| in the sky's normalize(d).y and in normalize_w from the
 // square root's own rsq (sqrt_core_rcp) instead of a second transcendental (v_rcp)
 #ifndef RT_SKY_RSQ
-#define RT_SKY_RSQ 0
+#define RT_SKY_RSQ 1
 #endif
 // normalize(v) = v / sqrt(v.v) (WGSL normalize).  kFast: when every active lane's |v|^2 is
 // in [2^-20, 2^40] (NaN, 0 and inf are not) and its components are >= 2^-100 in
@@ -1486,7 +1486,7 @@ constexpr uint32_t kSingleWg = RT_SINGLE_WG;
 #endif
 // records per tile and step of the joint list walk (both tiles' lists in one loop)
 #ifndef RT_SINGLE_CHUNK
-#define RT_SINGLE_CHUNK RT_LIST_CHUNK
+#define RT_SINGLE_CHUNK 1
 #endif
 // skip the hit shading of a tile none of whose rays hit
 #ifndef RT_SINGLE_GATE
@@ -1541,7 +1541,7 @@ constexpr int kSingleDisk = RT_SINGLE_DISK;
 // miss, the degenerate scatter direction, metal absorption) only in waves whose lanes
 // differ — a wave-uniform branch on a lane mask skips them otherwise
 #ifndef RT_SINGLE_UNIF
-#define RT_SINGLE_UNIF 0
+#define RT_SINGLE_UNIF 1
 #endif
 // RT_SINGLE_AND: "some discriminant of the chunk is not negative" as the sign of the AND of
 // their bit patterns (one 2-cycle v_and per record instead of a 4-cycle v_max_i32).  Exact
@@ -1549,7 +1549,7 @@ constexpr int kSingleDisk = RT_SINGLE_DISK;
 // finite (|h|, sqrt(D) <= 2^53, consider_fast) and never -0 (max_bits above), so its sign bit
 // is set exactly when it is < 0.
 #ifndef RT_SINGLE_AND
-#define RT_SINGLE_AND 0
+#define RT_SINGLE_AND 1
 #endif
 
 // RT_SINGLE_DIEL: the one-frame kernel's dielectric scatter with the sphere's precomputed
