@@ -850,7 +850,10 @@ __device__ __forceinline__ v3 sel3(bool c, v3 a, v3 b) {
 }
 
 // RT_SKY_RSQ: the reciprocal of |v| in the sky's normalize(d).y and in normalize_w from the
-// square root's own rsq (sqrt_core_rcp) instead of a second transcendental (v_rcp)
+// square root's own rsq (sqrt_core_rcp) instead of a second transcendental (v_rcp).  On by
+// default since round 4, with RT_SINGLE_UNIF, RT_SINGLE_AND and RT_SINGLE_CHUNK = 1 (the
+// "all4" build: K3 14.95 -> 14.68 µs per update over three interleaved rounds, 816 GPU tests
+// green on it; profiles/r04/r04k_ab_single_variants.txt)
 #ifndef RT_SKY_RSQ
 #define RT_SKY_RSQ 1
 #endif
@@ -1484,7 +1487,8 @@ constexpr uint32_t kSingleWg = RT_SINGLE_WG;
 #ifndef RT_SINGLE_SCAN
 #define RT_SINGLE_SCAN 0
 #endif
-// records per tile and step of the joint list walk (both tiles' lists in one loop)
+// records per tile and step of the joint list walk (both tiles' lists in one loop): 1 since
+// round 4 (fewer padding records tested when the two lists differ in length; see RT_SKY_RSQ)
 #ifndef RT_SINGLE_CHUNK
 #define RT_SINGLE_CHUNK 1
 #endif
@@ -1539,7 +1543,8 @@ constexpr int kSingleDisk = RT_SINGLE_DISK;
 
 // RT_SINGLE_UNIF: the one-frame kernel's per-lane selects after the hit shading (hit /
 // miss, the degenerate scatter direction, metal absorption) only in waves whose lanes
-// differ — a wave-uniform branch on a lane mask skips them otherwise
+// differ — a wave-uniform branch on a lane mask skips them otherwise (default since round 4,
+// see RT_SKY_RSQ)
 #ifndef RT_SINGLE_UNIF
 #define RT_SINGLE_UNIF 1
 #endif
@@ -1547,7 +1552,7 @@ constexpr int kSingleDisk = RT_SINGLE_DISK;
 // their bit patterns (one 2-cycle v_and per record instead of a 4-cycle v_max_i32).  Exact
 // on the camera-ray domain the host proves for these instances: every discriminant is
 // finite (|h|, sqrt(D) <= 2^53, consider_fast) and never -0 (max_bits above), so its sign bit
-// is set exactly when it is < 0.
+// is set exactly when it is < 0.  (Default since round 4, see RT_SKY_RSQ.)
 #ifndef RT_SINGLE_AND
 #define RT_SINGLE_AND 1
 #endif
