@@ -1697,6 +1697,13 @@ constexpr bool kSingleLds = RT_SINGLE_LDS == 2 || (RT_SINGLE_LDS == 1 && S == 1)
 #ifndef RT_SINGLE_LDS_HIT
 #define RT_SINGLE_LDS_HIT 0
 #endif
+// RT_SINGLE_SPREF: the joint list walk also loads each entry's 32-B sphere record with scalar
+// loads beside its scan record (wave-uniform: the entry is the tile's), and a lane whose best
+// hit changes keeps that record in VGPRs — the shading then starts without the dependent
+// load of the hit record after the scan
+#ifndef RT_SINGLE_SPREF
+#define RT_SINGLE_SPREF 0
+#endif
 template <uint32_t S>
 constexpr bool kSingleLdsHit = kSingleLds<S> || (RT_SINGLE_LDS_HIT && S > 1);
 template <uint32_t S, bool kUniRs>
@@ -1743,20 +1750,28 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
         // sphere_list_hit over each tile's list, the tiles' chunks interleaved
         float tmax[S], a[S], ya[S];
         int idx[S];
+        // (RT_SINGLE_SPREF: the current best entry's sphere record, taken from the scalar
+        // loads issued beside its scan record)
+        float4 bpr[S], bmat[S];
+        bool pref = false;
         bool joint = true;
         uint32_t m = 0;
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s) {
             tmax[s] = 0x1.05ed2ep+118f;                           // 3.4e35 (wgsl:266)
             idx[s] = -1;
+            bpr[s] = bmat[s] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             a[s] = dot(d[s], d[s]);
             ya[s] = rcp_refined(a[s]);
             joint = joint && ncand[s] != kCandNone;
             m = max(m, ncand[s]);
         }
         if (RT_SINGLE_SCAN == 0 && joint) {
+            constexpr bool kPref = RT_SINGLE_SPREF && !kSingleLdsHit<S>;
+            pref = kPref;
             for (uint32_t i = 0; i < m; i += K) {
                 float hh[S][K], dd[S][K];
+                float4 spr[S][K], smat[S][K];
                 int mx = (int)0x80000000;
                 uint32_t an = 0xFFFFFFFFu;   // (RT_SINGLE_AND: the AND of the bit patterns)
 #pragma unroll
@@ -1766,6 +1781,10 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                         const float4 g =
                             kSingleLds<S> ? lblk[s * kCandStride + kCandRecOff + i + k]
                                           : load_rec<true>(blk[s] + kCandRecOff, i + k);
+                        if (kPref) {   // (entry i + k's sphere record: wave-uniform, scalar)
+                            spr[s][k] = load_rec<true>(blk[s] + kCandSphOff, 2u * (i + k));
+                            smat[s][k] = load_rec<true>(blk[s] + kCandSphOff, 2u * (i + k) + 1u);
+                        }
                         dd[s][k] = discriminant(g, o[s], d[s], a[s], hh[s][k]);
                         if (RT_SINGLE_AND)
                             an &= __float_as_uint(dd[s][k]);
@@ -1777,9 +1796,15 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                     for (uint32_t s = 0; s < S; ++s)
 #pragma unroll
                         for (int k = 0; k < K; ++k)
-                            if (i + k < ncand[s])
+                            if (i + k < ncand[s]) {
+                                const int before = idx[s];
                                 consider_fast(dd[s][k], hh[s][k], a[s], ya[s], i + k, tmax[s],
                                               idx[s]);
+                                if (kPref && idx[s] != before) {
+                                    bpr[s] = spr[s][k];
+                                    bmat[s] = smat[s][k];
+                                }
+                            }
                 }
             }
         } else {
@@ -1817,7 +1842,10 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
                 const uint32_t j = hit[s] ? (uint32_t)idx[s] : 0u;
-                if (kSingleLdsHit<S> && ncand[s] != kCandNone) {
+                if (pref) {   // (the joint walk kept them: no load after the scan)
+                    pr[s] = bpr[s];
+                    mat[s] = bmat[s];
+                } else if (kSingleLdsHit<S> && ncand[s] != kCandNone) {
                     pr[s] = lblk[s * kCandStride + kCandSphOff + 2u * j];
                     mat[s] = lblk[s * kCandStride + kCandSphOff + 2u * j + 1u];
                 } else {
