@@ -213,3 +213,71 @@ def test_header_layout_locks_compile_in_c(tmp_path):
     ok = subprocess.run(["g++", "-std=c++17", "-I", str(HEADER.parent), "-c", str(cpp), "-o",
                          str(tmp_path / "c.o")], capture_output=True, text=True)
     assert ok.returncode == 0, ok.stderr
+
+
+def test_bound_update_frames_passes_the_same_arguments(rt, monkeypatch):
+    """bind_update_frames (what StripeRenderer.frames issues) hands rt_update_frames the
+    same arguments as ComputeShaderPipeline.update_frames, reports the newest image the same
+    way, and raises on a failing status — checked without a device against a stand-in for
+    the library function (the GPU tests run both through the real one)."""
+    import gpu_ray_tracing.compute_shader as cs
+
+    calls = []
+
+    def fake_update_frames(*args):
+        flat = []
+        for a in args:
+            if isinstance(a, ctypes.c_void_p):
+                flat.append(("ptr", a.value))
+            elif type(a).__name__ == "CArgObject":          # ctypes.byref(...)
+                obj = a._obj
+                flat.append(("ref", bytes(obj) if not isinstance(obj, ctypes.c_int) else "int"))
+                if isinstance(obj, ctypes.c_int):
+                    obj.value = 1
+            else:
+                flat.append(a)
+        calls.append(flat)
+        return fake_update_frames.status
+
+    fake_update_frames.status = 0
+
+    class FakeLib:
+        rt_update_frames = staticmethod(fake_update_frames)
+
+        @staticmethod
+        def rt_last_error():
+            return b"stand-in failure"
+
+    class FakeImage:
+        def __init__(self, addr):
+            self.addr = addr
+
+        def data_ptr(self):
+            return self.addr
+
+    sc = rt.SphereCollection.generate(rt.SCENE_DEFAULT, 0, 1)
+    cam = rt.SceneCamera.from_settings(rt.CameraSettings(), 64, 48, 0.25)
+    seeds = np.array([0.25, 0.5, 0.75], np.float32)
+    monkeypatch.setattr(cs._lib, "lib", lambda: FakeLib)
+    monkeypatch.setattr(cs, "_check_image", lambda *a: None)
+    pipe = object.__new__(cs.ComputeShaderPipeline)
+    pipe._ctx = ctypes.c_void_p(0x1234)
+    pipe._sphere_keep = None
+    monkeypatch.setattr(pipe, "_stream", lambda: ctypes.c_void_p(0x77))
+    monkeypatch.setattr(cs, "stripe_local_rows", lambda h, r, n: (h + n - 1) // n)
+    a, b = FakeImage(0x1000), FakeImage(0x2000)
+    newest_plain = pipe.update_frames(a, b, 64, 48, cam, sc, seeds, 1, 3)
+    run = pipe.bind_update_frames(a, b, 64, 48, 1, 3)
+    newest_bound = run(cam, sc, seeds)
+    assert newest_plain == newest_bound == 1
+    assert len(calls) == 2
+    # (contiguous float32 spheres and seeds are passed without copies: the same addresses)
+    plain, bound = calls
+    assert len(plain) == len(bound) == 14
+    assert plain == bound
+    fake_update_frames.status = 3
+    try:
+        with pytest.raises(Exception, match="stand-in failure"):
+            run(cam, sc, seeds)
+    finally:
+        pipe._ctx = ctypes.c_void_p()   # (no context to destroy: close() skips a null one)
