@@ -662,13 +662,18 @@ rt_status plan_wg_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_
 // waves resident per SIMD on average); S times as many, S times shorter waves keep them
 // busy to the end.  S = 4 up to kSplit4MaxTiles tiles per launch, 2 up to kSplit2MaxTiles,
 // else 1 (per wave; RT_PATHS_SPLIT forces at least 2); never more chunks than frames.
-// RT_BOUNCE_SPLIT (environment, diagnostic) overrides S.  Measured (tools/k5_ab.py, 64-frame
-// K5 launches, the modes interleaved launch by launch, 7 each; profiles/r04/k5_ab_r04e.jsonl):
-// 8-rank share per wave 4 635 µs, S = 2 4 422, S = 4 4 821, S = 8 4 970; 4-rank share per
-// wave 8 010, S = 2 8 388, S = 4 9 490 — the chunks' scratch traffic, merges and extra wave
-// starts cost more than the shorter tail saves except for two chunks at 8 ranks.
+// RT_BOUNCE_SPLIT (environment, diagnostic) overrides S.  With a measured tile order only the
+// costliest tiles split (the unit order below).  Measured (tools/k5_ab.py, 64-frame K5
+// launches, the modes interleaved launch by launch): every tile split, first build
+// (profiles/r04/k5_ab_r04e.jsonl): 8-rank share per wave 4 635 µs, S = 2 4 422, S = 4 4 821,
+// S = 8 4 970; 4-rank per wave 8 010, S = 2 8 388 — the chunks' hand-off traffic, merges and
+// extra wave starts cost more than the shorter tail saves.  The unit order
+// (profiles/r04/r04l_k5_unit_order.jsonl, 7 launches each): 8-rank share per wave 4 593, every
+// tile in 2 chunks 4 447, the unit order with S = 4 and alpha 0.25 4 253 (0.879 of the 1-GPU
+// per-wave rate); 4-rank per wave 7 896 against 8 008, whole image 29 911 against 30 185 — so
+// AUTO splits (S = 4, unit order) shares of at most 20 000 tiles and runs larger ones per wave.
 #ifndef RT_SPLIT4_MAX_TILES
-#define RT_SPLIT4_MAX_TILES 0
+#define RT_SPLIT4_MAX_TILES 20000
 #endif
 #ifndef RT_SPLIT2_MAX_TILES
 #define RT_SPLIT2_MAX_TILES 20000
@@ -680,6 +685,8 @@ constexpr uint64_t kSplit4MaxTiles = RT_SPLIT4_MAX_TILES, kSplit2MaxTiles = RT_S
 #ifndef RT_SPLIT_FRAC
 #define RT_SPLIT_FRAC 1.0
 #endif
+// alpha: a tile splits when its recorded cost exceeds alpha times the launch's ideal span
+// (the sum of all costs over the device's resident waves); 0.25 measured best with S = 4
 #ifndef RT_SPLIT_ALPHA
 #define RT_SPLIT_ALPHA 0.25
 #endif

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Round 4, session m (sessions l and z in one call, for a pool with few free boxes): the -m gpu
 # suite and smoke() on the committed build (unit-order split schedule, the one-frame kernel's
-# round-4 defaults, bind_update_frames), the K5 A/B of the unit order's alpha at 1, 4 and 8
-# ranks, the K3 A/B of the diel / ldshit / spref variants against the defaults, the driver's
+# round-4 defaults, bind_update_frames), the K5 A/B of AUTO (S = 4 with the unit order for
+# shares of at most 20 000 tiles) against per wave at 1, 4 and 8 ranks, the driver's
 # bench command twice and the default bench line, the driver command's rocprofv3 kernel
 # trace, the PMC passes of the timed K3 kernel, and the host cost per call.
 # Usage: bash tools/sessions/gpu_r04m.sh TAG
@@ -17,11 +17,9 @@ tail -2 $O/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 \
   || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-timeout -k 10 400 python tools/k5_ab.py 5 1,4,8 per_wave,split2f100,split2a25,split2a50,split2a100 \
+timeout -k 10 400 python tools/k5_ab.py 7 1,4,8 per_wave,auto \
   > $O/k5_ab.jsonl || { echo k5_ab failed; exit 1; }
 cat $O/k5_ab.jsonl | python -c "import json,sys; [print(' ', d['world'], d['mode'], d['median_us'], d['min_us']) for d in map(json.loads, sys.stdin)]"
-bash tools/gpu_ab_bench.sh ${TAG}_ab "K3" 3 default $V/librt_hip_diel.so $V/librt_hip_ldshit.so \
-  $V/librt_hip_spref.so || exit 1
 for r in 1 2; do
   t0=$(date +%s.%N)
   timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver_$r.json 2> $O/bench_driver_$r.err \
