@@ -705,6 +705,9 @@ rt_status plan_split(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t s
     if (mode == RT_PATHS_SPLIT) S = std::max(S, 2u);
     if (const char* e = std::getenv("RT_BOUNCE_SPLIT")) S = (uint32_t)std::max(1L, std::atol(e));
     S = std::min(S, p.frames);
+    // AUTO splits only with a measured order (the unit order below): a launch without one runs
+    // per wave, so the costs it records are whole tiles', not a chunk's scaled by S
+    if (mode == RT_PATHS_AUTO && !p.tile_order && !std::getenv("RT_SPLIT_FRAC")) S = 1u;
     if (S <= 1u || tiles == 0) {
         p.compact = 0u;
         return RT_OK;

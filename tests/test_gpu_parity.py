@@ -402,11 +402,11 @@ def test_bench_k5_launches_match_golden(rt):
                                          (8, "per_wave")])
 def test_bench_k5_shares_match_golden(rt, world, paths):
     """bench.py --config K5 per rank: rank 0's stripe share of the 64-spp 3840x2160 depth-8
-    render (one 64-frame bounce launch), AUTO splitting each tile's frames into two chunks on
-    separate waves for 8-rank shares (forced on the whole image and a 4-rank share), per wave
-    otherwise — the fixture's sampled pixels that fall in rank 0's bands,
-    bit for bit, on two consecutive steps (the second runs the cost order the first
-    measured; the arrival counters are reused)."""
+    render (one 64-frame bounce launch) — the fixture's sampled pixels that fall in rank 0's
+    bands, bit for bit, on two consecutive steps: the first runs per wave under AUTO and
+    measures the tile costs, the second runs the cost order (AUTO on an 8-rank share: the split
+    schedule's unit order, the costliest tiles in four chunks on separate waves; the arrival
+    counters are reused).  Forced splits on the whole image and a 4-rank share."""
     g = load_golden("k5.npz")
     w, h = int(g["width"]), int(g["height"])
     p = rt.ComputeShaderPipeline(0)
@@ -421,7 +421,7 @@ def test_bench_k5_shares_match_golden(rt, world, paths):
             newest = p.update_frames(a, b, w, h, rt.SceneCamera(g["camera"]),
                                      rt.SphereCollection(g["spheres"]), g["seeds"], 0, world)
             info = p.last_launch_info()
-            split = paths == "split" or (paths == "auto" and world >= 8)
+            split = paths == "split" or (paths == "auto" and world >= 8 and step == 1)
             assert info["kernel_name"] == ("rt_bounce_kernel<3>" if split
                                            else "rt_bounce_kernel<0>"), info
             img = host(b if newest == 1 else a)
@@ -818,7 +818,10 @@ def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, s
         assert_same(got_prev, want_prev)
 
 
-BOUNCE_PATH_KERNEL = {"per_wave": 0, "compact": 1, "pair": 2, "auto": 3, "split": 3,
+# (AUTO splits only once a launch has measured the tile costs: each launch of
+# _check_bounce_launches without frames_per_launch is the first of its candidate generation,
+# so AUTO runs per wave there; the K5 share test covers its split on the second step)
+BOUNCE_PATH_KERNEL = {"per_wave": 0, "compact": 1, "pair": 2, "auto": 0, "split": 3,
                       "split_part": 3, "split_lpt": 3}
 # split_part: three chunks for the costliest 30 % of the tiles (the order's first slots), one
 # unit for every other tile; split_lpt: once an order is measured, the unit order with a
