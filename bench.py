@@ -362,9 +362,10 @@ def driver_record_sides(device, stream, main_cfg, main_us):
             pipe.set_frame_images("last_two")
             r = StripeRenderer(pipe, w, h, 0, world)
             r.frames(cam, sc, seeds)                   # records the tile costs
-            # (each call restarts from the camera's reset; the median of three launches)
-            runs = sorted(timed(stream, lambda: r.frames(cam, sc, seeds)) for _ in range(3))
-            t = runs[1]
+            r.frames(cam, sc, seeds)                   # builds the order (and its buffers)
+            # (each call restarts from the camera's reset; the median of five launches)
+            runs = sorted(timed(stream, lambda: r.frames(cam, sc, seeds)) for _ in range(5))
+            t = runs[2]
             info = pipe.last_launch_info()
             return {"us_per_step": round(t * 1e6, 1), "us_per_spp": round(t / 64 * 1e6, 2),
                     "runs_us": [round(x * 1e6, 1) for x in runs],
@@ -382,7 +383,8 @@ def driver_record_sides(device, stream, main_cfg, main_us):
         k5 = k5_share(1)
         out["k5"] = dict(k5, Mrays_per_s=round(3840 * 2160 * 64 / k5["us_per_step"], 1),
                          what="one 64-spp 3840x2160 depth-8 step (one 64-frame bounce launch, "
-                              "cost-ordered by the step before), 512 sampled pixels")
+                              "cost-ordered by the steps before; the median of five), 512 "
+                              "sampled pixels")
         shares = {"K3": {}, "K5": {}}
         base = {"dispatch": main_us if main_cfg == "K3" else None}
         for mode in ("dispatch", "chain"):
