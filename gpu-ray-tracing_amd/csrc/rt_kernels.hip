@@ -1557,6 +1557,14 @@ constexpr int kSingleDisk = RT_SINGLE_DISK;
 #define RT_SINGLE_AND 1
 #endif
 
+// RT_SINGLE_SKYDD: the sky's |d|^2 (wgsl:294's normalize) taken from where the direction was
+// made — the camera ray's a = d.d (wgsl:184, computed for the scan), the Lambertian scatter's
+// |n + ruv|^2 (computed for its degenerate-direction test, wgsl:89), or the normalised
+// metal / dielectric direction's own dot — instead of one more dot product per pixel (the
+// same operations on the same operands: the same bits)
+#ifndef RT_SINGLE_SKYDD
+#define RT_SINGLE_SKYDD 0
+#endif
 // RT_SINGLE_DIEL: the one-frame kernel's dielectric scatter with the sphere's precomputed
 // RN(1 / ri) and front-face r0 (rt_abi.cpp upload_spheres) and checked fast square roots
 #ifndef RT_SINGLE_DIEL
@@ -1589,7 +1597,7 @@ __device__ __forceinline__ v3 refract_checked(v3 e1, v3 e2, float eta) {
 // the scatter's random numbers.  Lanes with !hit compute garbage that the caller drops.
 __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, v3 d,
                                           float r_sb, v3 ruv, bool hit, uint64_t hm, v3& nd,
-                                          v3& att, bool& black, bool& took_other) {
+                                          v3& att, bool& black, bool& took_other, float& ndd) {
     const v3 hp = fmas(t, d, o);
     const v3 rel = sub(hp, mk(pr.x, pr.y, pr.z));
     v3 outward;                                                   // wgsl:209
@@ -1607,12 +1615,16 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
     // lambertian (wgsl:84-93), computed for every lane; the other materials below
     v3 dir = add(n, ruv);
     const float ddir = dot(dir, dir);
+    ndd = ddir;                     // |nd|^2 for the sky (RT_SINGLE_SKYDD)
     if (!RT_SINGLE_UNIF ||
         (__builtin_amdgcn_fcmpf(ddir, 0x1.0c6f7ap-20f, 4) & hm) != 0ull) {   // (FCMP_OLT)
         // (the degenerate scatter direction, wgsl:89-91: per-lane selects only in a wave
         // that has one)
         if (RT_SINGLE_UNIF) asm volatile("");
-        if (ddir < 0x1.0c6f7ap-20f) dir = n;
+        if (ddir < 0x1.0c6f7ap-20f) {
+            dir = n;
+            ndd = dot(n, n);
+        }
     }
     nd = dir;
     att = mk(mat.x, mat.y, mat.z);
@@ -1627,6 +1639,7 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
             const v3 refl = fmas(mat.w, ruv, normalize_w<true>(reflect(d, n)));
             black = !(dot(refl, n) > 0.0f);                       // wgsl:277-279
             nd = normalize_w<true>(refl);
+            ndd = dot(nd, nd);
         } else if (RT_SINGLE_DIEL) {                              // dielectric wgsl:102-135
             // the sphere's RN(1 / ri) and the front face's r0 from its record (upload_spheres
             // fills the unused colour channels of a dielectric: the same IEEE operations on
@@ -1651,6 +1664,7 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
             const float x2 = x * x;
             const bool refl = cannot || fmaf(1.0f - r0, (x2 * x2) * x, r0) > r_sb;
             nd = normalize_w<true>(refl ? reflect(u, n) : refract_checked(u, n, ratio));
+            ndd = dot(nd, nd);
         } else {                                                  // dielectric wgsl:102-135
             att = mk(1.0f, 1.0f, 1.0f);
             const float ratio = front ? 1.0f / mat.x : mat.x;
@@ -1660,13 +1674,13 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
             const bool cannot = ratio * sin_t > 1.0f;
             const bool refl = cannot || reflectance(cos_t, ratio) > r_sb;
             nd = normalize_w<true>(refl ? reflect(u, n) : refract(u, n, ratio));
+            ndd = dot(nd, nd);
         }
     }
 }
 
 // normalize(d).y of the sky (wgsl:293-296) and its colour times cf
-__device__ __forceinline__ v3 sky_w(v3 cf, v3 d) {
-    const float dd = dot(d, d);
+__device__ __forceinline__ v3 sky_w(v3 cf, v3 d, float dd) {
     float uy;
     if (rt_ballot(__float_as_uint(dd) - kBits2m20 >= kBits2p40 - kBits2m20) == 0ull) {
         if (RT_SKY_RSQ) {
@@ -1684,6 +1698,7 @@ __device__ __forceinline__ v3 sky_w(v3 cf, v3 d) {
     const float om = 1.0f - a;
     return mul(cf, mk(fmaf(a, 0.5f, om), fmaf(a, 0x1.666666p-1f, om), fmaf(a, 1.0f, om)));
 }
+__device__ __forceinline__ v3 sky_w(v3 cf, v3 d) { return sky_w(cf, d, dot(d, d)); }
 
 // One sample of kSinglePix pixels per lane (get_ray + ray_color at depth <= 1).  seed[s] =
 // 1 + n + B (wgsl:353) of pixel s; kUniRs: every live pixel holds the hinted count, and the
@@ -1738,11 +1753,13 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
         for (uint32_t s = 0; s < S; ++s) lblk[s * kCandStride + lane] = bv[s];
     }
     v3 cf[S], dsky[S];
+    float ddsky[S];                   // |dsky|^2 (RT_SINGLE_SKYDD)
     bool black[S], any_other[S];      // (any_other: wave-uniform, a metal / dielectric hit)
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
         cf[s] = mk(1.0f, 1.0f, 1.0f);
         dsky[s] = d[s];
+        ddsky[s] = dot(d[s], d[s]);   // (wgsl:184's a as well)
         black[s] = false;
         any_other[s] = false;
     }
@@ -1761,7 +1778,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
             tmax[s] = 0x1.05ed2ep+118f;                           // 3.4e35 (wgsl:266)
             idx[s] = -1;
             bpr[s] = bmat[s] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            a[s] = dot(d[s], d[s]);
+            a[s] = ddsky[s];
             ya[s] = rcp_refined(a[s]);
             joint = joint && ncand[s] != kCandNone;
             m = max(m, ncand[s]);
@@ -1870,18 +1887,21 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                 }
                 v3 nd, att;
                 bool blk_s, other_s;
+                float ndd;
                 shade_hit(pr[s], mat[s], tmax[s], o[s], d[s], r_sb, ruv, hit[s], hm[s], nd,
-                          att, blk_s, other_s);
+                          att, blk_s, other_s, ndd);
                 any_other[s] = other_s;
                 if (RT_SINGLE_UNIF && RT_SINGLE_MASKS && hm[s] == live_m[s]) {
                     // every live lane hit (a tile inside a sphere's image): no selects
                     asm volatile("");
                     cf[s] = att;
                     dsky[s] = nd;
+                    ddsky[s] = ndd;
                     black[s] = blk_s;
                 } else if (hit[s]) {                              // wgsl:285-286
                     cf[s] = att;
                     dsky[s] = nd;
+                    ddsky[s] = ndd;
                     black[s] = blk_s;
                 }
             }
@@ -1889,7 +1909,8 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
     }
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
-        const v3 c = sky_w(cf[s], dsky[s]);                       // wgsl:293-296
+        const v3 c = RT_SINGLE_SKYDD ? sky_w(cf[s], dsky[s], ddsky[s])  // wgsl:293-296
+                                     : sky_w(cf[s], dsky[s]);
         // (black: only metal hits absorb, so only a wave that shaded one selects)
         if (RT_SINGLE_UNIF && !any_other[s]) {
             asm volatile("");
