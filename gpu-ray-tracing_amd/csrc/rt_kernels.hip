@@ -1561,9 +1561,11 @@ constexpr int kSingleDisk = RT_SINGLE_DISK;
 // made — the camera ray's a = d.d (wgsl:184, computed for the scan), the Lambertian scatter's
 // |n + ruv|^2 (computed for its degenerate-direction test, wgsl:89), or the normalised
 // metal / dielectric direction's own dot — instead of one more dot product per pixel (the
-// same operations on the same operands: the same bits)
+// same operations on the same operands: the same bits).  Default since round 4: 828 GPU
+// tests green on it; K3 14.51 against 14.56 µs per update at the default length, 15.93
+// against 16.37 in the driver's command (profiles/r04/r04p_ab_skydd.txt, three rounds each)
 #ifndef RT_SINGLE_SKYDD
-#define RT_SINGLE_SKYDD 0
+#define RT_SINGLE_SKYDD 1
 #endif
 // RT_SINGLE_DIEL: the one-frame kernel's dielectric scatter with the sphere's precomputed
 // RN(1 / ri) and front-face r0 (rt_abi.cpp upload_spheres) and checked fast square roots
