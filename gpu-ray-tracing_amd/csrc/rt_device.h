@@ -74,9 +74,10 @@ RT_HD float flip_sign(float x, uint32_t m) {
 // k1s / k1c: the leading coefficients of the two polynomials, -0x1.9943f2p-13f and
 // 0x1.99eb9cp-16f, passed in so that a kernel can keep them in registers (sincos_c below
 // passes the literals; the arithmetic is the same either way).
-RT_HD void sincos_k(float x, float& s, float& c, float k1s, float k1c) {
+// finite: x is known finite (no NaN guard on the quadrant; the same bits for finite x)
+RT_HD void sincos_k(float x, float& s, float& c, float k1s, float k1c, bool finite = false) {
     const float q = rintf(x * 0x1.45f306p-1f);
-    const int k = (q == q) ? (int)q : 0;
+    const int k = (finite || q == q) ? (int)q : 0;
     float r = fmaf(q, -0x1.921fb6p+0f, x);
     r = fmaf(q, 0x1.777a5cp-25f, r);
     r = fmaf(q, 0x1p-49f, r);

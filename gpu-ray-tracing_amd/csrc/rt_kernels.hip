@@ -807,6 +807,10 @@ __device__ __forceinline__ void disk_unit(float sa, float ca, float& ux, float& 
     }
 }
 
+// RT_SINCOS_FIN: no NaN guard on the lens sample's quadrant in get_ray (its angle is finite)
+#ifndef RT_SINCOS_FIN
+#define RT_SINCOS_FIN 0
+#endif
 // get_ray (wgsl:305-325) with the pixel-invariant hash(hash(x*73) ^ hash(y*51)) part
 // precomputed per pixel: seed = hash(hxy ^ su), su = sample_index*25 + B (wave-uniform
 // when every pixel of the wave holds the same sample count).
@@ -834,7 +838,8 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
     if (cam.defocus_angle > 0.0f) {                     // defocus_disk_sample wgsl:327-331
         const float ang = (float)hash(seed + 1u) * 0x1.921fb4p-30f;  // 2*3.1415926 * rf
         float sa, ca, ux, uy;
-        sincos_k(ang, sa, ca, cam.k1s, cam.k1c);
+        // (ang = f32(hash) * 2pi 2^-32: always finite, RT_SINCOS_FIN drops the NaN guard)
+        sincos_k(ang, sa, ca, cam.k1s, cam.k1c, RT_SINCOS_FIN != 0);
         disk_unit<kTable>(sa, ca, ux, uy);
         o = fmas(uy, cam.ddv, fmas(ux, cam.ddu, c0));
     } else {
@@ -1557,6 +1562,11 @@ constexpr int kSingleDisk = RT_SINGLE_DISK;
 #define RT_SINGLE_AND 1
 #endif
 
+// RT_SINGLE_FRONT: the hit normal's face flip (wgsl:217-220) as per-lane selects only in a
+// wave with a back-face hit
+#ifndef RT_SINGLE_FRONT
+#define RT_SINGLE_FRONT 0
+#endif
 // RT_SINGLE_SKYDD: the sky's |d|^2 (wgsl:294's normalize) taken from where the direction was
 // made — the camera ray's a = d.d (wgsl:184, computed for the scan), the Lambertian scatter's
 // |n + ruv|^2 (computed for its degenerate-direction test, wgsl:89), or the normalised
@@ -1612,8 +1622,15 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
     } else {
         outward = divs(rel, pr.w);
     }
-    const bool front = dot(d, outward) < 0.0f;
-    const v3 n = front ? outward : neg(outward);
+    const float dno = dot(d, outward);
+    const bool front = dno < 0.0f;
+    v3 n = outward;
+    if (!RT_SINGLE_FRONT || (mask_not_lt(dno, 0.0f) & hm) != 0ull) {
+        // (a back-face hit in the wave: per-lane selects; camera rays from outside every
+        // sphere only hit front faces)
+        if (RT_SINGLE_FRONT) asm volatile("");
+        n = front ? outward : neg(outward);
+    }
     // lambertian (wgsl:84-93), computed for every lane; the other materials below
     v3 dir = add(n, ruv);
     const float ddir = dot(dir, dir);
