@@ -807,9 +807,11 @@ __device__ __forceinline__ void disk_unit(float sa, float ca, float& ux, float& 
     }
 }
 
-// RT_SINCOS_FIN: no NaN guard on the lens sample's quadrant in get_ray (its angle is finite)
+// RT_SINCOS_FIN: no NaN guard on the lens sample's quadrant in get_ray (its angle is finite).
+// Default since round 4: K3 14.26 against 14.42 µs per update over three interleaved rounds;
+// RT_SINGLE_FRONT measured neutral (profiles/r04/r04q_ab_front_fin.txt)
 #ifndef RT_SINCOS_FIN
-#define RT_SINCOS_FIN 0
+#define RT_SINCOS_FIN 1
 #endif
 // get_ray (wgsl:305-325) with the pixel-invariant hash(hash(x*73) ^ hash(y*51)) part
 // precomputed per pixel: seed = hash(hxy ^ su), su = sample_index*25 + B (wave-uniform
