@@ -1147,6 +1147,25 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 // one GPU: 16.8 / 18.8 us; 8-rank share: 3.13 / 2.95 us (`profiles/r01_rank_sim_groups_k3.txt`).
 template <int kScan>
 constexpr uint32_t frame_group() { return kScan == kTraceListQuad ? 4u : 2u; }
+// RT_GROUP_FLAGS: the frame group's hand-off without a workgroup barrier per group: a ring of
+// kGroupSlots colour slots with LDS counters — a producer wave writes its colours into the
+// group's slot once wave 0 has consumed the group kGroupSlots before it, then counts its
+// arrival (release); wave 0 waits for the group's arrivals (acquire), accumulates, frees
+// the slot.  The producers run up to kGroupSlots - 1 groups ahead instead of waiting at every
+// group's barrier for wave 0's accumulation and image stores.
+#ifndef RT_GROUP_FLAGS
+#define RT_GROUP_FLAGS 0
+#endif
+constexpr uint32_t kGroupSlots = 4;
+template <int kScan>
+constexpr size_t group_lds_bytes() {
+    return RT_GROUP_FLAGS ? (size_t)kGroupSlots * (frame_group<kScan>() - 1u) * 64u * 16u + 64u
+                          : (size_t)2u * (frame_group<kScan>() - 1u) * 64u * 16u;
+}
+__device__ __forceinline__ uint32_t lds_acquire(const uint32_t* a) {
+    return __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
 template <int kScan>
 __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam, uint32_t tile,
                                            uint32_t ncand, const TileCoord& tc, uint32_t hxy,
@@ -1158,6 +1177,70 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
     // bookkeeping, rt_abi.cpp fill_hint): the count arithmetic of wgsl:341-362 is scalar.
     const uint32_t lane = threadIdx.x & 63u;
     constexpr uint32_t kFrameGroup = frame_group<kScan>();
+#if RT_GROUP_FLAGS
+    // ctr[k]: producers arrived in slot k; ctr[kGroupSlots]: groups wave 0 has consumed
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(lds_recs + kGroupSlots * (kFrameGroup - 1u) * 64u);
+    if (threadIdx.x <= kGroupSlots) ctr[threadIdx.x] = 0u;
+    __syncthreads();
+    for (uint32_t f = 0, g = 0; f < p.frames; f += kFrameGroup, ++g) {
+        const uint32_t fw = f + w;
+        v3 col = mk(0.0f, 0.0f, 0.0f);
+        if (fw < p.frames) {
+            const uint32_t ng = p.hint_n[fw];
+            if (ng < spp && rt_ballot(tc.valid) != 0ull)           // wgsl:352
+                col = sample<kScan>(p, cam, tile, ncand, tc, hxy, ng, p.seed_b[fw], fw,
+                                    tc.valid, fw < p.hint_frames);
+        }
+        const uint32_t k = g % kGroupSlots;
+        float4* slot = lds_recs + k * (kFrameGroup - 1u) * 64u;
+        if (w != 0u) {
+            // the slot is free once wave 0 has consumed group g - kGroupSlots (every wait is
+            // bounded — about 2^20 sleeps — so that no wave can spin forever)
+            for (uint32_t spin = 0; g >= kGroupSlots &&
+                                    lds_acquire(&ctr[kGroupSlots]) + kGroupSlots <= g &&
+                                    spin < (1u << 20); ++spin)
+                __builtin_amdgcn_s_sleep(1);
+            slot[(w - 1u) * 64u + lane] = make_float4(col.x, col.y, col.z, 0.0f);
+            if (lane == 0u)
+                __hip_atomic_fetch_add(&ctr[k], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            continue;
+        }
+        for (uint32_t spin = 0; lds_acquire(&ctr[k]) < kFrameGroup - 1u && spin < (1u << 20);
+             ++spin)
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (uint32_t j = 0; j < kFrameGroup; ++j) {
+            const uint32_t fj = f + j;
+            if (fj >= p.frames) break;
+            if (j != 0) {
+                const float4 cj = slot[(j - 1u) * 64u + lane];
+                col = mk(cj.x, cj.y, cj.z);
+            }
+            const uint32_t nb = p.hint_n[fj];                     // count before frame fj
+            uint32_t na = nb;
+            if (nb < spp) {                                       // wgsl:352-358
+                const v3 num = sub(col, c);
+                if (RT_ACC_F64 && nb < (1u << 24) && rt_ballot(tc.valid && !acc_f64_ok(num)) == 0ull) {
+                    c = acc_f64(c, num, p.hint_rcp[fj]);
+                } else {
+                    const float kk = (float)(nb + 1u);            // wgsl:356
+                    c = mk(c.x + num.x / kk, c.y + num.y / kk, c.z + num.z / kk);
+                }
+                na = nb + 1u;
+            }
+            if ((p.store_each == 2u || fj + 2u >= p.frames) && tc.valid)       // wgsl:362-363
+                ((fj & 1u) ? p.out2 : p.out)[tc.idx] = make_float4(c.x, c.y, c.z, (float)na);
+        }
+        // the slot's colours are read (the loads above completed: their values are used):
+        // free it for group g + kGroupSlots
+        if (lane == 0u) {
+            __hip_atomic_store(&ctr[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&ctr[kGroupSlots], g + 1u, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    return;
+#endif
     for (uint32_t f = 0; f < p.frames; f += kFrameGroup) {
         const uint32_t fw = f + w;
         v3 col = mk(0.0f, 0.0f, 0.0f);
@@ -3548,12 +3631,10 @@ hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
         return launch_trace_as<kTraceCulled>(p, (size_t)p.lds_records * sizeof(float4), stream);
     if (kernel == kTraceList) return launch_trace_as<kTraceList>(p, 0, stream);
     if (kernel == kTraceListPair)
-        return launch_trace_as<kTraceListPair>(
-            p, 2 * (frame_group<kTraceListPair>() - 1) * 64 * sizeof(float4), stream);
+        return launch_trace_as<kTraceListPair>(p, group_lds_bytes<kTraceListPair>(), stream);
     if (kernel == kTraceBounce) return launch_bounce(p, stream);
     if (kernel == kTraceListQuad)
-        return launch_trace_as<kTraceListQuad>(
-            p, 2 * (frame_group<kTraceListQuad>() - 1) * 64 * sizeof(float4), stream);
+        return launch_trace_as<kTraceListQuad>(p, group_lds_bytes<kTraceListQuad>(), stream);
     return launch_trace_as<kTraceExhaustive>(p, 0, stream);
 }
 
