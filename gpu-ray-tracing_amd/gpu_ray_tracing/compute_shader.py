@@ -40,6 +40,20 @@ def _np_ptr(a: np.ndarray) -> ctypes.c_void_p:
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
+def _is_f32c(a) -> bool:
+    return isinstance(a, np.ndarray) and a.dtype == np.float32 and a.flags.c_contiguous
+
+
+def _cam_blob(camera: SceneCamera) -> np.ndarray:
+    """The camera's 44 f32 as one contiguous array: the rt_scene_camera layout itself."""
+    blob = camera.blob
+    if not _is_f32c(blob) or blob.size != 44:
+        blob = np.ascontiguousarray(blob, np.float32)
+        if blob.size != 44:
+            raise ValueError("a SceneCamera blob holds 44 f32 (176 bytes)")
+    return blob
+
+
 def _check_image(t: torch.Tensor, width: int, height: int, name: str) -> None:
     if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
         raise ValueError(f"{name} must be a CUDA (HIP) tensor")
@@ -280,13 +294,19 @@ class ComputeShaderPipeline:
         pnew = ctypes.byref(newest)
         stream = self._stream
         spheres_of = self._spheres
+        last = [None, None, None, 0]     # the spheres object, its array, pointer, count
 
         def run(camera: SceneCamera, spheres: SphereCollection, seeds) -> int:
-            cam = camera.to_c()
-            p, n = spheres_of(spheres)
-            s = np.ascontiguousarray(seeds, np.float32)
-            rc = fn(ctx, pa, pb, width, height, rank, nranks, ctypes.byref(cam), p, n, s.size,
-                    _np_ptr(s), stream(), pnew)
+            # the camera blob itself is the 176-byte rt_scene_camera (no struct copy); the
+            # same spheres object and array keep their pointer (the library compares the
+            # contents on every call, so an array changed in place is still uploaded)
+            blob = _cam_blob(camera)
+            if spheres is not last[0] or spheres.spheres is not last[1]:
+                p, n = spheres_of(spheres)
+                last[:] = [spheres, spheres.spheres, p, n]
+            s = seeds if _is_f32c(seeds) else np.ascontiguousarray(seeds, np.float32)
+            rc = fn(ctx, pa, pb, width, height, rank, nranks, blob.__array_interface__["data"][0],
+                    last[2], last[3], s.size, s.__array_interface__["data"][0], stream(), pnew)
             if rc:
                 _lib.check(rc, "rt_update_frames")
             return newest.value

@@ -226,9 +226,16 @@ def test_bound_update_frames_passes_the_same_arguments(rt, monkeypatch):
 
     def fake_update_frames(*args):
         flat = []
-        for a in args:
-            if isinstance(a, ctypes.c_void_p):
+        for i, a in enumerate(args):
+            if i == 7:                                       # the camera: its 176 bytes
+                if type(a).__name__ == "CArgObject":
+                    flat.append(("cam", bytes(a._obj)))
+                else:
+                    flat.append(("cam", ctypes.string_at(a, 176)))
+            elif isinstance(a, ctypes.c_void_p):
                 flat.append(("ptr", a.value))
+            elif i in (8, 11) and isinstance(a, int):        # spheres / seeds addresses
+                flat.append(("ptr", a))
             elif type(a).__name__ == "CArgObject":          # ctypes.byref(...)
                 obj = a._obj
                 flat.append(("ref", bytes(obj) if not isinstance(obj, ctypes.c_int) else "int"))
