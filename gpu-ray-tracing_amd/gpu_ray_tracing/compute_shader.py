@@ -133,11 +133,12 @@ class ComputeShaderPipeline:
                 "packets": int(packets.value), "why": why}
 
     def set_path_compaction(self, mode: str) -> None:
-        """rt_set_path_compaction for bounce launches: "auto" (default: "split" with two
-        chunks for launches of at most 20 000 tiles, else "per_wave"), "per_wave", "compact"
-        (paths repacked across four waves after every bounce), "pair" (two waves per tile on
-        alternate frames) or "split" (each tile's frames in chunks on separate waves, the
-        last finisher accumulating)."""
+        """rt_set_path_compaction for bounce launches: "auto" (default: "split" with four
+        chunks for launches of at most 20 000 tiles once their tile costs are measured, else
+        "per_wave"), "per_wave", "compact" (paths repacked across four waves after every
+        bounce), "pair" (two waves per tile on alternate frames) or "split" (a tile's frames in
+        chunks on separate waves, the last finisher accumulating; with measured costs only
+        the costliest tiles split, every unit dispatched by its own cost)."""
         _lib.call("rt_set_path_compaction", self._ctx,
                   {"auto": 0, "per_wave": 1, "compact": 2, "pair": 3, "split": 4}[mode])
 

@@ -372,12 +372,15 @@ RT_API rt_status rt_update_submit_status(rt_ctx* ctx, int* aql_available, uint32
  * frames, the second handing its colours to the first through LDS (shorter chains for
  * small per-rank shares); RT_PATHS_COMPACT repacks the live paths of a workgroup's four
  * waves into the fewest waves after every bounce (ballot + mbcnt prefix, path state through
- * LDS); RT_PATHS_SPLIT splits each tile's frames into 2 or 4 consecutive chunks, each traced
- * by its own wave, which stores its frames' colours (device scratch the context keeps: 1 KB
- * per tile and frame); the tile's last finishing chunk accumulates every frame in order and
- * writes the images.  RT_PATHS_AUTO (default): RT_PATHS_SPLIT with 2 chunks for launches of
- * at most 20 000 tiles (small per-rank shares: a few waves per SIMD), else RT_PATHS_PER_WAVE
- * (DESIGN.md §5).  Pixel results are identical in every mode. */
+ * LDS); RT_PATHS_SPLIT splits a tile's frames into consecutive chunks (2 or 4), each traced
+ * by its own wave: the first keeps its accumulator in registers, the later ones store their
+ * frames' colours (device scratch the context keeps: 1 KB per tile and frame), and the tile's
+ * last finishing chunk accumulates them in order and writes the images; once a launch has
+ * measured the tile costs, only the tiles costlier than a quarter of the launch's ideal span
+ * split and every unit is dispatched by its own cost.  RT_PATHS_AUTO (default): RT_PATHS_SPLIT
+ * with 4 chunks for launches of at most 20 000 tiles (small per-rank shares: a few waves per
+ * SIMD) once their costs are measured, else RT_PATHS_PER_WAVE.  Pixel results
+ * are identical in every mode. */
 #define RT_PATHS_AUTO 0
 #define RT_PATHS_PER_WAVE 1
 #define RT_PATHS_COMPACT 2
