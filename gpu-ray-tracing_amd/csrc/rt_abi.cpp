@@ -1205,7 +1205,8 @@ const char* rt_kernel_name(int which) {
                                         "rt_bounce_kernel<1>",     "rt_bounce_kernel<2>",
                                         rtk::single_kernel_name(0),
                                         rtk::single_kernel_name(1),
-                                        "rt_bounce_kernel<3>"};
+                                        "rt_bounce_kernel<3>",
+                                        "rt_trace_kernel<11>"};
     if (which >= 0 && which < (int)(sizeof(names) / sizeof(names[0]))) return names[which];
     return rtk::trace_kernel_name();
 }
@@ -1306,7 +1307,7 @@ rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launch) {
 rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     if (mode != RT_FRAME_PAIRS_AUTO && mode != RT_FRAME_PAIRS_OFF && mode != RT_FRAME_PAIRS_ON &&
-        mode != RT_FRAME_PAIRS_QUAD)
+        mode != RT_FRAME_PAIRS_QUAD && mode != RT_FRAME_PAIRS_OCT)
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown frame-pair mode");
     ctx->frame_pairs = mode;
     return RT_OK;
@@ -1522,7 +1523,9 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
             const uint64_t tiles = (uint64_t)((w + 7u) >> 3) * p.local_bands;
             const bool quad = ctx->frame_pairs == RT_FRAME_PAIRS_QUAD ||
                               (ctx->frame_pairs == RT_FRAME_PAIRS_AUTO && tiles <= rtk::kQuadMaxTiles);
-            kernel = quad ? rtk::kTraceListQuad : rtk::kTraceListPair;
+            kernel = ctx->frame_pairs == RT_FRAME_PAIRS_OCT ? rtk::kTraceListOct
+                     : quad                                 ? rtk::kTraceListQuad
+                                                            : rtk::kTraceListPair;
         }
         kernel = single_or(ctx, p, kernel);
         const bool aql = chain && nf == 1u &&

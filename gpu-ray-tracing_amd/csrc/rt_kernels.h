@@ -142,6 +142,9 @@ constexpr int kTraceListPair = 3;
 // The same with four waves per tile: for small per-rank shares (few tiles per SIMD), where
 // shorter per-wave frame chains keep more waves resident (rt_abi.cpp picks it).
 constexpr int kTraceListQuad = 4;
+// ... and with eight (opt-in: rt_set_frame_pairs(RT_FRAME_PAIRS_OCT))
+constexpr int kTraceListOct = 11;
+static_assert(kTraceListOct == RT_KERNEL_LIST_OCT, "instance id is the ABI's RT_KERNEL_LIST_OCT");
 static_assert(kTraceExhaustive == RT_KERNEL_EXHAUSTIVE && kTraceCulled == RT_KERNEL_CULLED &&
                   kTraceList == RT_KERNEL_LIST && kTraceListPair == RT_KERNEL_LIST_PAIR &&
                   kTraceListQuad == RT_KERNEL_LIST_QUAD,
@@ -164,7 +167,9 @@ static_assert(kTraceSingle == RT_KERNEL_SINGLE && kTraceSingleOne == RT_KERNEL_S
 #define RT_SINGLE_ONE_MAX_TILES 9000
 #endif
 constexpr uint64_t kSingleOneMaxTiles = RT_SINGLE_ONE_MAX_TILES;
-constexpr bool is_group_kernel(int k) { return k == kTraceListPair || k == kTraceListQuad; }
+constexpr bool is_group_kernel(int k) {
+    return k == kTraceListPair || k == kTraceListQuad || k == kTraceListOct;
+}
 constexpr bool is_list_kernel(int k) { return k == kTraceList || is_group_kernel(k); }
 // Waves (tiles) per workgroup of the one-wave-per-tile instances (kTraceExhaustive,
 // kTraceList): four-wave workgroups dispatch faster than one-wave ones (K3 single-frame

@@ -1146,7 +1146,9 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 // Waves per tile: 2 (kTraceListPair) or 4 (kTraceListQuad).  K3 per frame, whole image on
 // one GPU: 16.8 / 18.8 us; 8-rank share: 3.13 / 2.95 us (`profiles/r01_rank_sim_groups_k3.txt`).
 template <int kScan>
-constexpr uint32_t frame_group() { return kScan == kTraceListQuad ? 4u : 2u; }
+constexpr uint32_t frame_group() {
+    return kScan == kTraceListOct ? 8u : kScan == kTraceListQuad ? 4u : 2u;
+}
 // RT_GROUP_FLAGS: the frame group's hand-off without a workgroup barrier per group: a ring of
 // kGroupSlots colour slots with LDS counters — a producer wave writes its colours into the
 // group's slot once wave 0 has consumed the group kGroupSlots before it, then counts its
@@ -3635,6 +3637,8 @@ hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
     if (kernel == kTraceBounce) return launch_bounce(p, stream);
     if (kernel == kTraceListQuad)
         return launch_trace_as<kTraceListQuad>(p, group_lds_bytes<kTraceListQuad>(), stream);
+    if (kernel == kTraceListOct)
+        return launch_trace_as<kTraceListOct>(p, group_lds_bytes<kTraceListOct>(), stream);
     return launch_trace_as<kTraceExhaustive>(p, 0, stream);
 }
 
