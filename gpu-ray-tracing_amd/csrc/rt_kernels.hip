@@ -3367,8 +3367,8 @@ static dim3 tile_grid(const TraceParams& p, uint32_t waves = 4) {
 // Launches through hipModuleLaunchKernel with the arguments packed in the kernel's layout and
 // a function handle cached per device and kernel (the launch_single path below): no
 // per-launch symbol lookup or per-argument marshalling of the 2.6-KB TraceParams block.
-// Slots: 0-4 rt_trace_kernel<k>, 5-8 rt_bounce_kernel<m>.
-constexpr int kLaunchSlots = 12;   // trace instances by kScan (0-4, 11), bounce 5-8
+// Slots: 0-4 and 11 rt_trace_kernel<k>, 5-8 rt_bounce_kernel<m>.
+constexpr int kLaunchSlots = 12;
 static hipError_t launch_packed(int slot, const void* sym, dim3 grid, dim3 block, size_t lds,
                                 hipStream_t stream, void* args, size_t bytes) {
     constexpr int kMaxDevices = 64;
