@@ -380,6 +380,26 @@ def driver_record_sides(device, stream, main_cfg, main_us):
                                                  (d["us_per_step"] * 1e3) / PEAK_HBM_GBS, 4),
                                   what=f"{other}: 5 + 20 frames from a reset, one update "
                                        f"launch per frame, µs per update by HIP events")
+        # K4: one 64-spp 1920x1080 render from a reset (fused frames), as --config K4 steps,
+        # the full-image SHA-256 of k4.npz
+        w4, h4, sc4, seeds4, cam4 = setup("K4")
+        pipe.set_frames_per_launch(0)
+        pipe.set_frame_images("last_two")
+        r4 = StripeRenderer(pipe, w4, h4, 0, 1)
+        for _ in range(2):
+            r4.frames(cam4, sc4, seeds4)               # costs recorded, order built
+        runs4 = sorted(timed(stream, lambda: r4.frames(cam4, sc4, seeds4)) for _ in range(5))
+        info4 = pipe.last_launch_info()
+        ok4, what4 = image_check("K4", r4.local[:h4], 64, cam4, w4, h4)
+        out["k4"] = {"us_per_step": round(runs4[2] * 1e6, 1),
+                     "us_per_frame": round(runs4[2] / 64 * 1e6, 2),
+                     "runs_us": [round(x * 1e6, 1) for x in runs4],
+                     "kernel": info4["kernel_name"], "launches_per_step": info4["launches"],
+                     "image_ok": ok4, "image_check": what4,
+                     "Mrays_per_s": round(w4 * h4 * 64 / (runs4[2] * 1e6), 1),
+                     "what": "K4: one 64-spp 1920x1080 render from a reset (fused frames, "
+                             "cost-ordered after two untimed renders), the median of five"}
+        del r4
         k5 = k5_share(1)
         out["k5"] = dict(k5, Mrays_per_s=round(3840 * 2160 * 64 / k5["us_per_step"], 1),
                          what="one 64-spp 3840x2160 depth-8 step (one 64-frame bounce launch, "
