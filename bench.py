@@ -790,7 +790,13 @@ def main():
             side["cold_start"] = cold_start
         if dispatch and depth == 1:
             # K2 / K5 / rank shares: each with its image check
-            side.update(driver_record_sides(device, stream, cfg, render_s / args.steps * 1e6))
+            # (a side measurement that fails is reported in the line, never costs the line)
+            try:
+                side.update(driver_record_sides(device, stream, cfg,
+                                                render_s / args.steps * 1e6))
+            except Exception as e:          # noqa: BLE001
+                torch.cuda.synchronize()
+                side["side_error"] = f"{type(e).__name__}: {e}"[:400]
     line.update(side)
 
     if rank == 0:
