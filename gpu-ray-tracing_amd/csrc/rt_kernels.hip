@@ -1563,9 +1563,10 @@ static_assert(kSinglePix >= 1 && kSinglePix <= 4, "1 to 4 tiles per wave");
 #ifndef RT_SKO
 #define RT_SKO 0
 #endif
-// waves per workgroup of the one-frame kernel
+// waves per workgroup of the one-frame kernel: 2 since round 4 (profiles/r04/r04a2_single_shape.txt,
+// r04b2_driver_wg2.txt: 0.2 us per update faster than 4 at K3, same bits)
 #ifndef RT_SINGLE_WG
-#define RT_SINGLE_WG 4
+#define RT_SINGLE_WG 2
 #endif
 constexpr uint32_t kSingleWg = RT_SINGLE_WG;
 // RT_SINGLE_PRIO: the first RT_SINGLE_PRIO workgroups of wg_order (the costliest) run at
