@@ -31,4 +31,3 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_driver -o driver -
 echo rocprof done
 PMC_ROUND=r04 bash tools/pmc_bench.sh ${TAG}_pmc "K3" || exit 1
 echo pmc done
-echo pmc done
