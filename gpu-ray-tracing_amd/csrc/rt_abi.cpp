@@ -704,7 +704,7 @@ rt_status plan_split(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t s
     uint32_t S = tiles <= kSplit4MaxTiles ? 4u : tiles <= kSplit2MaxTiles ? 2u : 1u;
     if (mode == RT_PATHS_SPLIT) S = std::max(S, 2u);
     if (const char* e = std::getenv("RT_BOUNCE_SPLIT")) S = (uint32_t)std::max(1L, std::atol(e));
-    S = std::min(S, p.frames);
+    S = std::min(std::min(S, p.frames), 8u);   // a unit-order entry holds chunks 0-7
     // AUTO splits only with a measured order (the unit order below): a launch without one runs
     // per wave, so the costs it records are whole tiles', not a chunk's scaled by S
     if (mode == RT_PATHS_AUTO && !p.tile_order && !std::getenv("RT_SPLIT_FRAC")) S = 1u;
