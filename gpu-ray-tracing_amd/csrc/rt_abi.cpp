@@ -672,6 +672,8 @@ rt_status plan_wg_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_
 // tile in 2 chunks 4 447, the unit order with S = 4 and alpha 0.25 4 253 (0.879 of the 1-GPU
 // per-wave rate); 4-rank per wave 7 896 against 8 008, whole image 29 911 against 30 185 — so
 // AUTO splits (S = 4, unit order) shares of at most 20 000 tiles and runs larger ones per wave.
+// Against S = 8 and other alphas (profiles/r04/r04e2_k5_chunks_alpha.jsonl, 8-rank share):
+// AUTO 4 248, S = 8 alpha 0.25 / 0.5 4 318 / 4 391, S = 4 alpha 0.125 / 0.5 4 686 / 4 264.
 #ifndef RT_SPLIT4_MAX_TILES
 #define RT_SPLIT4_MAX_TILES 20000
 #endif
