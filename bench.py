@@ -222,7 +222,11 @@ def cpu_baseline(cam, spheres, w, h, seconds):
 
     T = host_threads()
     frames, dt = threaded(T, 2 * seconds / 5, 8)
-    A = host_cpus()[1]
+    # every CPU the process may run on at once: the affinity set, capped by the cgroup's CPU
+    # bandwidth quota (a GPU box shows 256 CPUs in its affinity set while its cgroup
+    # schedules 16: 256 threads there time-slice 16 CPUs and measure the oversubscription)
+    aff, quota = host_cpus()[1], cgroup_cpus()
+    A = max(1, min(aff, int(quota))) if quota else aff
     band = max(1, min(8, h // (2 * A)))        # at least two bands per thread
     fa, dta = threaded(A, seconds / 5, band)
     return {"value": round(w * h * frames / dt / 1e6, 3), "unit": "Mrays/s", "cores": T,
@@ -234,12 +238,15 @@ def cpu_baseline(cam, spheres, w, h, seconds):
                               "sample": f"{w}x{rows1} rows of one update"},
             "all_cores": {"value": round(w * h * fa / dta / 1e6, 3), "cores": A,
                           "sample": f"{fa} full {w}x{h} update(s) on {A} threads "
-                                    f"({band}-row bands from a shared counter), {dta:.1f} s"},
+                                    f"({band}-row bands from a shared counter), {dta:.1f} s",
+                          "bound": ("cgroup CPU quota" if quota and int(quota) < aff
+                                    else "affinity set")},
             "cpu_model": cpu_model(),
-            "nproc": host_cpus()[0], "affinity_cpus": host_cpus()[1],
-            "cgroup_cpu_quota": cgroup_cpus(),
+            "nproc": host_cpus()[0], "affinity_cpus": aff,
+            "cgroup_cpu_quota": quota,
             "cores_rule": "value: min(16, affinity) threads, the per-GPU share of the box's host "
-                          "cores; all_cores: every core of the affinity set"}
+                          "cores; all_cores: min(affinity set, cgroup CPU quota) threads — every "
+                          "CPU the process can run on at once"}
 
 
 def load_pmc(config, kernel, frames_per_launch):
@@ -296,8 +303,8 @@ def image_check(config, image, frames, cam, w, h):
     return bool(same.all()), f"{want.shape[0]} sampled pixels of the 64-spp render"
 
 
-def share_pixels_ok(config, local, frames, world):
-    """Rank 0's share (local rows of bands 0, world, 2*world, ...) against the fixture's
+def share_pixels_ok(config, local, frames, world, rank=0):
+    """A rank's share (local rows of bands rank, rank + world, ...) against the fixture's
     sampled pixels that fall in those bands (the K2/K3 fixtures after `frames` frames, K5's
     64-spp render)."""
     img = local.detach().cpu().numpy()
@@ -311,19 +318,36 @@ def share_pixels_ok(config, local, frames, world):
         g = dict(np.load(GOLDEN / f"{config.lower()}.npz"))
         want = g["pixels"]
     py, px = g["py"], g["px"]
-    mine = (py // 8) % world == 0
+    mine = (py // 8) % world == rank
     ly = (py[mine] // 8 // world) * 8 + py[mine] % 8
     got, want = img[ly, px[mine]], want[mine]
     same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
     return bool(same.all()) and int(mine.sum()) > 0
 
 
+def over_ranks(share, world):
+    """share(rank) -> {"us_per_step", ...} for every rank of a world-size run, timed one after
+    another on this GPU: the job's step is the slowest rank's (bench.py --gpus N takes the
+    max over ranks), so `us_per_step` is the max; each rank's own time and pixel check are
+    kept (rank_us, image_ok = every rank's share matches the fixture)."""
+    per = [share(r) for r in range(world)]
+    slow = max(range(world), key=lambda r: per[r]["us_per_step"])
+    out = dict(per[slow])
+    out.update({"us_per_step": per[slow]["us_per_step"], "max_over_ranks": True,
+                "slowest_rank": slow, "rank_us": [d["us_per_step"] for d in per],
+                "rank0_us": per[0]["us_per_step"],
+                "image_ok": all(d["image_ok"] for d in per) if all(
+                    d["image_ok"] is not None for d in per) else None})
+    return out
+
+
 def driver_record_sides(device, stream, main_cfg, main_us):
     """Side measurements for the driver's N=1 record (after the timed region), each with its
-    image check: the other per-dispatch config (K2 next to K3), one K5 64-spp step, and rank
-    0's 1/2, 1/4, 1/8 shares of K3 (one update launch per frame, and frame chains) and K5 timed
-    alone on this GPU — what each rank of `bench.py --gpus N` computes per step, so the
-    strong-scaling curve has a per-rank measurement behind it (tools/rank_sim.py's method)."""
+    image check: the other per-dispatch config (K2 next to K3), one K5 64-spp step, and every
+    rank's 1/2, 1/4, 1/8 share of K3 (one update launch per frame, and frame chains) and K5
+    timed alone on this GPU — what each rank of `bench.py --gpus N` computes per step, the
+    slowest rank setting the step — so the strong-scaling curve has a per-rank measurement
+    behind it (tools/rank_sim.py's method)."""
     out = {}
     pipe = rt.ComputeShaderPipeline(device)
     try:
@@ -339,28 +363,28 @@ def driver_record_sides(device, stream, main_cfg, main_us):
                 sc, seeds, cam = rt.SphereCollection(g["spheres"]), g["seeds"], rt.SceneCamera(g["camera"])
             return w, h, sc, seeds, cam
 
-        def dispatch_share(cfg, world, mode):
+        def dispatch_share(cfg, world, mode, rank=0):
             # the driver's structure: 5 frames from a reset, then 20 timed (25-frame fixture);
             # one untimed pass first on scratch images (the share's lists, order, code)
             w, h, sc, seeds, cam = setup(cfg)
             set_frame_launch(pipe, mode)
             cam_t = cam.with_fields(camera_has_moved=0.0)
-            scratch = StripeRenderer(pipe, w, h, 0, world)
+            scratch = StripeRenderer(pipe, w, h, rank, world)
             scratch.frames(cam, sc, seeds[:20])
             del scratch
-            r = StripeRenderer(pipe, w, h, 0, world)
+            r = StripeRenderer(pipe, w, h, rank, world)
             r.frames(cam, sc, seeds[:5])
             t = timed(stream, lambda: r.frames(cam_t, sc, seeds[5:25])) / 20
             info = pipe.last_launch_info()
             return {"us_per_step": round(t * 1e6, 2), "kernel": info["kernel_name"],
                     "launches_per_step": round(info["launches"] / 20, 3),
-                    "image_ok": share_pixels_ok(cfg, r.local, 25, world)}
+                    "image_ok": share_pixels_ok(cfg, r.local, 25, world, rank)}
 
-        def k5_share(world):
+        def k5_share(world, rank=0):
             w, h, sc, seeds, cam = setup("K5")
             pipe.set_frames_per_launch(0)
             pipe.set_frame_images("last_two")
-            r = StripeRenderer(pipe, w, h, 0, world)
+            r = StripeRenderer(pipe, w, h, rank, world)
             r.frames(cam, sc, seeds)                   # records the tile costs
             r.frames(cam, sc, seeds)                   # builds the order (and its buffers)
             # (each call restarts from the camera's reset; the median of five launches)
@@ -370,7 +394,7 @@ def driver_record_sides(device, stream, main_cfg, main_us):
             return {"us_per_step": round(t * 1e6, 1), "us_per_spp": round(t / 64 * 1e6, 2),
                     "runs_us": [round(x * 1e6, 1) for x in runs],
                     "kernel": info["kernel_name"],
-                    "image_ok": share_pixels_ok("K5", r.local, 64, world)}
+                    "image_ok": share_pixels_ok("K5", r.local, 64, world, rank)}
 
         other = "K2" if main_cfg == "K3" else "K3"
         d = dispatch_share(other, 1, "dispatch")
@@ -413,7 +437,8 @@ def driver_record_sides(device, stream, main_cfg, main_us):
                 if world == 1 and mode == "dispatch" and base["dispatch"]:
                     rows["1"] = {"us_per_step": round(base["dispatch"], 2), "kernel": "(the timed steps)"}
                     continue
-                rows[str(world)] = dispatch_share("K3", world, mode)
+                rows[str(world)] = over_ranks(
+                    lambda rk: dispatch_share("K3", world, mode, rk), world)
             ref = rows["1"]["us_per_step"]
             for k, v in rows.items():
                 v["predicted_efficiency"] = round(ref / (int(k) * v["us_per_step"]), 3)
@@ -425,13 +450,14 @@ def driver_record_sides(device, stream, main_cfg, main_us):
                 v["efficiency_vs_1gpu_step"] = round(one / (int(k) * v["us_per_step"]), 3)
         k5rows = {"1": {"us_per_step": k5["us_per_step"], "us_per_spp": k5["us_per_spp"]}}
         for world in (2, 4, 8):
-            k5rows[str(world)] = k5_share(world)
+            k5rows[str(world)] = over_ranks(lambda rk: k5_share(world, rk), world)
         for k, v in k5rows.items():
             v["predicted_efficiency"] = round(k5["us_per_step"] / (int(k) * v["us_per_step"]), 3)
         shares["K5"]["fused_64"] = k5rows
-        shares["what"] = ("rank 0's stripe share (8-row bands dealt round-robin) timed alone on "
-                          "this GPU, i.e. one rank's step of bench.py --gpus N; "
-                          "predicted_efficiency = the 1-rank time / (N x the share's time) in "
+        shares["what"] = ("every rank's stripe share (8-row bands dealt round-robin) timed alone "
+                          "on this GPU, i.e. each rank's step of bench.py --gpus N; us_per_step "
+                          "= the slowest rank's (max_over_ranks; rank_us lists them all); "
+                          "predicted_efficiency = the 1-rank time / (N x that time) in "
                           "the same launch structure; K3 'dispatch' = one update launch per "
                           "frame, 'chain' = fused launches writing every frame's image "
                           "(--frame-launch auto takes chain for shares <= %d tiles)"
@@ -446,6 +472,48 @@ def _unserializable(o):
     """json default: a value the line cannot hold is named, not fatal (the line still
     prints; the bad path shows in its place)."""
     return f"<{type(o).__name__} {getattr(o, '__name__', '')}>"
+
+
+def timed_steps(run, sync, world, barrier=None, device=None, stamp=None):
+    """The timed region of the K steps.  Every rank leaves an opening barrier (then
+    synchronises), starts its clock, issues the steps (`run`), synchronises, and stops its
+    clock: its own wall time of the K steps.  The closing barrier follows outside that time
+    and is reported on its own (`barrier_s`), so that at N > 1 the value measures the render,
+    not the collective's latency (a 8-rank K3 step is ~3 µs, the same order as one barrier).
+    The job's time is the MAX over ranks (all ranks start together after the opening
+    barrier).  Returns {"dt": max over ranks, "per_rank": [s...], "issue": this rank's host
+    issue time, "barrier_s": max over ranks of the closing barrier}.  `stamp(name)` (optional)
+    is called at the start, when the issue returns and after the synchronise."""
+    barrier = barrier or dist.barrier
+    sync()
+    if world > 1:
+        barrier()
+        sync()
+    if stamp:
+        stamp("t0")
+    t0 = time.perf_counter()
+    run()
+    t_issued = time.perf_counter()
+    if stamp:
+        stamp("issued")
+    sync()
+    mine = time.perf_counter() - t0
+    if stamp:
+        stamp("synced")
+    bar = 0.0
+    per_rank, bars = [mine], [0.0]
+    if world > 1:
+        tb = time.perf_counter()
+        barrier()
+        sync()
+        bar = time.perf_counter() - tb
+        t = torch.tensor([mine, bar], dtype=torch.float64, device=device)
+        got = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(got, t)
+        per_rank = [float(g[0]) for g in got]
+        bars = [float(g[1]) for g in got]
+    return {"dt": max(per_rank), "per_rank": per_rank, "issue": t_issued - t0,
+            "barrier_s": max(bars)}
 
 
 def timed(stream, fn):
@@ -573,21 +641,25 @@ def main():
         r.finish()
     # (HIP events created before the timed region: their creation is host work, not steps)
     ev0, ev1, ev2, ev3 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
 
-    # timed: K steps issued by rt_update_frames
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    step_block(args.steps, args.warmup == 0)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    # timed: K steps issued by rt_update_frames (timed_steps: opening barrier, each rank's
+    # own clock around its steps and synchronize, the max over ranks; the closing barrier
+    # reported apart)
+    host_t = {} if os.environ.get("RT_TIMELINE") is not None else None   # tools/timeline.py
+
+    def stamp(name):
+        host_t[name] = (time.clock_gettime_ns(time.CLOCK_MONOTONIC),
+                        time.clock_gettime_ns(time.CLOCK_BOOTTIME))
+
+    def run():
+        ev0.record(stream)
+        step_block(args.steps, args.warmup == 0)
+        ev1.record(stream)
+
+    red_dev = "cuda" if backend == "nccl" else "cpu"
+    ts = timed_steps(run, torch.cuda.synchronize, world, device=red_dev,
+                     stamp=stamp if host_t is not None else None)
+    dt = ts["dt"]
     info = pipe.last_launch_info()             # the last timed rt_update_frames call
     # the job's one gather of the finished tiles, timed on its own (barrier on both sides)
     t1 = time.perf_counter()
@@ -602,7 +674,7 @@ def main():
     render_s, gather_s = ev0.elapsed_time(ev1) / 1e3, ev2.elapsed_time(ev3) / 1e3
     if world > 1:
         t = torch.tensor([dt, render_s, gather_s, dt_gather], dtype=torch.float64,
-                         device="cuda")
+                         device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, render_s, gather_s, dt_gather = (float(x) for x in t.tolist())
     frames_total = (args.warmup + args.steps) if dispatch else spf
@@ -625,10 +697,14 @@ def main():
     kernel = info["kernel_name"]
     fpl = info["max_frames_per_launch"]
     bytes_launch = local_px * BYTES_PER_PIXEL_LAUNCH
+    ref_bytes_launch = bytes_launch
     if launch_mode == "chain":
-        # a frame chain carries fpl progressive updates: the reference's 32 B per pixel each
-        # (it writes every frame's 16 B; the accumulator stays in registers between frames)
-        bytes_launch *= fpl
+        # a frame chain carries fpl progressive updates but keeps the accumulator in
+        # registers between them: it reads the input once (16 B per pixel) and writes every
+        # frame's image (16 B per pixel per frame).  The reference's 32 B per pixel per frame
+        # (a load and a store per dispatch) is reported beside it, not as `achieved`.
+        bytes_launch = local_px * (16 * fpl + 16)
+        ref_bytes_launch = local_px * BYTES_PER_PIXEL_LAUNCH * fpl
     pmc, pmc_path = load_pmc(cfg, kernel, fpl) if world == 1 else (None, None)
     wgt, wgt_path = load_weighted(cfg, kernel) if pmc else (None, None)
     roof = {"bound": "hbm", "achieved": round(bytes_launch / launch_s / 1e9, 1),
@@ -639,6 +715,7 @@ def main():
             "frames_per_launch": fpl, "launches_per_step": launches_per_step,
             "queues": queues, "submit": info.get("submit"),
             "algorithmic_bytes_per_launch": bytes_launch,
+            "reference_bytes_per_launch": ref_bytes_launch,
             "binding": "valu",
             # the same bytes against the measured streaming floor of the pattern (no tracing)
             "practical_hbm": {"floor_GBs": RMW_FLOOR_GBS,
@@ -692,8 +769,13 @@ def main():
         "roofline": roof,
         "image_ok": image_ok,
         "image_check": image_what,
-        # max over ranks: the K steps by HIP events (value's wall time adds the barriers)
-        "timed_breakdown_ms": {"steps": round(render_s * 1e3, 4)},
+        # max over ranks: the K steps by HIP events; each rank's own wall time of its K steps
+        # (value's time is their max); the closing barrier after them, outside value
+        "timed_breakdown_ms": {"steps": round(render_s * 1e3, 4),
+                               # host time of the steps' issue (this rank): the call returned
+                               "host_issue": round(ts["issue"] * 1e3, 4),
+                               "per_rank_ms": [round(x * 1e3, 4) for x in ts["per_rank"]],
+                               "barrier_ms": round(ts["barrier_s"] * 1e3, 4)},
         # the job's output collection after the timed steps, and the job-level rate with it
         "gather": {"how": gather_how, "wall_ms": round(dt_gather * 1e3, 4),
                    "events_ms": round(gather_s * 1e3, 4),
@@ -707,6 +789,12 @@ def main():
                             "(--warm-ms): the timed steps are a running render's, not a "
                             "freshly started process's first launches"},
     }
+
+    if host_t is not None:
+        # host clocks (CLOCK_MONOTONIC, CLOCK_BOOTTIME ns) at the timed region's start, when
+        # the steps' issue returned, and after the closing synchronize: tools/timeline.py
+        # places them on a rocprofv3 trace of the same run
+        line["timeline_host"] = host_t
 
     # ---- side measurements (after the timed region and its image check) -------------
     side = {}

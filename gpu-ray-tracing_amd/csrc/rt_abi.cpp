@@ -109,6 +109,7 @@ struct rt_ctx {
     uint32_t* unit_order = nullptr;     // unit_cap entries, then the count
     uint64_t unit_cap = 0;
     uint64_t unit_key[5] = {~0ull, 0, 0, 0, 0};
+    int cus = 0;                        // compute units of `device` (0: not queried yet)
 };
 
 namespace {
@@ -707,6 +708,9 @@ rt_status plan_split(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t s
     if (mode == RT_PATHS_SPLIT) S = std::max(S, 2u);
     if (const char* e = std::getenv("RT_BOUNCE_SPLIT")) S = (uint32_t)std::max(1L, std::atol(e));
     S = std::min(std::min(S, p.frames), 8u);   // a unit-order entry holds chunks 0-7
+    // a power of two: rt_unit_order_kernel moves a split tile's cost bucket by 4·log2 S
+    // places (cost / S), and launches of 3, 5, 6 or 7 frames would otherwise give S = 3..7
+    while (S & (S - 1u)) S &= S - 1u;
     // AUTO splits only with a measured order (the unit order below): a launch without one runs
     // per wave, so the costs it records are whole tiles', not a chunk's scaled by S
     if (mode == RT_PATHS_AUTO && !p.tile_order && !std::getenv("RT_SPLIT_FRAC")) S = 1u;
@@ -757,14 +761,15 @@ rt_status plan_split(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t s
             ctx->unit_cap = cap + 1;
             ctx->unit_key[0] = ~0ull;
         }
-        // (resident waves of the launch: every SIMD of the device at 8 waves)
-        static const int cus = [] {
-            int n = 0, dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        // (resident waves of the launch: every SIMD of the context's device at 8 waves)
+        if (ctx->cus == 0) {
+            int n = 0;
+            if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, ctx->device) !=
+                    hipSuccess || n <= 0)
                 n = 256;
-            return n > 0 ? n : 256;
-        }();
+            ctx->cus = n;
+        }
+        const int cus = ctx->cus;
         const float k_thr = (float)(alpha / (cus * 4.0 * 8.0));
         uint32_t kbits;
         std::memcpy(&kbits, &k_thr, 4);
@@ -1054,11 +1059,12 @@ rt_status ensure_aux_streams(rt_ctx* ctx, uint32_t n) {
     return RT_OK;
 }
 
-// aux[0..n) wait for everything issued on `stream` so far
-rt_status fork_aux(rt_ctx* ctx, uint32_t n, hipStream_t stream) {
-    hipError_t e = hipEventRecord(ctx->fork_ev, stream);
-    for (uint32_t k = 0; e == hipSuccess && k < n; ++k) e = hipStreamWaitEvent(ctx->aux[k], ctx->fork_ev, 0);
-    return e == hipSuccess ? RT_OK : hip_fail(e, "fork (hipEventRecord / hipStreamWaitEvent)");
+// How the parts of a call's first update are forked from the caller's stream: 1 (default)
+// skips the fork event when the stream is idle (hipStreamQuery), 0 always records it
+// (RT_FORK=0 in the environment, diagnostic A/B: tools/driver_region.py).
+int fork_mode() {
+    const char* e = std::getenv("RT_FORK");
+    return (e && e[0] == '0') ? 0 : 1;
 }
 
 // `stream` waits for everything issued on aux[0..n) so far
@@ -1569,12 +1575,28 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
             // every part's next frame reads only the pixels its own previous frame wrote;
             // what `stream` prepared (lists, order, the input image) is forked to the others
             if (rt_status s = ensure_aux_streams(ctx, parts - 1u)) return s;
+            // The fork: the aux streams wait for an event recorded on `stream` — unless
+            // `stream` has nothing left to run (a new call on an idle stream: then everything
+            // it was given is complete and the aux streams, joined into it at the end of the
+            // previous call, are idle too), which spares the first update the event record and
+            // the waits before its second part ("Fixed cost of a call").  Part 0
+            // goes out before the waits either way.
+            bool wait_fork = false;
             if (!forked) {
-                if (rt_status s = fork_aux(ctx, parts - 1u, stream)) return s;
+                if (fork_mode() == 0 || hipStreamQuery(stream) != hipSuccess) {
+                    hipError_t e = hipEventRecord(ctx->fork_ev, stream);
+                    if (e != hipSuccess) return hip_fail(e, "fork (hipEventRecord)");
+                    wait_fork = true;
+                }
                 forked = true;
             }
             for (uint32_t k = 0; k < parts; ++k) {
                 p.part = k;
+                if (k == 1u && wait_fork)
+                    for (uint32_t j = 0; j + 1u < parts; ++j) {
+                        hipError_t e = hipStreamWaitEvent(ctx->aux[j], ctx->fork_ev, 0);
+                        if (e != hipSuccess) return hip_fail(e, "fork (hipStreamWaitEvent)");
+                    }
                 hipError_t e = rtk::launch_trace(p, kernel, k ? ctx->aux[k - 1] : stream);
                 if (e != hipSuccess) return hip_fail(e, "rt_single_kernel launch");
                 if (k) fl.aux_live = std::max(fl.aux_live, k);

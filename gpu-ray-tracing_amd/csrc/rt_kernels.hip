@@ -20,6 +20,16 @@
 #include <cstddef>
 #include <cstring>
 
+// The device code is written for gfx950 only.  Two of its hand-offs between workgroups (the
+// split bounce schedule's chunk colours, the AQL chain's frames) rely on that target's cache
+// policy bits — the buffer intrinsics' aux = 16 is sc1: write-through stores and L1-bypassing
+// loads — and on the drained-`sc1` forms MI355X_MICROARCH.md measures for it (inter-workgroup
+// visibility, "Valid forms") in place of agent-scope release / acquire fences.  Another
+// target would need those re-checked (or the fences), so it does not compile.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "rt_kernels.hip targets gfx950 only (cache-policy bits of the sc1 hand-offs)"
+#endif
+
 namespace rtk {
 
 using namespace rtd;

@@ -294,20 +294,28 @@ class ComputeShaderPipeline:
         newest = ctypes.c_int(-1)
         pnew = ctypes.byref(newest)
         stream = self._stream
-        spheres_of = self._spheres
-        last = [None, None, None, 0]     # the spheres object, its array, pointer, count
+        # the caller's spheres array when it can be passed as it is (contiguous float32
+        # (N, 8)), its data pointer and count; `held` keeps the array the pointer points into
+        # alive until the next call replaces it (a converted copy included)
+        last = {"arr": None, "ptr": None, "n": 0, "held": None}
 
         def run(camera: SceneCamera, spheres: SphereCollection, seeds) -> int:
-            # the camera blob itself is the 176-byte rt_scene_camera (no struct copy); the
-            # same spheres object and array keep their pointer (the library compares the
-            # contents on every call, so an array changed in place is still uploaded)
+            # the camera blob itself is the 176-byte rt_scene_camera (no struct copy).  A
+            # spheres array that is contiguous float32 (N, 8) is passed as it is, its pointer
+            # re-read only when the array object or its length changes; any other array is
+            # converted on every call.  (The library compares the contents on every call, so
+            # an array edited in place is still uploaded.)
             blob = _cam_blob(camera)
-            if spheres is not last[0] or spheres.spheres is not last[1]:
-                p, n = spheres_of(spheres)
-                last[:] = [spheres, spheres.spheres, p, n]
+            arr = spheres.spheres
+            if arr is not last["arr"] or arr.shape[0] != last["n"]:
+                direct = _is_f32c(arr) and arr.ndim == 2 and arr.shape[1] == 8
+                held = arr if direct else np.ascontiguousarray(arr, np.float32).reshape(-1, 8)
+                last.update(arr=arr if direct else None, held=held, n=held.shape[0],
+                            ptr=held.__array_interface__["data"][0])
             s = seeds if _is_f32c(seeds) else np.ascontiguousarray(seeds, np.float32)
             rc = fn(ctx, pa, pb, width, height, rank, nranks, blob.__array_interface__["data"][0],
-                    last[2], last[3], s.size, s.__array_interface__["data"][0], stream(), pnew)
+                    last["ptr"], last["n"], s.size, s.__array_interface__["data"][0], stream(),
+                    pnew)
             if rc:
                 _lib.check(rc, "rt_update_frames")
             return newest.value

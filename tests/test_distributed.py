@@ -332,3 +332,56 @@ def test_stripe_comm_from_nccl_process_group():
         if p.is_alive():
             p.terminate()
             p.join(timeout=10)
+
+
+def _timed_region_worker(rank, world, port, step_s, slow_s, q):
+    """bench.py's timed region (timed_steps) over gloo: rank r's steps take step_s[r]; the
+    barrier of rank 1 sleeps slow_s before entering it (an artificially slow barrier)."""
+    import time
+    sys.path[:0] = [str(PKG_DIR), str(ROOT)]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+
+        def slow_barrier():
+            if rank == 1:
+                time.sleep(slow_s)
+            dist.barrier()
+
+        ts = bench.timed_steps(lambda: time.sleep(step_s[rank]), lambda: None, world,
+                               barrier=slow_barrier, device="cpu")
+        q.put((rank, ts))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_timed_region_excludes_closing_barrier():
+    """The N > 1 timed region (round-4 verdict item 2): each rank's clock runs from the
+    opening barrier to its own synchronize after its steps, the value's time is the max over
+    ranks, and a slow closing barrier is reported as barrier_s without entering that time."""
+    world, step_s, slow_s = 2, [0.05, 0.02], 0.5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timed_region_worker, args=(r, world, port, step_s, slow_s, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        got = dict(q.get(timeout=5) for _ in range(world))
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    for rank, ts in got.items():
+        assert len(ts["per_rank"]) == world
+        # rank 0's steps (50 ms) set the job's time; the 500-ms barrier stays out of it
+        assert 0.05 <= ts["dt"] < 0.05 + 0.2, ts
+        assert ts["dt"] == max(ts["per_rank"])
+        assert 0.02 <= ts["per_rank"][1] < 0.02 + 0.2, ts
+        assert ts["barrier_s"] >= 0.4, ts

@@ -288,3 +288,60 @@ def test_bound_update_frames_passes_the_same_arguments(rt, monkeypatch):
             run(cam, sc, seeds)
     finally:
         pipe._ctx = ctypes.c_void_p()   # (no context to destroy: close() skips a null one)
+
+
+def test_bound_run_keeps_converted_spheres_alive(rt, monkeypatch):
+    """A spheres array that is not contiguous float32 (here float64) is converted on every
+    bound call, and the converted copy stays alive while the library may read it — even when
+    StripeRenderer's two bound directions alternate and each converts its own copy (round-4
+    ADVICE: a cached pointer into a copy freed by the other direction).  The stand-in library
+    reads the sphere bytes at the pointer it is given, after freed small blocks have been
+    reused."""
+    import gpu_ray_tracing.compute_shader as cs
+    seen = []
+
+    def fake_update_frames(*args):
+        ptr, n = args[8], args[9]
+        seen.append(np.frombuffer(ctypes.string_at(ptr, n * 32), np.float32).reshape(n, 8).copy())
+        return 0
+
+    class FakeLib:
+        rt_update_frames = staticmethod(fake_update_frames)
+
+    class FakeImage:
+        def __init__(self, addr):
+            self.addr = addr
+
+        def data_ptr(self):
+            return self.addr
+
+    cam = rt.SceneCamera.from_settings(rt.CameraSettings(), 16, 16, 0.25)
+    monkeypatch.setattr(cs._lib, "lib", lambda: FakeLib)
+    monkeypatch.setattr(cs, "_check_image", lambda *a: None)
+    pipe = object.__new__(cs.ComputeShaderPipeline)
+    pipe._ctx = ctypes.c_void_p(0x1234)
+    pipe._sphere_keep = None
+    monkeypatch.setattr(pipe, "_stream", lambda: ctypes.c_void_p(0x77))
+    a, b = FakeImage(0x1000), FakeImage(0x2000)
+    runs = [pipe.bind_update_frames(a, b, 16, 16), pipe.bind_update_frames(b, a, 16, 16)]
+    seeds = np.array([0.25], np.float32)
+    rng = np.random.default_rng(3)
+    sc64 = rt.SphereCollection(rng.random((5, 8)))                 # float64: converted
+    sc32 = rt.SphereCollection(rng.random((5, 8)).astype(np.float32))
+    want = []
+    junk = []
+    for k in range(8):
+        sc = sc64 if k % 3 else sc32
+        runs[k % 2](cam, sc, seeds)
+        want.append(np.array(sc.spheres, np.float32))       # (a copy: sc32 is edited below)
+        # reuse freed blocks of the converted copies' size
+        junk += [np.full((5, 8), -7.0, np.float32) for _ in range(4)]
+        # an in-place edit of the float32 array is still seen (no stale copy)
+        sc32.spheres[0, 0] += 1.0
+    assert len(seen) == len(want)
+    for got, exp in zip(seen, want):
+        assert np.array_equal(got, exp)
+    # the direct (float32) array is passed without a copy
+    runs[0](cam, sc32, seeds)
+    assert np.array_equal(seen[-1], sc32.spheres)
+    pipe._ctx = ctypes.c_void_p()
