@@ -452,22 +452,8 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
         hipError_t e = hipMemcpyAsync(ctx->d_geom, geom.data(), geom.size() * sizeof(float4),
                                       hipMemcpyHostToDevice, stream);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(sphere geometry)");
-        // The device records carry, in a dielectric's unused colour channels (wgsl:102-135
-        // reads only color[0] = ri), RN(1 / ri) and the front face's Schlick r0 =
-        // RN(RN((1 - y) / (1 + y))^2) with y = RN(1 / ri): the one-frame kernel's
-        // RT_SINGLE_DIEL reads them instead of two divisions (the same IEEE f32 operations
-        // as wgsl:104 and wgsl:137-141, so the same bits).  Dielectric = neither
-        // color[3] < -1 nor color[3] <= 1, the kernels' test (NaN included).
-        std::vector<rt_sphere> dev(spheres, spheres + count);
-        for (rt_sphere& d : dev)
-            if (!(d.color[3] < -1.0f) && !(d.color[3] <= 1.0f)) {
-                const float y = 1.0f / d.color[0];
-                float r0 = (1.0f - y) / (1.0f + y);
-                r0 = r0 * r0;
-                d.color[1] = y;
-                d.color[2] = r0;
-            }
-        e = hipMemcpyAsync(ctx->d_sph, dev.data(), count * sizeof(rt_sphere),
+        // the sphere records as the reference uploads them (bytemuck, lib.rs:186)
+        e = hipMemcpyAsync(ctx->d_sph, spheres, count * sizeof(rt_sphere),
                            hipMemcpyHostToDevice, stream);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(sphere records)");
         e = hipStreamSynchronize(stream);
@@ -1213,8 +1199,7 @@ const char* rt_kernel_name(int which) {
                                         "rt_bounce_kernel<1>",     "rt_bounce_kernel<2>",
                                         rtk::single_kernel_name(0),
                                         rtk::single_kernel_name(1),
-                                        "rt_bounce_kernel<3>",
-                                        "rt_trace_kernel<11>"};
+                                        "rt_bounce_kernel<3>"};
     if (which >= 0 && which < (int)(sizeof(names) / sizeof(names[0]))) return names[which];
     return rtk::trace_kernel_name();
 }
@@ -1315,7 +1300,7 @@ rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launch) {
 rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     if (mode != RT_FRAME_PAIRS_AUTO && mode != RT_FRAME_PAIRS_OFF && mode != RT_FRAME_PAIRS_ON &&
-        mode != RT_FRAME_PAIRS_QUAD && mode != RT_FRAME_PAIRS_OCT)
+        mode != RT_FRAME_PAIRS_QUAD)
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown frame-pair mode");
     ctx->frame_pairs = mode;
     return RT_OK;
@@ -1531,9 +1516,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
             const uint64_t tiles = (uint64_t)((w + 7u) >> 3) * p.local_bands;
             const bool quad = ctx->frame_pairs == RT_FRAME_PAIRS_QUAD ||
                               (ctx->frame_pairs == RT_FRAME_PAIRS_AUTO && tiles <= rtk::kQuadMaxTiles);
-            kernel = ctx->frame_pairs == RT_FRAME_PAIRS_OCT ? rtk::kTraceListOct
-                     : quad                                 ? rtk::kTraceListQuad
-                                                            : rtk::kTraceListPair;
+            kernel = quad ? rtk::kTraceListQuad : rtk::kTraceListPair;
         }
         kernel = single_or(ctx, p, kernel);
         const bool aql = chain && nf == 1u &&

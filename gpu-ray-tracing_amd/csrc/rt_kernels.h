@@ -142,9 +142,6 @@ constexpr int kTraceListPair = 3;
 // The same with four waves per tile: for small per-rank shares (few tiles per SIMD), where
 // shorter per-wave frame chains keep more waves resident (rt_abi.cpp picks it).
 constexpr int kTraceListQuad = 4;
-// ... and with eight (opt-in: rt_set_frame_pairs(RT_FRAME_PAIRS_OCT))
-constexpr int kTraceListOct = 11;
-static_assert(kTraceListOct == RT_KERNEL_LIST_OCT, "instance id is the ABI's RT_KERNEL_LIST_OCT");
 static_assert(kTraceExhaustive == RT_KERNEL_EXHAUSTIVE && kTraceCulled == RT_KERNEL_CULLED &&
                   kTraceList == RT_KERNEL_LIST && kTraceListPair == RT_KERNEL_LIST_PAIR &&
                   kTraceListQuad == RT_KERNEL_LIST_QUAD,
@@ -168,7 +165,7 @@ static_assert(kTraceSingle == RT_KERNEL_SINGLE && kTraceSingleOne == RT_KERNEL_S
 #endif
 constexpr uint64_t kSingleOneMaxTiles = RT_SINGLE_ONE_MAX_TILES;
 constexpr bool is_group_kernel(int k) {
-    return k == kTraceListPair || k == kTraceListQuad || k == kTraceListOct;
+    return k == kTraceListPair || k == kTraceListQuad;
 }
 constexpr bool is_list_kernel(int k) { return k == kTraceList || is_group_kernel(k); }
 // Waves (tiles) per workgroup of the one-wave-per-tile instances (kTraceExhaustive,
@@ -238,8 +235,7 @@ const char* single_kernel_name(uint32_t pix);
 // tile_order for launch_trace: the local tiles by decreasing recorded cost (quantised
 // log2 of tile_cost), so the slowest tiles start first and the cheap ones fill the tail.
 hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, uint32_t tiles,
-                             uint32_t tiles_x, hipStream_t stream, uint32_t snake = 0,
-                             uint32_t parts = 1);
+                             uint32_t tiles_x, hipStream_t stream, uint32_t parts = 1);
 // The bounce split schedule's unit order (rt_kernels.hip rt_unit_order_kernel): a tile whose
 // recorded cost exceeds k_thr times the sum of all costs runs as `split` chunks of a
 // 1/split share each, and all units are ordered by their own cost, costliest first.

@@ -34,46 +34,6 @@ namespace rtk {
 
 using namespace rtd;
 
-// Knock-out builds for cost attribution only (tools; never the product): RT_KO bit 1 skips
-// the sphere scan, 2 the shading, 4 the random camera ray, 8 the accumulator load, 16 the
-// store, 32 the accumulator load (keeping the hinted count), 64 the accumulator's divisions
-// of the frame-group path (c = col), 128 the sky's normalisation (uy = d.y), 256 every
-// tile walks tile 0's candidate list (L2-resident lists: the cost of the list misses).
-#ifndef RT_KO
-#define RT_KO 0
-#endif
-
-// ---- diagnostic phase stamps (RT_STAMPS=1 builds only; never in the product) ---------
-#ifndef RT_STAMPS
-#define RT_STAMPS 0
-#endif
-#if RT_STAMPS
-constexpr int kStampWaves = 65536;
-__device__ unsigned long long g_stamp[kStampWaves][8];
-__shared__ unsigned long long s_last[4], s_acc[4][8];
-__device__ __forceinline__ void stamp(int k) {
-    const unsigned w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63u) == 0) {
-        const unsigned long long t = __builtin_amdgcn_s_memtime();
-        if (k == -2)
-            for (int i = 0; i < 8; ++i) s_acc[w][i] = i == 7 ? t : 0;  // [7] = entry time
-        if (k == 0 && s_acc[w][6] == 0) s_acc[w][6] = t - s_acc[w][7];  // entry -> 1st ray
-        else if (k == 0) s_acc[w][0] += t - s_last[w];                  // -> later rays
-        if (k > 0) s_acc[w][k] += t - s_last[w];
-        if (k == 5) s_acc[w][7] = t - s_acc[w][7];                      // lifetime
-        s_last[w] = t;
-        if (k == 5) {
-            const unsigned gw = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + w;
-            if (gw < kStampWaves)
-                for (int i = 0; i < 8; ++i) g_stamp[gw][i] = s_acc[w][i];
-        }
-    }
-}
-#define STAMP(k) stamp(k)
-#else
-#define STAMP(k) ((void)0)
-#endif
-
 // ---- diagnostic wave trace (RT_WAVE_TRACE=1 builds only; never in the product) -------
 // Per wave of the camera-ray-only and bounce instances: start and end s_memrealtime, HW_ID, XCC_ID,
 // indexed by workgroup * 4 + wave (tools/wave_trace.py reads them via rt_diag_wave_trace).
@@ -140,16 +100,13 @@ __device__ __forceinline__ void sst_put(int k, unsigned long long t) {
 __device__ __forceinline__ unsigned long long rt_ballot(bool x) {
     return __builtin_amdgcn_ballot_w64(x);
 }
-// the one-frame kernel (and normalize_w)'s wave-uniform decisions from lane masks (mask_*) instead of ballots
-// (default since round 3 with RT_SINGLE_DISK 3 and RT_ORIGIN_VGPR 1: K3 19.5-19.8 -> 18.9-19.1 µs,
-// K2 13.6-13.8 -> 13.4 µs per update, profiles/r03t_ab_single_masks_all.log)
-#ifndef RT_SINGLE_MASKS
-#define RT_SINGLE_MASKS 1
-#endif
-// Lane masks straight from one compare (llvm.amdgcn.icmp / fcmp: the v_cmp's SGPR result),
-// combined with & and | as 64-bit scalars.  A ballot of a boolean that crosses blocks or
-// combines earlier booleans compiles to a v_cndmask 0/1 + v_cmp_ne round trip (two 4-cycle
-// VALU operations) at every use; these do not (RT_SINGLE_MASKS).
+// The one-frame kernel's (and normalize_w's) wave-uniform decisions come from lane masks
+// (mask_*) instead of ballots: lane masks straight from one compare (llvm.amdgcn.icmp /
+// fcmp: the v_cmp's SGPR result), combined with & and | as 64-bit scalars.  A ballot of a
+// boolean that crosses blocks or combines earlier booleans compiles to a v_cndmask 0/1 +
+// v_cmp_ne round trip (two 4-cycle VALU operations) at every use; these do not (round 3:
+// K3 19.5-19.8 -> 18.9-19.1 µs, K2 13.6-13.8 -> 13.4 µs per update,
+// profiles/r03t_ab_single_masks_all.log).
 __device__ __forceinline__ uint64_t mask_ult(uint32_t a, uint32_t b) {
     return __builtin_amdgcn_uicmp(a, b, 36);          // ICMP_ULT
 }
@@ -286,16 +243,10 @@ constexpr bool kStoreEach = is_list_kernel(kScan);
 // operands), 16 the defocus disk's reciprocal table (disk_unit).  K3 per frame (fused): 21.7 us without, 20.9 / 20.1 / 20.1 us with bits
 // 1 / 1-2 / 1-4; the accumulator's three divisions by f32(n + 1) the same way (checked
 // numerators in [2^-88, 2^88)) measured +0.75 us and are left to the compiler.
-#ifndef RT_FAST_CORES
-#define RT_FAST_CORES 31
-#endif
 // The accumulator's division by f32(n + 1) as RN32(num * RN64(1 / (n + 1))) in the frame
 // groups, where every pixel holds the hinted count n (trace_pair: K3 16.5 against 17.3 us
 // per fused frame; the same in the one-wave loop measured +1.4 us per single-frame update,
 // from its register pressure, and is not used).
-#ifndef RT_ACC_F64
-#define RT_ACC_F64 1
-#endif
 // Exactness of acc_f64: for an integer k <= 2^24 and a quotient q = num / k in the normal
 // f32 range, q never falls on an f32 rounding midpoint (a midpoint has 25 significant bits
 // with an odd last one, so num = midpoint * k would need 25) and lies at least 2^-49
@@ -319,18 +270,10 @@ __device__ __forceinline__ v3 acc_f64(v3 c, v3 num, double y) {
               c.z + (float)((double)num.z * y));
 }
 template <int kScan>
-constexpr bool fast_core(int bit) { return is_list_kernel(kScan) && (RT_FAST_CORES & bit) != 0; }
-// The defocus disk's reciprocal in the camera-ray-only trace instances: 1 = the workgroup's
-// LDS table (one barrier at wave start), 2 = the closed form in registers (disk_rcp_reg)
-#ifndef RT_TRACE_DISK
-#define RT_TRACE_DISK 1
-#endif
-constexpr int kTraceDisk = RT_TRACE_DISK;
-// get_ray: the lens centre copied to VGPRs before the defocus branch (1) or left to the
-// compiler (0)
-#ifndef RT_ORIGIN_VGPR
-#define RT_ORIGIN_VGPR 1
-#endif
+constexpr bool fast_core(int bit) { return is_list_kernel(kScan); }
+// The defocus disk's reciprocal in the camera-ray-only trace instances: the workgroup's LDS
+// table (one barrier at wave start)
+constexpr int kTraceDisk = 1;
 
 // Scan records are read through the constant address space: they do not change during a
 // launch, and only then may the compiler use scalar loads (s_load_dwordx8/16 into SGPRs)
@@ -517,8 +460,8 @@ __device__ __forceinline__ void consider_any(float disc, float h, float a, uint3
     }
 }
 // The grid's launch parameters (TraceParams grid_*), as one value: built from the kernel
-// argument, or (rt_bounce_kernel, RT_BOUNCE_RELOAD) re-read from the kernarg segment at every
-// use so that they do not stay live in SGPRs across the frame loop.
+// argument, or (rt_bounce_kernel) re-read from the kernarg segment at every use so that they
+// do not stay live in SGPRs across the frame loop.
 struct GridP {
     const uint2* cells;
     const float4* geom;
@@ -640,23 +583,17 @@ __device__ __forceinline__ Hit scan_culled(const GridP& gp, const float4* __rest
     // Bounce rays walk the grid whenever the wave may (measured faster than the cone
     // culling even for coherent specular waves); camera rays of tiles without a candidate
     // list keep the cone, whose rays share a narrow beam.
-#ifndef RT_NO_GRID
     if (bounce && count >= kCullMinSpheres && grid_usable(gp, o, d, live))
         return scan_grid(gp, o, d, live);
-#endif
     (void)bounce;
     (void)gp;
     Cone k;
     if (count < kCullMinSpheres || !wave_cone(o, d, live, k))
         return scan_exhaustive<RT_SCAN_CHUNK>(geom, count, o, d);
-    STAMP(2);
     const uint32_t lane = threadIdx.x & 63u;
     const float a = dot(d, d);
     float tmax = 0x1.05ed2ep+118f;
     int idx = -1;
-#ifndef RT_CULL_READLANE
-#define RT_CULL_READLANE 0
-#endif
     for (uint32_t base = 0; base < count; base += 64u) {
         const float4 g = recs[base + lane];
         const bool keep = (base + lane < count) && !cone_misses(k, g);
@@ -664,18 +601,12 @@ __device__ __forceinline__ Hit scan_culled(const GridP& gp, const float4* __rest
         while (mask) {                                    // survivors, in index order
             const int j = __builtin_ctzll(mask);
             mask &= mask - 1ull;
-#if RT_CULL_READLANE
-            const float4 gs = make_float4(lane_f(g.x, j), lane_f(g.y, j), lane_f(g.z, j),
-                                          lane_f(g.w, j));
-#else
             const float4 gs = recs[base + (uint32_t)j];   // broadcast read
-#endif
             float h;
             const float disc = discriminant(gs, o, d, a, h);
             consider(disc, h, a, base + (uint32_t)j, tmax, idx);
         }
     }
-    STAMP(3);
     return Hit{idx, tmax};
 }
 
@@ -817,12 +748,9 @@ __device__ __forceinline__ void disk_unit(float sa, float ca, float& ux, float& 
     }
 }
 
-// RT_SINCOS_FIN: no NaN guard on the lens sample's quadrant in get_ray (its angle is finite).
-// Default since round 4: K3 14.26 against 14.42 µs per update over three interleaved rounds;
-// RT_SINGLE_FRONT measured neutral (profiles/r04/r04q_ab_front_fin.txt)
-#ifndef RT_SINCOS_FIN
-#define RT_SINCOS_FIN 1
-#endif
+// The lens sample's sincos runs without a NaN guard on its quadrant (the angle is finite):
+// K3 14.26 against 14.42 µs per update over three interleaved rounds
+// (profiles/r04/r04q_ab_front_fin.txt).
 // get_ray (wgsl:305-325) with the pixel-invariant hash(hash(x*73) ^ hash(y*51)) part
 // precomputed per pixel: seed = hash(hxy ^ su), su = sample_index*25 + B (wave-uniform
 // when every pixel of the wave holds the same sample count).
@@ -838,20 +766,16 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
     const float sx = ((float)x + 0.5f) + offx;
     const float sy = ((float)y + 0.5f) + offy;
     const v3 pc = fmas(sy, cam.pdv, fmas(sx, cam.pdu, cam.vul));
-#if RT_ORIGIN_VGPR
     // the lens centre in VGPRs first (the copies the lens-less path needs anyway), so that
     // fma(u, ddu, centre) has one scalar operand (gfx950 VALU: one SGPR per instruction)
     // instead of a second copy per component
     v3 c0 = cam.center;
     asm volatile("" : "+v"(c0.x), "+v"(c0.y), "+v"(c0.z));
-#else
-    const v3 c0 = cam.center;
-#endif
     if (cam.defocus_angle > 0.0f) {                     // defocus_disk_sample wgsl:327-331
         const float ang = (float)hash(seed + 1u) * 0x1.921fb4p-30f;  // 2*3.1415926 * rf
         float sa, ca, ux, uy;
-        // (ang = f32(hash) * 2pi 2^-32: always finite, RT_SINCOS_FIN drops the NaN guard)
-        sincos_k(ang, sa, ca, cam.k1s, cam.k1c, RT_SINCOS_FIN != 0);
+        // (ang = f32(hash) * 2pi 2^-32: always finite, so no NaN guard)
+        sincos_k(ang, sa, ca, cam.k1s, cam.k1c, true);
         disk_unit<kTable>(sa, ca, ux, uy);
         o = fmas(uy, cam.ddv, fmas(ux, cam.ddu, c0));
     } else {
@@ -866,14 +790,11 @@ __device__ __forceinline__ v3 sel3(bool c, v3 a, v3 b) {
     return mk(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z);
 }
 
-// RT_SKY_RSQ: the reciprocal of |v| in the sky's normalize(d).y and in normalize_w from the
-// square root's own rsq (sqrt_core_rcp) instead of a second transcendental (v_rcp).  On by
-// default since round 4, with RT_SINGLE_UNIF, RT_SINGLE_AND and RT_SINGLE_CHUNK = 1 (the
-// "all4" build: K3 14.95 -> 14.68 µs per update over three interleaved rounds, 816 GPU tests
-// green on it; profiles/r04/r04k_ab_single_variants.txt)
-#ifndef RT_SKY_RSQ
-#define RT_SKY_RSQ 1
-#endif
+// The reciprocal of |v| in the sky's normalize(d).y and in normalize_w comes from the square
+// root's own rsq (sqrt_core_rcp) instead of a second transcendental (v_rcp).  Adopted in
+// round 4 with the one-frame kernel's select skipping, the AND sign test and one record per
+// tile and step (K3 14.95 -> 14.68 µs per update over three interleaved rounds;
+// profiles/r04/r04k_ab_single_variants.txt).
 // normalize(v) = v / sqrt(v.v) (WGSL normalize).  kFast: when every active lane's |v|^2 is
 // in [2^-20, 2^40] (NaN, 0 and inf are not) and its components are >= 2^-100 in
 // magnitude, sqrt_core and div_core with the shared reciprocal of |v| in [2^-10, 2^20]
@@ -884,12 +805,9 @@ __device__ __forceinline__ v3 normalize_w(v3 v) {
         const float dd = dot(v, v);
         const uint32_t span = __float_as_uint(dd) - kBits2m20;
         const uint32_t vmin = min(min(abs_bits(v.x), abs_bits(v.y)), abs_bits(v.z));
-        const bool in = span < kBits2p40 - kBits2m20 && vmin >= kBits2m100;
-        if ((RT_SINGLE_MASKS ? (mask_uge(span, kBits2p40 - kBits2m20) | mask_ult(vmin, kBits2m100))
-                             : rt_ballot(!in)) == 0ull) {
+        if ((mask_uge(span, kBits2p40 - kBits2m20) | mask_ult(vmin, kBits2m100)) == 0ull) {
             float y;
-            const float len = RT_SKY_RSQ ? sqrt_core_rcp(dd, y) : sqrt_core(dd);
-            if (!RT_SKY_RSQ) y = rcp_refined(len);
+            const float len = sqrt_core_rcp(dd, y);
             return mk(div_core(v.x, len, y), div_core(v.y, len, y), div_core(v.z, len, y));
         }
     }
@@ -917,10 +835,7 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
         // so the same chunk loop applies; hit.idx then indexes the tile's copy of the
         // sphere records.
         const bool listed = kScan != kTraceExhaustive && i == 0 && ncand != kCandNone;
-        const float4* blk = p.cand + ((RT_KO & 256) ? 0 : (size_t)tile * kCandStride);
-#if RT_KO & 1
-        const Hit hit = Hit{-1, 0.0f};
-#else
+        const float4* blk = p.cand + (size_t)tile * kCandStride;
         // (one inlined walk for both pointers: two copies measured slower)
         const Hit hit =
             (kScan != kTraceCulled || listed)
@@ -928,19 +843,12 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
                       listed ? blk + kCandRecOff : p.geom, listed ? ncand : p.count, o, d)
             : p.lds_records ? scan_culled<true>(grid_params(p), p.geom, p.count, o, d, live, i > 0)
                             : scan_culled<false>(grid_params(p), p.geom, p.count, o, d, live, i > 0);
-#endif
-        if (kScan != kTraceCulled) STAMP(2);                      // (culled: inside the scan)
         const float4* hs = listed ? blk + kCandSphOff : p.sph;
         if (!live) continue;
         if (hit.idx < 0) {                                        // wgsl:288-290
             live = false;
             continue;
         }
-#if RT_KO & 2
-        cf = mk(hit.t, hit.t, hit.t);
-        live = false;
-        continue;
-#endif
         // Hit record of the winner (wgsl:205-218).  The two record loads are per-lane and
         // depend on the scan; the scatter's random numbers do not depend on the material
         // (lambertian and metal draw random_unit_vector(sb), dielectric draws rf(sb), its
@@ -1013,9 +921,6 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
     // with either quotient.
     const float dd = dot(d, d);
     float uy;
-#if RT_KO & 128
-    uy = d.y * (dd > -1.0f ? 1.0f : 0.5f);
-#else
     if (fast_core<kScan>(4) &&
         rt_ballot(__float_as_uint(dd) - kBits2m20 >= kBits2p40 - kBits2m20) == 0ull) {
         const float len = sqrt_core(dd);
@@ -1023,7 +928,6 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
     } else {
         uy = d.y / sqrtf(dd);
     }
-#endif
     const float a = 0.5f * (uy + 1.0f);
     const float om = 1.0f - a;
     return mul(cf, mk(fmaf(a, 0.5f, om), fmaf(a, 0x1.666666p-1f, om), fmaf(a, 1.0f, om)));
@@ -1066,17 +970,9 @@ __device__ __forceinline__ v3 sample(const TraceParams& p, const Cam& cam, uint3
     const uint32_t depth = p.depth;
     const uint32_t seed = 1u + n + B;                             // wgsl:353
     v3 o, d;
-    STAMP(0);
-#if RT_KO & 4
-    o = cam.center;
-    d = sub(fmas((float)tc.y, cam.pdv, fmas((float)tc.x, cam.pdu, cam.vul)), o);
-#else
     get_ray<fast_core<kScan>(16) ? kTraceDisk : 0>(cam, tc.x, tc.y, hxy, seed * 25u + B, o,
                                                   d);                          // wgsl:311
-#endif
-    STAMP(1);
     const v3 col = ray_color<kScan>(p, tile, ncand, depth, o, d, seed + 1u, live, uni, f);
-    STAMP(4);
     return col;
 }
 
@@ -1157,26 +1053,12 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 // one GPU: 16.8 / 18.8 us; 8-rank share: 3.13 / 2.95 us (`profiles/r01_rank_sim_groups_k3.txt`).
 template <int kScan>
 constexpr uint32_t frame_group() {
-    return kScan == kTraceListOct ? 8u : kScan == kTraceListQuad ? 4u : 2u;
+    return kScan == kTraceListQuad ? 4u : 2u;
 }
-// RT_GROUP_FLAGS: the frame group's hand-off without a workgroup barrier per group: a ring of
-// kGroupSlots colour slots with LDS counters — a producer wave writes its colours into the
-// group's slot once wave 0 has consumed the group kGroupSlots before it, then counts its
-// arrival (release); wave 0 waits for the group's arrivals (acquire), accumulates, frees
-// the slot.  The producers run up to kGroupSlots - 1 groups ahead instead of waiting at every
-// group's barrier for wave 0's accumulation and image stores.
-#ifndef RT_GROUP_FLAGS
-#define RT_GROUP_FLAGS 0
-#endif
-constexpr uint32_t kGroupSlots = 4;
+// LDS of a frame group: two slots of the producer waves' colours (double-buffered groups)
 template <int kScan>
 constexpr size_t group_lds_bytes() {
-    return RT_GROUP_FLAGS ? (size_t)kGroupSlots * (frame_group<kScan>() - 1u) * 64u * 16u + 64u
-                          : (size_t)2u * (frame_group<kScan>() - 1u) * 64u * 16u;
-}
-__device__ __forceinline__ uint32_t lds_acquire(const uint32_t* a) {
-    return __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+    return (size_t)2u * (frame_group<kScan>() - 1u) * 64u * 16u;
 }
 template <int kScan>
 __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam, uint32_t tile,
@@ -1189,70 +1071,6 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
     // bookkeeping, rt_abi.cpp fill_hint): the count arithmetic of wgsl:341-362 is scalar.
     const uint32_t lane = threadIdx.x & 63u;
     constexpr uint32_t kFrameGroup = frame_group<kScan>();
-#if RT_GROUP_FLAGS
-    // ctr[k]: producers arrived in slot k; ctr[kGroupSlots]: groups wave 0 has consumed
-    uint32_t* ctr = reinterpret_cast<uint32_t*>(lds_recs + kGroupSlots * (kFrameGroup - 1u) * 64u);
-    if (threadIdx.x <= kGroupSlots) ctr[threadIdx.x] = 0u;
-    __syncthreads();
-    for (uint32_t f = 0, g = 0; f < p.frames; f += kFrameGroup, ++g) {
-        const uint32_t fw = f + w;
-        v3 col = mk(0.0f, 0.0f, 0.0f);
-        if (fw < p.frames) {
-            const uint32_t ng = p.hint_n[fw];
-            if (ng < spp && rt_ballot(tc.valid) != 0ull)           // wgsl:352
-                col = sample<kScan>(p, cam, tile, ncand, tc, hxy, ng, p.seed_b[fw], fw,
-                                    tc.valid, fw < p.hint_frames);
-        }
-        const uint32_t k = g % kGroupSlots;
-        float4* slot = lds_recs + k * (kFrameGroup - 1u) * 64u;
-        if (w != 0u) {
-            // the slot is free once wave 0 has consumed group g - kGroupSlots (every wait is
-            // bounded — about 2^20 sleeps — so that no wave can spin forever)
-            for (uint32_t spin = 0; g >= kGroupSlots &&
-                                    lds_acquire(&ctr[kGroupSlots]) + kGroupSlots <= g &&
-                                    spin < (1u << 20); ++spin)
-                __builtin_amdgcn_s_sleep(1);
-            slot[(w - 1u) * 64u + lane] = make_float4(col.x, col.y, col.z, 0.0f);
-            if (lane == 0u)
-                __hip_atomic_fetch_add(&ctr[k], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            continue;
-        }
-        for (uint32_t spin = 0; lds_acquire(&ctr[k]) < kFrameGroup - 1u && spin < (1u << 20);
-             ++spin)
-            __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-        for (uint32_t j = 0; j < kFrameGroup; ++j) {
-            const uint32_t fj = f + j;
-            if (fj >= p.frames) break;
-            if (j != 0) {
-                const float4 cj = slot[(j - 1u) * 64u + lane];
-                col = mk(cj.x, cj.y, cj.z);
-            }
-            const uint32_t nb = p.hint_n[fj];                     // count before frame fj
-            uint32_t na = nb;
-            if (nb < spp) {                                       // wgsl:352-358
-                const v3 num = sub(col, c);
-                if (RT_ACC_F64 && nb < (1u << 24) && rt_ballot(tc.valid && !acc_f64_ok(num)) == 0ull) {
-                    c = acc_f64(c, num, p.hint_rcp[fj]);
-                } else {
-                    const float kk = (float)(nb + 1u);            // wgsl:356
-                    c = mk(c.x + num.x / kk, c.y + num.y / kk, c.z + num.z / kk);
-                }
-                na = nb + 1u;
-            }
-            if ((p.store_each == 2u || fj + 2u >= p.frames) && tc.valid)       // wgsl:362-363
-                ((fj & 1u) ? p.out2 : p.out)[tc.idx] = make_float4(c.x, c.y, c.z, (float)na);
-        }
-        // the slot's colours are read (the loads above completed: their values are used):
-        // free it for group g + kGroupSlots
-        if (lane == 0u) {
-            __hip_atomic_store(&ctr[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&ctr[kGroupSlots], g + 1u, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    }
-    return;
-#endif
     for (uint32_t f = 0; f < p.frames; f += kFrameGroup) {
         const uint32_t fw = f + w;
         v3 col = mk(0.0f, 0.0f, 0.0f);
@@ -1279,19 +1097,15 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
                 const uint32_t nb = p.hint_n[fj];                 // count before frame fj
                 uint32_t na = nb;
                 if (nb < spp) {                                   // wgsl:352-358
-#if RT_KO & 64
-                    c = col;
-#else
                     const v3 num = sub(col, c);
                     // num / f32(nb + 1) (wgsl:356) as RN32(num * RN64(1 / k)) (acc_f64)
-                    if (RT_ACC_F64 && nb < (1u << 24) &&
+                    if (nb < (1u << 24) &&
                         rt_ballot(tc.valid && !acc_f64_ok(num)) == 0ull) {
                         c = acc_f64(c, num, p.hint_rcp[fj]);
                     } else {
                         const float k = (float)(nb + 1u);         // wgsl:356
                         c = mk(c.x + num.x / k, c.y + num.y / k, c.z + num.z / k);
                     }
-#endif
                     na = nb + 1u;
                 }
                 // wgsl:362-363: the images that survive (or every frame's, store_each 2)
@@ -1326,9 +1140,6 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
 // its first instruction of ray setup).
 // Image accesses of the trace kernel as non-temporal (streaming) loads (bit 1) / stores
 // (bit 2), so that the per-frame image traffic does not evict the candidate lists from L2.
-#ifndef RT_NT_IMAGE
-#define RT_NT_IMAGE 0
-#endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 nt_load(const float4* a) {
     const f32x4 v = __builtin_nontemporal_load((const f32x4*)a);
@@ -1338,9 +1149,6 @@ __device__ __forceinline__ void nt_store(float4 v, float4* a) {
     const f32x4 w = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(w, (f32x4*)a);
 }
-#ifndef RT_KARG_PREFETCH
-#define RT_KARG_PREFETCH 1
-#endif
 // Leading scalar arguments of rt_trace_kernel (before the TraceParams block): what a wave
 // needs before its first ray — the tile's candidate count, the seed-hash tables, the
 // accumulator and the tile geometry.  Built with -mllvm -amdgpu-kernarg-preload-count=9
@@ -1405,7 +1213,6 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const TraceParams p) {
-    STAMP(-2);
     WAVE_TRACE(0);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tiles_x = (a_width + 7u) >> 3;
@@ -1433,25 +1240,15 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     // per-column / per-row tables: issued from the preloaded arguments, before the
     // kernel-argument prefetch below is awaited
     const uint32_t ncand = (kScan != kTraceExhaustive && a_cand && wave_in)
-                               ? load_cnt(a_cand, (RT_KO & 256) ? 0 : tile)
+                               ? load_cnt(a_cand, tile)
                                : kCandNone;
-#if RT_KO & 8
-    const float4 acc = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-#elif RT_KO & 32
-    // knock-out: no accumulator load; the count the hint expects (so no retrace)
-    const float4 acc = make_float4(0.0f, 0.0f, 0.0f, (float)p.hint_n[0]);
-#else
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     // (loaded even when frame 0 resets the pixel or the wave has no tile, so that the load
     // waits for no kernarg read and no branch; the value is discarded then)
-    if (RT_NT_IMAGE & 1)
-        acc = nt_load(&a_in[tc.valid ? tc.idx : 0]);
-    else
-        acc = a_in[tc.valid ? tc.idx : 0];
-#endif
+    acc = a_in[tc.valid ? tc.idx : 0];
     const uint32_t hxy =
         a_hx[min(tc.x, a_width - 1u)] ^ a_hx[hy_offset(a_width) + min(tc.y, a_height - 1u)];
-    if (RT_KARG_PREFETCH && kScan == kTraceList) karg_prefetch();
+    if (kScan == kTraceList) karg_prefetch();
     // Culled scan: the workgroup stages the scan records (count padded to 64) in LDS once;
     // the per-block cone test then reads them at LDS latency instead of L2 latency.
     if (kScan == kTraceCulled && p.lds_records) {
@@ -1493,19 +1290,10 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
     }
     const float4 res = trace_pixel<kScan, !is_group_kernel(kScan)>(p, cam, tile, ncand, tc,
                                                                    hxy, acc);
-#if RT_KO & 16
-    if (res.x == 12345.678f) p.out[tc.idx] = res;
-#else
-    if (tc.valid && !(kStoreEach<kScan> && p.store_each)) {      // wgsl:363
-        if (RT_NT_IMAGE & 2)
-            nt_store(res, &p.out[tc.idx]);
-        else
-            p.out[tc.idx] = res;
-    }
-#endif
+    if (tc.valid && !(kStoreEach<kScan> && p.store_each))        // wgsl:363
+        p.out[tc.idx] = res;
     record_cost<kScan>(p, tile, wave, lane);
     WAVE_TRACE(1);
-    STAMP(5);
 }
 
 // ---- Single-frame update (kTraceSingle): one `update` dispatch, camera rays only --------
@@ -1531,18 +1319,15 @@ struct SingleParams {
     uint32_t seed_b;       // B = u32(random_seed * 2^32) (wgsl:311, 353)
     uint32_t hy_off;       // hash(y * 51) table offset in the hx buffer
     double rcp_hint;       // RN64(1 / (n_hint + 1))
-    // RT_SINGLE_NCHK: n_hint < 2^24 (n_exact), the bits of f32(n_hint) and of f32(the count
-    // after the frame): a pixel holding exactly f32(n_hint) holds the hinted count
-    uint32_t n_exact, ng_bits, n_after_bits;
+    // (12 unused bytes: the kernels' register allocation and kernarg loads were tuned and
+    // measured with the fields after them at these offsets)
+    uint32_t reserved[3];
     // local bands of a launch in raster order (no a_order): lband = first + blockIdx.y *
     // step, first | step << 16 — one of the update's concurrent parts (launch_single)
     uint32_t lbands;
     float4 rs;             // (rf(sb), random_unit_vector(sb)) of frame 0, bounce 0
     float center[3], vul[3], pdu[3], pdv[3], ddu[3], ddv[3];
     float defocus_angle;
-#if RT_SINGLE_DISK == 1
-    double disk_rcp[8];    // (the LDS-table form only: every byte here is host launch cost)
-#endif
     // the launch's workgroups per row (rt_chain_kernel reads it here instead of the hidden
     // kernel arguments: its packets are written by rt_chain.cpp)
     uint32_t grid_x;
@@ -1564,9 +1349,6 @@ static_assert(kSinglePix >= 1 && kSinglePix <= 4, "1 to 4 tiles per wave");
 #ifndef RT_SINGLE_MIN_WAVES
 #define RT_SINGLE_MIN_WAVES 7
 #endif
-#ifndef RT_SINGLE_ACC_F64
-#define RT_SINGLE_ACC_F64 1
-#endif
 // Knock-out builds of the one-frame kernel (cost attribution only, never the product):
 // bit 1 no accumulator load, 2 no sphere scan, 4 no random camera ray, 8 no hit shading,
 // 16 no image store.
@@ -1579,26 +1361,8 @@ static_assert(kSinglePix >= 1 && kSinglePix <= 4, "1 to 4 tiles per wave");
 #define RT_SINGLE_WG 2
 #endif
 constexpr uint32_t kSingleWg = RT_SINGLE_WG;
-// RT_SINGLE_PRIO: the first RT_SINGLE_PRIO workgroups of wg_order (the costliest) run at
-// raised wave priority (s_setprio), so that on a SIMD shared with cheap waves the launch's
-// longest waves issue first; 0 = off.
-#ifndef RT_SINGLE_PRIO
-#define RT_SINGLE_PRIO 0
-#endif
-// sphere scan of the one-frame kernel: 0 = both tiles' lists in one loop, RT_LIST_CHUNK
-// records of each per step; k > 0 = each tile's list on its own, k records per step
-#ifndef RT_SINGLE_SCAN
-#define RT_SINGLE_SCAN 0
-#endif
-// records per tile and step of the joint list walk (both tiles' lists in one loop): 1 since
-// round 4 (fewer padding records tested when the two lists differ in length; see RT_SKY_RSQ)
-#ifndef RT_SINGLE_CHUNK
-#define RT_SINGLE_CHUNK 1
-#endif
-// skip the hit shading of a tile none of whose rays hit
-#ifndef RT_SINGLE_GATE
-#define RT_SINGLE_GATE 0
-#endif
+// The one-frame kernel walks both tiles' candidate lists in one loop, one record of each per
+// step (round 4: fewer padding records tested when the two lists differ in length).
 // The tiles' 1-KB candidate blocks are loaded whole at wave start (one 16-B load per lane,
 // beside the seed and accumulator loads) and kept in LDS: the scan records and the hit
 // records are then LDS reads instead of dependent L2/HBM round trips.  It shortens a
@@ -1608,29 +1372,12 @@ constexpr uint32_t kSingleWg = RT_SINGLE_WG;
 #ifndef RT_SINGLE_LDS
 #define RT_SINGLE_LDS 1
 #endif
-#ifndef RT_SINGLE_WT
-#define RT_SINGLE_WT 1
-#endif
-// wave-invariant constants of the camera ray kept in VGPRs (1) or left to the compiler (0)
-#ifndef RT_SINGLE_VCONST
-#define RT_SINGLE_VCONST 0
-#endif
-// the hinted count checked as the f32 bits of the stored count (1) or through f2u (0)
-#ifndef RT_SINGLE_NCHK
-#define RT_SINGLE_NCHK 0
-#endif
-// The defocus disk's reciprocal in the one-frame kernel: 1 = the workgroup's LDS table
-// (filled by wave 0 from the launch parameters, one barrier), 2 = its closed form in
-// registers (disk_rcp_reg: no table, no barrier), 3 = all-f32 (disk_unit<3>: the length and
-// its reciprocal from the bits of len2, one Markstein step; no f64).  2 over 1: K3 23.30 ->
-// 22.46 us, K2 17.13 -> 16.0 us per update, 8-rank K3 share 6.26 -> 5.52 us
-// (profiles/r03a_ab_single.log): the barrier made every wave of a workgroup wait for wave 0's
-// kernarg read at wave start.  3 (default since round 3, with RT_SINGLE_MASKS and
-// RT_ORIGIN_VGPR): profiles/r03t_ab_single_masks_all.log.
-#ifndef RT_SINGLE_DISK
-#define RT_SINGLE_DISK 3
-#endif
-constexpr int kSingleDisk = RT_SINGLE_DISK;
+// The defocus disk's reciprocal in the one-frame kernel is all-f32 (disk_unit<3>: the length
+// and its reciprocal from the bits of len2, one Markstein step; no f64, no LDS table, no
+// barrier).  The workgroup's LDS table made every wave wait for wave 0's kernarg read at
+// wave start (K3 23.30 -> 22.46 µs per update without it, profiles/r03a_ab_single.log); the
+// all-f32 form with the lane masks: profiles/r03t_ab_single_masks_all.log.
+constexpr int kSingleDisk = 3;
 // hash(x*73) ^ hash(y*51) (wgsl:309-310) of the one-frame kernel: from the per-column /
 // per-row tables (two dependent loads behind the order entry) or computed in the wave —
 // one hash per lane (lanes [0, 8*kPix) the wave's columns, the next 8 its rows), handed to
@@ -1643,64 +1390,15 @@ constexpr int kSingleDisk = RT_SINGLE_DISK;
 #define RT_SINGLE_HASH 1
 #endif
 
-
-// RT_SINGLE_UNIF: the one-frame kernel's per-lane selects after the hit shading (hit /
-// miss, the degenerate scatter direction, metal absorption) only in waves whose lanes
-// differ — a wave-uniform branch on a lane mask skips them otherwise (default since round 4,
-// see RT_SKY_RSQ)
-#ifndef RT_SINGLE_UNIF
-#define RT_SINGLE_UNIF 1
-#endif
-// RT_SINGLE_AND: "some discriminant of the chunk is not negative" as the sign of the AND of
-// their bit patterns (one 2-cycle v_and per record instead of a 4-cycle v_max_i32).  Exact
-// on the camera-ray domain the host proves for these instances: every discriminant is
-// finite (|h|, sqrt(D) <= 2^53, consider_fast) and never -0 (max_bits above), so its sign bit
-// is set exactly when it is < 0.  (Default since round 4, see RT_SKY_RSQ.)
-#ifndef RT_SINGLE_AND
-#define RT_SINGLE_AND 1
-#endif
-
-// RT_SINGLE_FRONT: the hit normal's face flip (wgsl:217-220) as per-lane selects only in a
-// wave with a back-face hit
-#ifndef RT_SINGLE_FRONT
-#define RT_SINGLE_FRONT 0
-#endif
-// RT_SINGLE_SKYDD: the sky's |d|^2 (wgsl:294's normalize) taken from where the direction was
-// made — the camera ray's a = d.d (wgsl:184, computed for the scan), the Lambertian scatter's
-// |n + ruv|^2 (computed for its degenerate-direction test, wgsl:89), or the normalised
-// metal / dielectric direction's own dot — instead of one more dot product per pixel (the
-// same operations on the same operands: the same bits).  Default since round 4: 828 GPU
-// tests green on it; K3 14.51 against 14.56 µs per update at the default length, 15.93
-// against 16.37 in the driver's command (profiles/r04/r04p_ab_skydd.txt, three rounds each)
-#ifndef RT_SINGLE_SKYDD
-#define RT_SINGLE_SKYDD 1
-#endif
-// RT_SINGLE_DIEL: the one-frame kernel's dielectric scatter with the sphere's precomputed
-// RN(1 / ri) and front-face r0 (rt_abi.cpp upload_spheres) and checked fast square roots
-#ifndef RT_SINGLE_DIEL
-#define RT_SINGLE_DIEL 0
-#endif
-// sqrtf(x) through sqrt_core when every active lane's x is finite and >= 2^-96 (or
-// negative: both give NaN there), the IEEE operation otherwise
-constexpr uint32_t kBits2m96 = 0x0F800000u;   // 2^-96
-__device__ __forceinline__ float sqrt_checked(float x) {
-    const uint32_t b = __float_as_uint(x);
-    // out of the domain: +-0, [0, 2^-96) and +inf / NaN of either sign ... as an unsigned range
-    // on the magnitude bits: |x| < 2^-96 or |x| >= +inf
-    const uint32_t m = b & 0x7FFFFFFFu;
-    if (__builtin_amdgcn_uicmp(m - kBits2m96, 0x7F800000u - kBits2m96, 35) == 0ull)   // UGE
-        return sqrt_core(x);
-    return sqrtf(x);
-}
-// WGSL refract (rt_device.h) with sqrt_checked
-__device__ __forceinline__ v3 refract_checked(v3 e1, v3 e2, float eta) {
-    const float d = dot(e2, e1);
-    const float k = fmaf(-(eta * eta), fmaf(-d, d, 1.0f), 1.0f);
-    if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
-    const float m = fmaf(eta, d, sqrt_checked(k));
-    return mk(fmaf(eta, e1.x, -(m * e2.x)), fmaf(eta, e1.y, -(m * e2.y)),
-              fmaf(eta, e1.z, -(m * e2.z)));
-}
+// The one-frame kernel's per-lane selects after the hit shading (hit / miss, the degenerate
+// scatter direction, metal absorption) run only in waves whose lanes differ: a wave-uniform
+// branch on a lane mask skips them otherwise (round 4, with sqrt_core_rcp above).  The
+// sky's |d|^2 (wgsl:294's normalize) is taken from where the direction was made — the
+// camera ray's a = d.d (wgsl:184, computed for the scan), the Lambertian scatter's
+// |n + ruv|^2 (computed for its degenerate-direction test, wgsl:89), or the normalised metal
+// / dielectric direction's own dot — instead of one more dot product per pixel (the same
+// operations on the same operands: the same bits; K3 15.93 against 16.37 µs per update in
+// the driver's command, profiles/r04/r04p_ab_skydd.txt).
 
 // Shading of a camera ray's hit at depth 1 (ray_color's loop body at i = 0, wgsl:266-286):
 // sets the scattered direction and attenuation, or black (metal absorbed).  r_sb / ruv are
@@ -1712,8 +1410,7 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
     const v3 rel = sub(hp, mk(pr.x, pr.y, pr.z));
     v3 outward;                                                   // wgsl:209
     const uint32_t rel_min = min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z));
-    if ((RT_SINGLE_MASKS ? (mask_ult(rel_min, kBits2m100) & hm)
-                         : rt_ballot(hit && rel_min < kBits2m100)) == 0ull) {
+    if ((mask_ult(rel_min, kBits2m100) & hm) == 0ull) {
         const float y = rcp_refined(pr.w);
         outward = mk(div_core(rel.x, pr.w, y), div_core(rel.y, pr.w, y),
                      div_core(rel.z, pr.w, y));
@@ -1722,22 +1419,15 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
     }
     const float dno = dot(d, outward);
     const bool front = dno < 0.0f;
-    v3 n = outward;
-    if (!RT_SINGLE_FRONT || (mask_not_lt(dno, 0.0f) & hm) != 0ull) {
-        // (a back-face hit in the wave: per-lane selects; camera rays from outside every
-        // sphere only hit front faces)
-        if (RT_SINGLE_FRONT) asm volatile("");
-        n = front ? outward : neg(outward);
-    }
+    const v3 n = front ? outward : neg(outward);
     // lambertian (wgsl:84-93), computed for every lane; the other materials below
     v3 dir = add(n, ruv);
     const float ddir = dot(dir, dir);
-    ndd = ddir;                     // |nd|^2 for the sky (RT_SINGLE_SKYDD)
-    if (!RT_SINGLE_UNIF ||
-        (__builtin_amdgcn_fcmpf(ddir, 0x1.0c6f7ap-20f, 4) & hm) != 0ull) {   // (FCMP_OLT)
+    ndd = ddir;                     // |nd|^2 for the sky (sky_w's dd)
+    if ((__builtin_amdgcn_fcmpf(ddir, 0x1.0c6f7ap-20f, 4) & hm) != 0ull) {   // (FCMP_OLT)
         // (the degenerate scatter direction, wgsl:89-91: per-lane selects only in a wave
         // that has one)
-        if (RT_SINGLE_UNIF) asm volatile("");
+        asm volatile("");
         if (ddir < 0x1.0c6f7ap-20f) {
             dir = n;
             ndd = dot(n, n);
@@ -1748,39 +1438,13 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
     black = false;
     took_other = false;
     const bool other = hit && !(mat.w < -1.0f);
-    if ((RT_SINGLE_MASKS ? (mask_not_lt(mat.w, -1.0f) & hm) : rt_ballot(other)) != 0ull)
+    if ((mask_not_lt(mat.w, -1.0f) & hm) != 0ull)
         took_other = true;
-    if ((RT_SINGLE_MASKS ? (mask_not_lt(mat.w, -1.0f) & hm) : rt_ballot(other)) != 0ull &&
-        other) {
+    if ((mask_not_lt(mat.w, -1.0f) & hm) != 0ull && other) {
         if (mat.w <= 1.0f) {                                      // metal wgsl:95-100
             const v3 refl = fmas(mat.w, ruv, normalize_w<true>(reflect(d, n)));
             black = !(dot(refl, n) > 0.0f);                       // wgsl:277-279
             nd = normalize_w<true>(refl);
-            ndd = dot(nd, nd);
-        } else if (RT_SINGLE_DIEL) {                              // dielectric wgsl:102-135
-            // the sphere's RN(1 / ri) and the front face's r0 from its record (upload_spheres
-            // fills the unused colour channels of a dielectric: the same IEEE operations on
-            // the host); the square roots through sqrt_core when every lane's operand is in
-            // its domain
-            att = mk(1.0f, 1.0f, 1.0f);
-            const float ratio = front ? mat.y : mat.x;
-            const v3 u = normalize_w<true>(d);
-            const float cos_t = fminf(dot(neg(u), n), 1.0f);
-            const float s2 = fmaf(-cos_t, cos_t, 1.0f);
-            const float sin_t = sqrt_checked(s2);
-            const bool cannot = ratio * sin_t > 1.0f;
-            float r0 = mat.z;
-            if (__builtin_amdgcn_ballot_w64(!front) != 0ull) {   // (back faces: wgsl:138)
-                asm volatile("");
-                if (!front) {
-                    r0 = (1.0f - ratio) / (1.0f + ratio);
-                    r0 = r0 * r0;
-                }
-            }
-            const float x = 1.0f - cos_t;
-            const float x2 = x * x;
-            const bool refl = cannot || fmaf(1.0f - r0, (x2 * x2) * x, r0) > r_sb;
-            nd = normalize_w<true>(refl ? reflect(u, n) : refract_checked(u, n, ratio));
             ndd = dot(nd, nd);
         } else {                                                  // dielectric wgsl:102-135
             att = mk(1.0f, 1.0f, 1.0f);
@@ -1800,14 +1464,9 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
 __device__ __forceinline__ v3 sky_w(v3 cf, v3 d, float dd) {
     float uy;
     if (rt_ballot(__float_as_uint(dd) - kBits2m20 >= kBits2p40 - kBits2m20) == 0ull) {
-        if (RT_SKY_RSQ) {
-            float y;
-            const float len = sqrt_core_rcp(dd, y);
-            uy = div_core(d.y, len, y);
-        } else {
-            const float len = sqrt_core(dd);
-            uy = div_core(d.y, len, rcp_refined(len));
-        }
+        float y;
+        const float len = sqrt_core_rcp(dd, y);
+        uy = div_core(d.y, len, y);
     } else {
         uy = d.y / sqrtf(dd);
     }
@@ -1823,21 +1482,6 @@ __device__ __forceinline__ v3 sky_w(v3 cf, v3 d) { return sky_w(cf, d, dot(d, d)
 // ncand[s] its count (kCandNone: the full list; 0 for a tile past the image edge).
 template <uint32_t S>
 constexpr bool kSingleLds = RT_SINGLE_LDS == 2 || (RT_SINGLE_LDS == 1 && S == 1);
-// RT_SINGLE_LDS_HIT: the multi-tile instance stages its tiles' candidate blocks in LDS too,
-// but for the hit records only (the scan keeps its scalar record loads): the hit sphere's
-// record is then an LDS read instead of a dependent L2 round trip before the shading
-#ifndef RT_SINGLE_LDS_HIT
-#define RT_SINGLE_LDS_HIT 0
-#endif
-// RT_SINGLE_SPREF: the joint list walk also loads each entry's 32-B sphere record with scalar
-// loads beside its scan record (wave-uniform: the entry is the tile's), and a lane whose best
-// hit changes keeps that record in VGPRs — the shading then starts without the dependent
-// load of the hit record after the scan
-#ifndef RT_SINGLE_SPREF
-#define RT_SINGLE_SPREF 0
-#endif
-template <uint32_t S>
-constexpr bool kSingleLdsHit = kSingleLds<S> || (RT_SINGLE_LDS_HIT && S > 1);
 template <uint32_t S, bool kUniRs>
 __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& cam,
                                               const TileCoord (&tc)[S],
@@ -1849,7 +1493,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                                               const uint64_t (&live_m)[S],
                                               const float4 (&bv)[S], float4* lblk,
                                               v3 (&col)[S]) {
-    constexpr int K = RT_SINGLE_CHUNK;
+    constexpr int K = 1;    // records per tile and step of the joint list walk
     v3 o[S], d[S];
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {                            // wgsl:311, 305-325
@@ -1864,13 +1508,13 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
     }
     SST_V(3, d[S - 1].x);
     const uint32_t lane = threadIdx.x & 63u;
-    if (kSingleLdsHit<S>) {
+    if (kSingleLds<S>) {
         // (this wave's own LDS slots: written and read by this wave only, in order)
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s) lblk[s * kCandStride + lane] = bv[s];
     }
     v3 cf[S], dsky[S];
-    float ddsky[S];                   // |dsky|^2 (RT_SINGLE_SKYDD)
+    float ddsky[S];                   // |dsky|^2 (sky_w's dd)
     bool black[S], any_other[S];      // (any_other: wave-uniform, a metal / dielectric hit)
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
@@ -1884,30 +1528,26 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
         // sphere_list_hit over each tile's list, the tiles' chunks interleaved
         float tmax[S], a[S], ya[S];
         int idx[S];
-        // (RT_SINGLE_SPREF: the current best entry's sphere record, taken from the scalar
-        // loads issued beside its scan record)
-        float4 bpr[S], bmat[S];
-        bool pref = false;
         bool joint = true;
         uint32_t m = 0;
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s) {
             tmax[s] = 0x1.05ed2ep+118f;                           // 3.4e35 (wgsl:266)
             idx[s] = -1;
-            bpr[s] = bmat[s] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             a[s] = ddsky[s];
             ya[s] = rcp_refined(a[s]);
             joint = joint && ncand[s] != kCandNone;
             m = max(m, ncand[s]);
         }
-        if (RT_SINGLE_SCAN == 0 && joint) {
-            constexpr bool kPref = RT_SINGLE_SPREF && !kSingleLdsHit<S>;
-            pref = kPref;
+        if (joint) {
             for (uint32_t i = 0; i < m; i += K) {
                 float hh[S][K], dd[S][K];
-                float4 spr[S][K], smat[S][K];
-                int mx = (int)0x80000000;
-                uint32_t an = 0xFFFFFFFFu;   // (RT_SINGLE_AND: the AND of the bit patterns)
+                // "some discriminant of the step is not negative" as the sign of the AND of
+                // their bit patterns (one 2-cycle v_and per record): exact on the camera-ray
+                // domain the host proves for these instances — every discriminant is finite
+                // (consider_fast) and never -0 (max_bits), so its sign bit is set exactly when
+                // it is < 0
+                uint32_t an = 0xFFFFFFFFu;
 #pragma unroll
                 for (uint32_t s = 0; s < S; ++s)
 #pragma unroll
@@ -1915,37 +1555,24 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                         const float4 g =
                             kSingleLds<S> ? lblk[s * kCandStride + kCandRecOff + i + k]
                                           : load_rec<true>(blk[s] + kCandRecOff, i + k);
-                        if (kPref) {   // (entry i + k's sphere record: wave-uniform, scalar)
-                            spr[s][k] = load_rec<true>(blk[s] + kCandSphOff, 2u * (i + k));
-                            smat[s][k] = load_rec<true>(blk[s] + kCandSphOff, 2u * (i + k) + 1u);
-                        }
                         dd[s][k] = discriminant(g, o[s], d[s], a[s], hh[s][k]);
-                        if (RT_SINGLE_AND)
-                            an &= __float_as_uint(dd[s][k]);
-                        else
-                            mx = max(mx, __float_as_int(dd[s][k]));
+                        an &= __float_as_uint(dd[s][k]);
                     }
-                if (__builtin_expect(RT_SINGLE_AND ? (int)an >= 0 : mx > (int)0xFF800000, 0)) {
+                if (__builtin_expect((int)an >= 0, 0)) {
 #pragma unroll
                     for (uint32_t s = 0; s < S; ++s)
 #pragma unroll
                         for (int k = 0; k < K; ++k)
-                            if (i + k < ncand[s]) {
-                                const int before = idx[s];
+                            if (i + k < ncand[s])
                                 consider_fast(dd[s][k], hh[s][k], a[s], ya[s], i + k, tmax[s],
                                               idx[s]);
-                                if (kPref && idx[s] != before) {
-                                    bpr[s] = spr[s][k];
-                                    bmat[s] = smat[s][k];
-                                }
-                            }
                 }
             }
         } else {
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
                 const bool listed = ncand[s] != kCandNone;
-                const Hit h = scan_exhaustive<(RT_SINGLE_SCAN == 0 ? K : RT_SINGLE_SCAN), true, true>(
+                const Hit h = scan_exhaustive<K, true, true>(
                     listed ? blk[s] + kCandRecOff : p.geom, listed ? ncand[s] : p.count, o[s],
                     d[s]);
                 idx[s] = h.idx;
@@ -1964,22 +1591,19 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
         uint64_t hm[S], any_m = 0;
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s) {
-            hm[s] = RT_SINGLE_MASKS ? (mask_sge(idx[s], 0) & live_m[s]) : 0ull;
+            hm[s] = mask_sge(idx[s], 0) & live_m[s];
             any_m |= hm[s];
         }
         if (RT_SKO & 8) {
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s)
                 if (hit[s]) cf[s] = mk(tmax[s], 0.5f, 0.5f);
-        } else if ((RT_SINGLE_MASKS ? any_m : rt_ballot(any)) != 0ull) {
+        } else if (any_m != 0ull) {
             float4 pr[S], mat[S];
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
                 const uint32_t j = hit[s] ? (uint32_t)idx[s] : 0u;
-                if (pref) {   // (the joint walk kept them: no load after the scan)
-                    pr[s] = bpr[s];
-                    mat[s] = bmat[s];
-                } else if (kSingleLdsHit<S> && ncand[s] != kCandNone) {
+                if (kSingleLds<S> && ncand[s] != kCandNone) {
                     pr[s] = lblk[s * kCandStride + kCandSphOff + 2u * j];
                     mat[s] = lblk[s * kCandStride + kCandSphOff + 2u * j + 1u];
                 } else {
@@ -1990,8 +1614,6 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
             }
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
-                if (RT_SINGLE_GATE && (RT_SINGLE_MASKS ? hm[s] : rt_ballot(hit[s])) == 0ull)
-                    continue;                                     // (sky tiles)
                 float r_sb;
                 v3 ruv;
                 if (kUniRs) {
@@ -2008,7 +1630,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                 shade_hit(pr[s], mat[s], tmax[s], o[s], d[s], r_sb, ruv, hit[s], hm[s], nd,
                           att, blk_s, other_s, ndd);
                 any_other[s] = other_s;
-                if (RT_SINGLE_UNIF && RT_SINGLE_MASKS && hm[s] == live_m[s]) {
+                if (hm[s] == live_m[s]) {
                     // every live lane hit (a tile inside a sphere's image): no selects
                     asm volatile("");
                     cf[s] = att;
@@ -2026,10 +1648,9 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
     }
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
-        const v3 c = RT_SINGLE_SKYDD ? sky_w(cf[s], dsky[s], ddsky[s])  // wgsl:293-296
-                                     : sky_w(cf[s], dsky[s]);
+        const v3 c = sky_w(cf[s], dsky[s], ddsky[s]);             // wgsl:293-296
         // (black: only metal hits absorb, so only a wave that shaded one selects)
-        if (RT_SINGLE_UNIF && !any_other[s]) {
+        if (!any_other[s]) {
             asm volatile("");
             col[s] = c;
         } else {
@@ -2049,7 +1670,7 @@ __device__ __forceinline__ void single_body(
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const uint32_t* __restrict__ a_order, const SingleParams& p) {
     static_assert(kPix >= 1 && kPix <= 4, "1 to 4 tiles per wave");
-    static_assert(!kChain || (RT_SINGLE_WT && !(RT_SKO & 16)),
+    static_assert(!kChain || !(RT_SKO & 16),
                   "frame chains hand the image over through write-through stores");
     constexpr uint32_t S = kPix;
     WAVE_TRACE(0);
@@ -2076,10 +1697,6 @@ __device__ __forceinline__ void single_body(
         const uint32_t e = __builtin_amdgcn_readfirstlane(a_order[pos]);
         gx = e & 0xFFFFu;
         lband = e >> 16;
-#if RT_SINGLE_PRIO
-        // (the costliest workgroups of the order: raised wave priority, see RT_SINGLE_PRIO)
-        if (pos < RT_SINGLE_PRIO) __builtin_amdgcn_s_setprio(2);
-#endif
     }
     SST_S(1, lband);
     const uint32_t tx0 = (gx * kSingleWg + wave) * S;
@@ -2117,17 +1734,15 @@ __device__ __forceinline__ void single_body(
                   : a_hx[min(tc[s].x, a_width - 1u)];
         hxy[s] = hx ^ hy;                                         // wgsl:309-310
     }
-    uint64_t valid_m[S];        // (RT_SINGLE_MASKS: tc[s].valid as a lane mask)
+    uint64_t valid_m[S];        // (tc[s].valid as a lane mask)
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s)
-        valid_m[s] = RT_SINGLE_MASKS
-                         ? (mask_ult(tc[s].x, a_width) & mask_ult(tc[s].y, a_height))
-                         : 0ull;
+        valid_m[s] = mask_ult(tc[s].x, a_width) & mask_ult(tc[s].y, a_height);
     // (issued after the seed-table loads: vmcnt waits in issue order, and the camera rays
     // need the seeds long before the scan and the accumulation need these)
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s)
-        bv[s] = (kSingleLdsHit<S> && tx0 + s < tiles_x) ? blk[s][lane]
+        bv[s] = (kSingleLds<S> && tx0 + s < tiles_x) ? blk[s][lane]
                                                       : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     // Frame chains (rt_chain.cpp): consecutive frames of a part are AQL packets with no
     // cache acquire between them, so the accumulator the previous frame stored (write-
@@ -2150,18 +1765,6 @@ __device__ __forceinline__ void single_body(
                      : kReset     ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)   // (discarded: no load)
                                   : a_in[tc[s].valid ? tc[s].idx : 0];            // wgsl:339
     }
-    if (kSingleDisk == 1 && p.defocus_angle > 0.0f) {             // (disk_unit's table)
-        if (threadIdx.x < 8u) {
-            double v = 0.0;
-#pragma unroll
-            for (uint32_t k = 0; k < 8u; ++k)
-#if RT_SINGLE_DISK == 1
-                if (threadIdx.x == k) v = p.disk_rcp[k];
-#endif
-            s_disk_rcp[threadIdx.x] = v;
-        }
-        __syncthreads();
-    }
     if (tx0 >= tiles_x) return;
     SST_V(2, hxy[S - 1]);
     SST_S(2, ncand[S - 1]);
@@ -2174,21 +1777,13 @@ __device__ __forceinline__ void single_body(
     cam.ddu = mk(p.ddu[0], p.ddu[1], p.ddu[2]);
     cam.ddv = mk(p.ddv[0], p.ddv[1], p.ddv[2]);
     cam.defocus_angle = p.defocus_angle;
-#if RT_SINGLE_VCONST
-    // wave-invariant operands that would otherwise be re-materialised per use (gfx950 VALU
-    // instructions take one SGPR or literal): the sincos coefficients the v_fmaak forms
-    // need in a register, and the lens centre of fma(u, ddu, centre) — one v_mov each per
-    // wave instead of per pixel
-    asm volatile("" : "+v"(cam.k1s), "+v"(cam.k1c));
-    asm volatile("" : "+v"(cam.center.x), "+v"(cam.center.y), "+v"(cam.center.z));
-#endif
     const uint32_t spp = p.spp;                                   // wgsl:343
 
     v3 c[S];
     uint32_t n[S];
     bool pending[S];
     bool any_pending = true;
-    uint64_t pend_m = 0;        // (RT_SINGLE_MASKS: the lanes with pending pixels)
+    uint64_t pend_m = 0;        // (the lanes with pending pixels)
     if (p.hinted) {
         // Every pixel is expected to hold n_hint (the host's count bookkeeping): trace with
         // it while the accumulator loads are in flight, then verify.
@@ -2209,26 +1804,14 @@ __device__ __forceinline__ void single_body(
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s) {
             c[s] = kReset ? mk(0.0f, 0.0f, 0.0f) : mk(acc[s].x, acc[s].y, acc[s].z);
-#if RT_SINGLE_NCHK
-            // f2u(acc.w) == ng (wgsl:341) holds for acc.w == f32(ng) (exact below 2^24); any
-            // other stored count — also one that truncates to ng — is traced again below
-            // with f2u(acc.w), which gives the same bits: one compare instead of the
-            // conversion with its saturation selects
-            n[s] = ng;
-            pending[s] = tc[s].valid && !kReset &&
-                         (p.n_exact ? __float_as_uint(acc[s].w) != p.ng_bits
-                                    : f2u(acc[s].w) != ng);
-#else
             n[s] = kReset ? 0u : f2u(acc[s].w);                   // wgsl:339-350
             pending[s] = tc[s].valid && n[s] != ng;               // a foreign count
-            if (RT_SINGLE_MASKS && !kReset) pend_m |= mask_ne(n[s], ng) & valid_m[s];
-#endif
+            if (!kReset) pend_m |= mask_ne(n[s], ng) & valid_m[s];
             any_pending = any_pending || pending[s];
             if (ng < spp) {                                       // wgsl:352-357
                 const v3 num = sub(col[s], c[s]);
-                if (RT_SINGLE_ACC_F64 && ng < (1u << 24) &&
-                    (RT_SINGLE_MASKS ? (mask_ult(acc_min_bits(num), kBits2m102 - 1u) & valid_m[s])
-                                     : rt_ballot(tc[s].valid && !acc_f64_ok(num))) == 0ull) {
+                if (ng < (1u << 24) &&
+                    (mask_ult(acc_min_bits(num), kBits2m102 - 1u) & valid_m[s]) == 0ull) {
                     c[s] = acc_f64(c[s], num, p.rcp_hint);
                 } else {
                     const float k = (float)(ng + 1u);             // wgsl:356
@@ -2244,8 +1827,7 @@ __device__ __forceinline__ void single_body(
             pend_m |= valid_m[s];
         }
     }
-    const bool wave_pending =
-        ((RT_SINGLE_MASKS && !RT_SINGLE_NCHK) ? pend_m : rt_ballot(any_pending)) != 0ull;
+    const bool wave_pending = pend_m != 0ull;
     if (wave_pending) {
         // pixels whose count is not the hinted one (or no hint): traced with their own
         // count and per-pixel random numbers
@@ -2263,7 +1845,7 @@ __device__ __forceinline__ void single_body(
         }
         uint64_t live_m[S];
 #pragma unroll
-        for (uint32_t s = 0; s < S; ++s) live_m[s] = RT_SINGLE_MASKS ? rt_ballot(live[s]) : 0ull;
+        for (uint32_t s = 0; s < S; ++s) live_m[s] = rt_ballot(live[s]);
         single_sample<S, false>(p, cam, tc, hxy, seed, blk, ncand, live, live_m, bv, lblk, col);
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s)
@@ -2282,7 +1864,7 @@ __device__ __forceinline__ void single_body(
     for (uint32_t s = 0; s < S; ++s)
         if (__float_as_uint(c[s].x + c[s].y + c[s].z) == p.hy_off + 0x7F7FFFFFu + n[s])
             p.out[tc[s].idx] = make_float4(c[s].x, c[s].y, c[s].z, (float)n[s]);
-#elif RT_SINGLE_WT
+#else
     // write-through (sc1) stores: the lines leave the XCD's L2 as they are written, so the
     // launch ends with no dirty image lines to write back at the kernel boundary
     float4* band = p.out + (size_t)lband * RT_STRIPE_ROWS * a_width;
@@ -2290,27 +1872,17 @@ __device__ __forceinline__ void single_body(
         band, 0, (int)(RT_STRIPE_ROWS * 16u * a_width), 0x00020000);
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s)
-        if (RT_SINGLE_MASKS || tc[s].valid) {                     // wgsl:362-363
+    {                                                             // wgsl:362-363
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            // (every pixel of a wave without a foreign count holds the hinted count after
-            // the frame: f32 of it from the host)
-            const uint32_t nb = (RT_SINGLE_NCHK && p.hinted && !wave_pending)
-                                    ? p.n_after_bits
-                                    : __float_as_uint((float)n[s]);
             const u32x4 v = {__float_as_uint(c[s].x), __float_as_uint(c[s].y),
-                             __float_as_uint(c[s].z), nb};
-            // RT_SINGLE_MASKS: no branch — a pixel past the image edge stores to an offset
-            // past the band's buffer record, which the buffer unit drops
+                             __float_as_uint(c[s].z), __float_as_uint((float)n[s])};
+            // no branch: a pixel past the image edge stores to an offset past the band's
+            // buffer record, which the buffer unit drops
             const uint32_t off = ((lane >> 3) * a_width + tc[s].x) * 16u;
-            const bool drop = (RT_SINGLE_MASKS && !tc[s].valid) || (kChain && aborted != 0u);
+            const bool drop = !tc[s].valid || (kChain && aborted != 0u);
             __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, (int)(drop ? 0x7FFFFFF0u : off), 0,
                                                    16);
         }
-#else
-#pragma unroll
-    for (uint32_t s = 0; s < S; ++s)
-        if (tc[s].valid)                                          // wgsl:362-363
-            p.out[tc[s].idx] = make_float4(c[s].x, c[s].y, c[s].z, (float)n[s]);
 #endif
 #if RT_SSTAMPS
     sst_put(7, __builtin_amdgcn_s_memtime());
@@ -2477,8 +2049,7 @@ __device__ __forceinline__ uint32_t compact_slot(bool live, uint32_t wave, uint3
                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Register plan of the bounce instance.  RT_BOUNCE_RELOAD: the camera (per frame) and the
-// grid parameters (per bounce scan) are re-read from the kernarg segment through a pointer
+// Register plan of the bounce instance.  The camera (per frame) and the grid parameters (per bounce scan) are re-read from the kernarg segment through a pointer
 // the compiler cannot see through (scalar-cache hits), instead of staying live in SGPRs for
 // the whole launch; with it a 7-wave plan fits 94 SGPRs (106 and 6 waves before).  K5 per
 // 64-spp step (profiles/r03f_ab_k5.log, two rounds): 31.3 ms as before, 29.7 reloading at 6
@@ -2494,9 +2065,6 @@ __device__ __forceinline__ uint32_t compact_slot(bool live, uint32_t wave, uint3
 // whole image unchanged (445 µs per spp).
 #ifndef RT_BOUNCE_PRIO
 #define RT_BOUNCE_PRIO 512
-#endif
-#ifndef RT_BOUNCE_RELOAD
-#define RT_BOUNCE_RELOAD 1
 #endif
 __device__ __forceinline__ const kconst TraceParams* karg_bounce_params() {
     // rt_bounce_kernel's only argument: the TraceParams block at kernarg offset 0
@@ -2594,9 +2162,6 @@ rt_bounce_kernel(const TraceParams p) {
     const uint32_t ncand = (p.cand_k && wave_in) ? load_cnt(p.cand, tile) : kCandNone;
     const float4* blk = p.cand + (size_t)tile * kCandStride;
     const uint32_t hxy = p.hx[min(tc.x, p.width - 1u)] ^ p.hy[min(tc.y, p.height - 1u)];
-#if !RT_BOUNCE_RELOAD
-    const Cam cam = cam_params(p);
-#endif
     const uint32_t spp = p.spp, depth = p.depth;        // wgsl:343, 264
     // the pixel's accumulator (wgsl:339-341; a frame-0 reset discards it)
     v3 c = mk(0.0f, 0.0f, 0.0f);
@@ -2646,9 +2211,7 @@ rt_bounce_kernel(const TraceParams p) {
         if (kCompact) s_bounce.res[me] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         // bounce 0: this wave's own camera rays (wgsl:305-325), its tile's scan
         v3 o, d, cf = mk(1.0f, 1.0f, 1.0f);
-#if RT_BOUNCE_RELOAD
         const Cam cam = cam_params(*karg_bounce_params());
-#endif
         get_ray<false>(cam, tc.x, tc.y, hxy, seed * 25u + B, o, d);
         uint32_t pseed = seed + 1u;                               // ray_color's seed
         bool live = sampling;
@@ -2663,11 +2226,7 @@ rt_bounce_kernel(const TraceParams p) {
             const float4* hs = p.sph;
             if (rt_ballot(live) != 0ull) {
                 const bool listed = i == 0u && ncand != kCandNone;
-#if RT_BOUNCE_RELOAD
                 const GridP gp = grid_params(*karg_bounce_params());
-#else
-                const GridP gp = grid_params(p);
-#endif
                 hit = listed ? scan_exhaustive<RT_SCAN_CHUNK, false, true>(blk + kCandRecOff,
                                                                           ncand, o, d)
                       : p.lds_records ? scan_culled<true>(gp, p.geom, p.count, o, d, live, i > 0)
@@ -2867,9 +2426,6 @@ rt_bounce_kernel(const TraceParams p) {
 // contend inside a wave), one block-wide scan over the [bucket][wave] counts turns them
 // into offsets, costliest bucket first, and each tile is placed at its wave's next slot of
 // its bucket (order inside a bucket is arbitrary: tiles are independent).
-// snake > 0: the sorted list is dealt in runs of `snake`, every second run reversed (the
-// costliest of run 2 pairs with the cheapest of run 1 on the dispatcher's round-robin over
-// CUs), for launches of a few workgroups per CU.
 // parts > 1: the sorted list is dealt round-robin into `parts` contiguous sub-lists (entry
 // pos to part pos % parts), one per concurrent part of a one-frame update (launch_single):
 // every part gets the same mix of costly and cheap workgroups, costliest first.
@@ -2878,17 +2434,10 @@ __device__ __forceinline__ uint32_t part_pos(uint32_t pos, uint32_t n, uint32_t 
     const uint32_t k = pos % parts, j = pos / parts;
     return k * (n / parts) + min(k, n % parts) + j;
 }
-__device__ __forceinline__ uint32_t snake_pos(uint32_t pos, uint32_t n, uint32_t g) {
-    if (g == 0u) return pos;
-    const uint32_t c = pos / g, j = pos - c * g;
-    if ((c & 1u) == 0u) return pos;
-    const uint32_t len = min(g, n - c * g);
-    return c * g + (len - 1u - j);
-}
 __global__ __launch_bounds__(1024) void rt_tile_order_kernel(const uint32_t* __restrict__ cost,
                                                              uint32_t* __restrict__ order,
                                                              uint32_t tiles, uint32_t tiles_x,
-                                                             uint32_t snake, uint32_t parts) {
+                                                             uint32_t parts) {
     constexpr uint32_t kBuckets = 128, kWaves = 16, kSlots = kBuckets * kWaves;
     __shared__ uint32_t hist[kSlots];          // [bucket][wave]
     __shared__ uint32_t scan[1024];
@@ -2945,7 +2494,7 @@ __global__ __launch_bounds__(1024) void rt_tile_order_kernel(const uint32_t* __r
             const uint32_t t = t0 + k * 1024u;
             if (t < tiles) {
                 const uint32_t pos = atomicAdd(&hist[bucket(c[k]) * kWaves + wave], 1u);
-                order[part_pos(snake_pos(pos, tiles, snake), tiles, parts)] =
+                order[part_pos(pos, tiles, parts)] =
                     ((t / tiles_x) << 16) | (t % tiles_x);
             }
         }
@@ -2953,11 +2502,10 @@ __global__ __launch_bounds__(1024) void rt_tile_order_kernel(const uint32_t* __r
 }
 
 hipError_t launch_tile_order(const uint32_t* tile_cost, uint32_t* tile_order, uint32_t tiles,
-                             uint32_t tiles_x, hipStream_t stream, uint32_t snake,
-                             uint32_t parts) {
+                             uint32_t tiles_x, hipStream_t stream, uint32_t parts) {
     if (tiles == 0) return hipSuccess;
     hipLaunchKernelGGL(rt_tile_order_kernel, dim3(1), dim3(1024), 0, stream, tile_cost,
-                       tile_order, tiles, tiles_x, snake, parts);
+                       tile_order, tiles, tiles_x, parts);
     return hipGetLastError();
 }
 
@@ -3043,10 +2591,6 @@ hipError_t launch_unit_order(const uint32_t* tile_cost, uint32_t* unit_order,
     return hipGetLastError();
 }
 
-// wg_order dealt in snake runs of this many workgroups (0 = straight costliest first)
-#ifndef RT_WG_SNAKE
-#define RT_WG_SNAKE 0
-#endif
 // Per-workgroup candidate-list load of one-frame launches (wg_order's sort key): the sum of
 // its `per` tiles' loads (4 + count for a tile with a list, 64 for a tile without one).
 __global__ __launch_bounds__(256) void rt_wg_cost_kernel(const float4* __restrict__ cand,
@@ -3512,18 +3056,7 @@ static bool single_args(const TraceParams& p, SingleArgs& args, dim3& grid) {
     q.seed_b = p.seed_b[0];
     q.hy_off = (uint32_t)(p.hy - p.hx);
     q.rcp_hint = p.hint_rcp[0];
-    {
-        const uint32_t ng = q.n_hint;
-        const uint32_t after = ng < q.spp ? ng + 1u : ng;           // wgsl:352-357
-        const float fng = (float)ng, faft = (float)after;
-        std::memcpy(&q.ng_bits, &fng, 4);
-        std::memcpy(&q.n_after_bits, &faft, 4);
-        q.n_exact = ng < (1u << 24) ? 1u : 0u;
-    }
     q.rs = p.hint_rs[0];
-#if RT_SINGLE_DISK == 1
-    for (int k = 0; k < 8; ++k) q.disk_rcp[k] = p.disk_rcp[k];
-#endif
     for (int i = 0; i < 3; ++i) {
         q.center[i] = p.center[i];
         q.vul[i] = p.vul[i];
@@ -3648,8 +3181,6 @@ hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
     if (kernel == kTraceBounce) return launch_bounce(p, stream);
     if (kernel == kTraceListQuad)
         return launch_trace_as<kTraceListQuad>(p, group_lds_bytes<kTraceListQuad>(), stream);
-    if (kernel == kTraceListOct)
-        return launch_trace_as<kTraceListOct>(p, group_lds_bytes<kTraceListOct>(), stream);
     return launch_trace_as<kTraceExhaustive>(p, 0, stream);
 }
 
@@ -3676,7 +3207,7 @@ hipError_t launch_wg_order(const float4* cand, uint32_t tiles_x, uint32_t bands,
                        tiles_x, cols, per, units, wg_cost);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_tile_order(wg_cost, wg_order, units, cols, stream, RT_WG_SNAKE, parts);
+    return launch_tile_order(wg_cost, wg_order, units, cols, stream, parts);
 }
 
 hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream) {
@@ -3723,22 +3254,6 @@ const char* single_kernel_name(uint32_t pix) {
 
 }  // namespace rtk
 
-#if RT_STAMPS
-// Diagnostic builds: summed cycles per phase (1 get_ray, 2 cone, 3 cull loop, 4 rest of
-// ray_color, 5 accumulate + store) over all waves since the last call; resets them.
-extern "C" __attribute__((visibility("default"))) int rt_diag_stamps(unsigned long long* out,
-                                                                     unsigned waves) {
-    // out[1..5]: summed phase cycles (get_ray, cone, cull loop, rest of ray_color,
-    // accumulate + store); out[6]: entry -> first ray; out[7]: wave lifetime.
-    static unsigned long long host[rtk::kStampWaves][8];
-    if (waves > (unsigned)rtk::kStampWaves) waves = rtk::kStampWaves;
-    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(rtk::g_stamp), sizeof(host)) != hipSuccess) return 1;
-    for (int i = 0; i < 8; ++i) out[i] = 0;
-    for (unsigned wv = 0; wv < waves; ++wv)
-        for (int i = 1; i < 8; ++i) out[i] += host[wv][i];
-    return 0;
-}
-#endif
 
 #if RT_SSTAMPS
 // Diagnostic builds: copies the one-frame kernel's per-wave stamps (12 words each, see

@@ -184,8 +184,6 @@ RT_API const char* rt_last_error(void);
 /* bounce rays, each tile's frames split into chunks traced by separate waves, the last
  * finisher accumulating them in order (RT_PATHS_SPLIT) */
 #define RT_KERNEL_BOUNCE_SPLIT 10
-/* the camera-ray-only instance with eight waves per tile (RT_FRAME_PAIRS_OCT) */
-#define RT_KERNEL_LIST_OCT 11
 /* The instance's name as rocprofv3 lists it ("rt_trace_kernel<k>", "rt_bounce_kernel<m>",
  * "rt_single_kernel<p>"), "rt_trace_kernel" for an unknown id. */
 RT_API const char* rt_kernel_name(int which);
@@ -302,12 +300,11 @@ RT_API rt_status rt_set_frame_images(rt_ctx* ctx, int mode);
  * which accumulates every frame in order: the same bits), whenever every pixel
  * holds the sample count the context expects (otherwise the launch falls back to one wave
  * per tile).  AUTO (default): 2 waves per tile, 4 for launches of at most 6144 tiles (small
- * per-rank shares); ON: 2; QUAD: 4; OCT: 8; OFF: one wave per tile. */
+ * per-rank shares); ON: 2; QUAD: 4; OFF: one wave per tile. */
 #define RT_FRAME_PAIRS_AUTO 0
 #define RT_FRAME_PAIRS_OFF 1
 #define RT_FRAME_PAIRS_ON 2
 #define RT_FRAME_PAIRS_QUAD 3
-#define RT_FRAME_PAIRS_OCT 4
 RT_API rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode);
 /* Tile scheduling (culled scan mode).  AUTO (default): fused multi-frame launches (the
  * camera-ray-only kernels and the bounce instance): the first such launch for a camera

@@ -128,7 +128,7 @@ def test_golden_k4_fused_64spp(rt, pipe):
     assert hashlib.sha256(img.tobytes()).hexdigest() == str(g["sha256"])
 
 
-@pytest.mark.parametrize("pairs", ["auto", "quad", "oct"])
+@pytest.mark.parametrize("pairs", ["auto", "quad"])
 def test_bench_k4_launches_match_golden(rt, pairs):
     """The kernel bench.py --config K4 times, at the timed size: rt_update_frames of 64
     frames from a reset at 1920x1080 / 500 spheres (AUTO: frame pairs, kTraceListPair; the
@@ -146,8 +146,7 @@ def test_bench_k4_launches_match_golden(rt, pairs):
             info = p.last_launch_info()
             assert info["launches"] == 1 and info["max_frames_per_launch"] == 64
             assert info["kernel_name"] == {"auto": "rt_trace_kernel<3>",
-                                           "quad": "rt_trace_kernel<4>",
-                                           "oct": "rt_trace_kernel<11>"}[pairs]
+                                           "quad": "rt_trace_kernel<4>"}[pairs]
             img = host(b if newest == 1 else a)
             assert hashlib.sha256(img.tobytes()).hexdigest() == str(g["sha256"]), launch
             other = host(a if newest == 1 else b)
@@ -769,7 +768,7 @@ def test_candidate_list_overflow_falls_back(rt, depth):
                                                   (7, 1, 4, 0), (4, 1, 500, 1), (6, 3, 500, 4),
                                                   (5, 8, 500, 4), (9, 2, 3, 3), (14, 1, 500, 4),
                                                   (11, 1, 6, 3)])
-@pytest.mark.parametrize("pairs", ["off", "on", "quad", "oct"])
+@pytest.mark.parametrize("pairs", ["off", "on", "quad"])
 @pytest.mark.parametrize("images", ["last_two", "every"])
 def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, spp, per, pairs,
                                               images):
@@ -1024,7 +1023,7 @@ def test_hinted_chain_matches_oracle(rt, oracle, pipe, depth, spp):
         assert_same(host(cur), ref)
 
 
-@pytest.mark.parametrize("pairs", ["off", "on", "quad", "oct"])
+@pytest.mark.parametrize("pairs", ["off", "on", "quad"])
 def test_update_frames_with_foreign_counts(rt, oracle, pipe, pairs):
     """rt_update_frames on an image whose counts the library did not write (mixed per-pixel
     counts behind its back, after init_image): the hinted / frame-pair launch falls back to
