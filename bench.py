@@ -618,9 +618,9 @@ def main():
     # Warm-up (untimed, scratch images): a progressive render's steps run back to back in a
     # process that has long been issuing them; a 20-step timed region (~0.4 ms) right after
     # process start would otherwise time the chip's start from idle (K3: 22.2 against 16.2 µs
-    # per update, profiles/r03w_driver_warm.log; not the waves' clock, 1.83 GHz cold and 1.88
-    # warm, profiles/r03zb_stamps_single_k3_*.jsonl, nor the host's issue rate,
-    # profiles/r03zc_driver_cold_warm_hip_aql.log).  The same frames on
+    # per update, profiles/r03/r03w_driver_warm.log; not the waves' clock, 1.83 GHz cold and 1.88
+    # warm, profiles/r03/r03zb_stamps_single_k3_*.jsonl, nor the host's issue rate,
+    # profiles/r03/r03zc_driver_cold_warm_hip_aql.log).  The same frames on
     # separate images: the timed images, their counts and the fixture check are untouched.
     warm_s = 0.0
     if args.warm_ms > 0:

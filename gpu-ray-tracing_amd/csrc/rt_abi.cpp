@@ -992,13 +992,13 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
 }
 
 // Concurrent parts of a one-frame update (rt_set_update_queues).  AUTO by the launch's
-// tiles (profiles/r03e_ab_queues.log, r03e_rank_sim_k3_q*.jsonl; µs per K3 update at 1 / 2
+// tiles (profiles/r03/r03e_ab_queues.log, r03/r03e_rank_sim_k3_q*.jsonl; µs per K3 update at 1 / 2
 // / 3 / 4 parts: whole image 22.7 / 19.6 / 19.6 / 19.0, K2 15.9 / 13.6 / 13.5 / 13.5; a
 // 2-rank share 12.5 / 11.4 / 11.5; 4-rank 7.8 / 7.5 / 9.7; 8-rank 5.9 / 7.9 / 10.9): each
 // part costs the host one more launch (2.7-4.4 µs each on the boxes measured,
-// profiles/r03g_launch_rate.jsonl, r03h_launch_rate.jsonl), which small shares cannot hide,
+// profiles/r03/r03g_launch_rate.jsonl, r03/r03h_launch_rate.jsonl), which small shares cannot hide,
 // and a slow host turns 4 parts into a host-bound chain (the driver's 20-step command:
-// 72-77 G rays/s at 4 parts, 87-90 at 2, 81-85 at 1, profiles/r03h_bench_driver_q*.json).
+// 72-77 G rays/s at 4 parts, 87-90 at 2, 81-85 at 1, profiles/r03/r03h_bench_driver_q*.json).
 constexpr uint64_t kQueues4MinTiles = ~0ull, kQueues2MinTiles = 12000;
 uint32_t update_parts(const rt_ctx* ctx, const rtk::TraceParams& p, int kernel) {
     if ((kernel != rtk::kTraceSingle && kernel != rtk::kTraceSingleOne) || p.frames != 1u)
@@ -1012,9 +1012,9 @@ uint32_t update_parts(const rt_ctx* ctx, const rtk::TraceParams& p, int kernel) 
 }
 
 // Parts of a one-frame update submitted as AQL packets: a packet costs the host ≈0.25 µs
-// (profiles/r03r_aql_probe.txt), so the host never bounds the parts; but four HSA queues
+// (profiles/r03/r03r_aql_probe.txt), so the host never bounds the parts; but four HSA queues
 // beside HIP's own measured 38.7 µs per K3 update against 20.4 with two
-// (profiles/r03s_ab_aql_nckarg.log): AUTO takes 2 from 2 000 tiles, else 1
+// (profiles/r03/r03s_ab_aql_nckarg.log): AUTO takes 2 from 2 000 tiles, else 1
 // (rt_set_update_queues overrides).
 constexpr uint64_t kAqlQueues4MinTiles = ~0ull, kAqlQueues2MinTiles = 2000;
 uint32_t update_parts_aql(const rt_ctx* ctx, const rtk::TraceParams& p) {
@@ -1094,7 +1094,7 @@ rt_status chain_report(rt_ctx* ctx) {
 // the machine does not offer it, AUTO falls back to HIP launches, and after a chain failure
 // every mode runs HIP launches.  Round 3 measured AQL faster only on mid-sized rank shares
 // of per-dispatch updates (a 4-rank K3 share 6.76 against 7.54-7.68 µs per update,
-// profiles/r03zd_rank_sim_*.jsonl; whole images and 2-rank shares alike either way, 8-rank
+// profiles/r03/r03zd_rank_sim_*.jsonl; whole images and 2-rank shares alike either way, 8-rank
 // shares slower); rank shares now run fused frame chains in one launch instead
 // (rt_set_frame_images), and no multi-GPU record of AQL submission exists.
 #ifndef RT_AQL_AUTO_MIN_TILES

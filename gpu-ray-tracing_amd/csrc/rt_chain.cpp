@@ -7,7 +7,7 @@
 // how many concurrent parts a small rank share can use, and HIP's dispatches carry cache
 // fences at every kernel boundary.  Here every frame of every part is one
 // hsa_kernel_dispatch_packet_t on that part's queue (≈0.25 µs of host time each,
-// profiles/r03r_aql_probe.txt):
+// profiles/r03/r03r_aql_probe.txt):
 //   * a part's frames run in order on its queue (barrier bit set: frame f + 1 reads the
 //     pixels frame f wrote); parts run concurrently on their own queues, as the HIP path's
 //     streams do;
@@ -28,7 +28,7 @@
 // can be before the packet's barrier resolves), in pinned host memory allocated non-coherent
 // so that the waves' scalar loads of the parameter block are served by L2 after the first
 // miss (fine-grained host memory is read over PCIe by every wave: 115 µs per K3 update
-// against 19.5, profiles/r03r_ab.log).  Each queue's first packet of a segment acquires at
+// against 19.5, profiles/r03/r03r_ab.log).  Each queue's first packet of a segment acquires at
 // system scope, which drops any line of a reused argument slot cached before the host
 // rewrote it.  A set's slots are rewritten only after its previous segment has completed.
 #include <hip/hip_runtime_api.h>

@@ -15,7 +15,7 @@
 
 // sincos_c's quadrant swap as bit selects (1, default) or selects (0); identical bits
 // (with the closed-form disk reciprocal, K2 15.74 against 16.0 us per update,
-// profiles/r03a_ab_single.log)
+// profiles/r03/r03a_ab_single.log)
 #ifndef RT_SINCOS_BITS
 #define RT_SINCOS_BITS 1
 #endif

@@ -106,7 +106,7 @@ __device__ __forceinline__ unsigned long long rt_ballot(bool x) {
 // boolean that crosses blocks or combines earlier booleans compiles to a v_cndmask 0/1 +
 // v_cmp_ne round trip (two 4-cycle VALU operations) at every use; these do not (round 3:
 // K3 19.5-19.8 -> 18.9-19.1 µs, K2 13.6-13.8 -> 13.4 µs per update,
-// profiles/r03t_ab_single_masks_all.log).
+// profiles/r03/r03t_ab_single_masks_all.log).
 __device__ __forceinline__ uint64_t mask_ult(uint32_t a, uint32_t b) {
     return __builtin_amdgcn_uicmp(a, b, 36);          // ICMP_ULT
 }
@@ -1375,8 +1375,8 @@ constexpr uint32_t kSingleWg = RT_SINGLE_WG;
 // The defocus disk's reciprocal in the one-frame kernel is all-f32 (disk_unit<3>: the length
 // and its reciprocal from the bits of len2, one Markstein step; no f64, no LDS table, no
 // barrier).  The workgroup's LDS table made every wave wait for wave 0's kernarg read at
-// wave start (K3 23.30 -> 22.46 µs per update without it, profiles/r03a_ab_single.log); the
-// all-f32 form with the lane masks: profiles/r03t_ab_single_masks_all.log.
+// wave start (K3 23.30 -> 22.46 µs per update without it, profiles/r03/r03a_ab_single.log); the
+// all-f32 form with the lane masks: profiles/r03/r03t_ab_single_masks_all.log.
 constexpr int kSingleDisk = 3;
 // hash(x*73) ^ hash(y*51) (wgsl:309-310) of the one-frame kernel: from the per-column /
 // per-row tables (two dependent loads behind the order entry) or computed in the wave —
@@ -1384,8 +1384,8 @@ constexpr int kSingleDisk = 3;
 // the pixels with ds_bpermute — so the camera rays need no memory at all.  Bit k set =
 // computed in the kPix = k + 1 instance.  Default: the one-tile instance (rank shares)
 // computes them — 4-rank shares 0.1-0.3 µs faster per update, 8-rank unchanged
-// (profiles/r03zn_single_hash1.txt); the two-tile instance (whole images) reads the tables
-// (computing them there cost 0.9 µs at K3, profiles/r03e_ab_single_switches.log).
+// (profiles/r03/r03zn_single_hash1.txt); the two-tile instance (whole images) reads the tables
+// (computing them there cost 0.9 µs at K3, profiles/r03/r03e_ab_single_switches.log).
 #ifndef RT_SINGLE_HASH
 #define RT_SINGLE_HASH 1
 #endif
@@ -2052,14 +2052,14 @@ __device__ __forceinline__ uint32_t compact_slot(bool live, uint32_t wave, uint3
 // Register plan of the bounce instance.  The camera (per frame) and the grid parameters (per bounce scan) are re-read from the kernarg segment through a pointer
 // the compiler cannot see through (scalar-cache hits), instead of staying live in SGPRs for
 // the whole launch; with it a 7-wave plan fits 94 SGPRs (106 and 6 waves before).  K5 per
-// 64-spp step (profiles/r03f_ab_k5.log, two rounds): 31.3 ms as before, 29.7 reloading at 6
+// 64-spp step (profiles/r03/r03f_ab_k5.log, two rounds): 31.3 ms as before, 29.7 reloading at 6
 // waves, 28.8 reloading at 7 (the default), 30.2 at 8 (78 SGPRs, 53 spilled to VGPR lanes),
 // 30.5 at 7 without reloading (81 spilled).
 #ifndef RT_BOUNCE_MIN_WAVES
 #define RT_BOUNCE_MIN_WAVES 7
 #endif
 // RT_BOUNCE_PRIO: the first RT_BOUNCE_PRIO workgroups of the cost order run at raised wave
-// priority (s_setprio), 0 = off.  K5 per-rank prediction (profiles/r03m_rank_sim_k5_*: two
+// priority (s_setprio), 0 = off.  K5 per-rank prediction (profiles/r03/r03m_rank_sim_k5_*: two
 // rounds of five 64-frame launches each, the same frames for every build): 8-rank share
 // 74.7 µs per spp off, 72.6 with 512 (efficiency 0.745 -> 0.769), 73.5 with 2048; the
 // whole image unchanged (445 µs per spp).
@@ -3078,7 +3078,7 @@ static hipError_t launch_single(const TraceParams& p, hipStream_t stream) {
     // hipModuleLaunchKernel with the arguments packed in the kernel's layout and a cached
     // function handle: no per-launch symbol lookup or per-argument marshalling (320-byte
     // arguments: 4.2-4.4 against 5.0-6.0 µs of host time per launch through the
-    // hipLaunchKernelGGL path, profiles/r03j_launch_rate.jsonl) — the host's issue rate
+    // hipLaunchKernelGGL path, profiles/r03/r03j_launch_rate.jsonl) — the host's issue rate
     // bounds small rank shares and the concurrent parts
     size_t bytes = sizeof(args);
     void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes,

@@ -4,7 +4,7 @@ A wave64 VALU instruction holds a SIMD-32 for a number of cycles that depends on
 ~2.3-2.5 for f32 add / mul / fma and 32-bit logic, ~4.1-4.5 for integer multiplies, SDWA,
 compares, selects with an SGPR mask, conversions, f64 and the div_scale family, ~8.1 for
 transcendentals (measured with 8 waves per SIMD: tools/valu_rates.hip ->
-profiles/archive/r01_valu_rates.txt, profiles/r03_valu_rates.txt).  The PMC counts the dynamic VALU
+profiles/archive/r01_valu_rates.txt, profiles/r03/r03_valu_rates.txt).  The PMC counts the dynamic VALU
 instructions per class (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F32, _INT32, _INT64, _CVT,
 _{ADD,MUL,FMA,TRANS}_F64; the rest = SQ_INSTS_VALU minus their sum: moves, compares,
 selects, lane ops).  A class mixes forms of different cost (INT32: v_xor 2.5, v_mul_lo_u32
