@@ -167,6 +167,35 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
+_fast = False
+
+
+def fastcall():
+    """The CPython binding of rt_update_frames (build/_rt_fastcall*.so, csrc/host/rt_fastcall.c:
+    the same library entry point without ctypes' per-call conversion), or None when it has
+    not been built, an experiment build of the library is selected (RT_HIP_LIB: the binding
+    links the in-tree librt_hip.so) or RT_FASTCALL=0 asks for ctypes (diagnostic A/B)."""
+    global _fast
+    if os.environ.get("RT_FASTCALL") == "0":
+        return None
+    if _fast is False:
+        _fast = None
+        if "RT_HIP_LIB" not in os.environ:
+            import importlib.machinery
+            import importlib.util
+            import sysconfig
+            path = PKG_ROOT / "build" / ("_rt_fastcall" + sysconfig.get_config_var("EXT_SUFFIX"))
+            if path.exists():
+                lib()                      # (the library first: the same mapping)
+                loader = importlib.machinery.ExtensionFileLoader("_rt_fastcall", str(path))
+                spec = importlib.util.spec_from_file_location("_rt_fastcall", path,
+                                                              loader=loader)
+                mod = importlib.util.module_from_spec(spec)
+                loader.exec_module(mod)
+                _fast = mod
+    return _fast
+
+
 def exported_symbols() -> list[str]:
     return list(_SIGS)
 

@@ -266,6 +266,7 @@ def test_bound_update_frames_passes_the_same_arguments(rt, monkeypatch):
     cam = rt.SceneCamera.from_settings(rt.CameraSettings(), 64, 48, 0.25)
     seeds = np.array([0.25, 0.5, 0.75], np.float32)
     monkeypatch.setattr(cs._lib, "lib", lambda: FakeLib)
+    monkeypatch.setattr(cs._lib, "fastcall", lambda: None)   # (the ctypes path under test)
     monkeypatch.setattr(cs, "_check_image", lambda *a: None)
     pipe = object.__new__(cs.ComputeShaderPipeline)
     pipe._ctx = ctypes.c_void_p(0x1234)
@@ -317,6 +318,7 @@ def test_bound_run_keeps_converted_spheres_alive(rt, monkeypatch):
 
     cam = rt.SceneCamera.from_settings(rt.CameraSettings(), 16, 16, 0.25)
     monkeypatch.setattr(cs._lib, "lib", lambda: FakeLib)
+    monkeypatch.setattr(cs._lib, "fastcall", lambda: None)   # (the ctypes path under test)
     monkeypatch.setattr(cs, "_check_image", lambda *a: None)
     pipe = object.__new__(cs.ComputeShaderPipeline)
     pipe._ctx = ctypes.c_void_p(0x1234)
@@ -345,3 +347,24 @@ def test_bound_run_keeps_converted_spheres_alive(rt, monkeypatch):
     runs[0](cam, sc32, seeds)
     assert np.array_equal(seen[-1], sc32.spheres)
     pipe._ctx = ctypes.c_void_p()
+
+
+def test_fastcall_binding_checks_arguments_without_device(rt):
+    """The CPython binding of rt_update_frames (build/_rt_fastcall*.so) reaches the library's
+    own argument checks (a NULL context: -RT_ERR_INVALID_CONTEXT, no HIP call) and refuses
+    buffers that are not C-contiguous float32 (the bound call then converts them)."""
+    fast = rt._lib.fastcall()
+    assert fast is not None, "build/_rt_fastcall*.so was not built (make -C gpu-ray-tracing_amd)"
+    blob = np.zeros(44, np.float32)
+    sph = np.zeros((500, 8), np.float32)
+    seeds = np.zeros(20, np.float32)
+    assert fast.update_frames(0, 0x1000, 0x2000, 64, 48, 0, 1, blob, sph, 500, seeds, None) == -6
+    with pytest.raises(TypeError):
+        fast.update_frames(0, 0x1000, 0x2000, 64, 48, 0, 1, blob, sph.astype(np.float64), 500,
+                           seeds, None)
+    with pytest.raises((TypeError, ValueError, BufferError)):
+        fast.update_frames(0, 0x1000, 0x2000, 64, 48, 0, 1, blob, sph[:, :4], 500, seeds, None)
+    with pytest.raises(ValueError):        # fewer records than the count claims
+        fast.update_frames(0, 0x1000, 0x2000, 64, 48, 0, 1, blob, sph[:10], 500, seeds, None)
+    with pytest.raises(TypeError):         # the camera is the 176-byte blob
+        fast.update_frames(0, 0x1000, 0x2000, 64, 48, 0, 1, blob[:40], sph, 500, seeds, None)

@@ -6,8 +6,9 @@ and quartiles of the wall time per step (perf_counter around the call and the cl
 synchronize, as bench.py's value), of the HIP-event time per step, and of the host issue
 time of the call.
 
-Variants: name=ENV=V[,ENV=V...][;queues=Q], e.g.  fork0=RT_FORK=0  q3=;queues=3.  The
-library reads its diagnostic switches (RT_FORK, ...) from the environment on every call.
+Variants: name=ENV=V[,ENV=V...][;queues=Q], e.g.  fork0=RT_FORK=0  q3=;queues=3
+ctypes=RT_FASTCALL=0.  The library reads its diagnostic switches (RT_FORK, ...) from the
+environment on every call; each variant has its own renderer, bound under its environment.
 usage: python tools/driver_region.py [R] [CFG] variant...   (CFG K3 | K2)"""
 import json
 import os
@@ -53,7 +54,8 @@ pipe.set_spheres(sc)
 pipe.set_frames_per_launch(1)
 pipe.set_frame_images("last_two")
 stream = torch.cuda.current_stream()
-r = StripeRenderer(pipe, w, h, 0, 1)
+# one renderer per variant (its calls are bound under that variant's environment)
+rend = {v[0]: None for v in variants}
 scratch = StripeRenderer(pipe, w, h, 0, 1)
 torch.cuda.synchronize()
 t_w = time.perf_counter()
@@ -68,6 +70,9 @@ for rep in range(R + 1):
         os.environ.update(base_env)
         os.environ.update(kv)
         pipe.set_update_queues(queues)
+        if rend[name] is None:
+            rend[name] = StripeRenderer(pipe, w, h, 0, 1)
+        r = rend[name]
         r.frames(cam0, sc, seeds[:5])                  # the warmup steps (frame 0 resets)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 5, session b: the fixed cost of the driver's 20-step K3 command, A/B in one process
 # (tools/driver_region.py, variants interleaved repetition by repetition): the fork skipped on
-# an idle stream (default) against the recorded fork (RT_FORK=0), two against three parts;
+# an idle stream (default) against the recorded fork (RT_FORK=0), the CPython binding of the
+# call against ctypes (RT_FASTCALL=0), both off (round 4's path), two against three parts;
 # then the same with the runtime's host wait spinning (ROC_ACTIVE_WAIT_TIMEOUT, hipDeviceScheduleSpin).
 # Usage: bash tools/sessions/gpu_r05b.sh TAG
 set -o pipefail
@@ -11,7 +12,7 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
   > $O/pytest_gpu.log 2>&1 || { tail -20 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
-timeout -k 10 200 python tools/driver_region.py 25 K3 base= fork0=RT_FORK=0 q3=\;queues=3 q3fork0=RT_FORK=0\;queues=3 \
+timeout -k 10 200 python tools/driver_region.py 25 K3 base= fork0=RT_FORK=0 ctypes=RT_FASTCALL=0 r4=RT_FORK=0,RT_FASTCALL=0 q3=\;queues=3 \
   > $O/region_k3.jsonl 2> $O/region_k3.err || { tail $O/region_k3.err; exit 1; }
 cat $O/region_k3.jsonl
 ROC_ACTIVE_WAIT_TIMEOUT=2000 timeout -k 10 200 python tools/driver_region.py 25 K3 base= fork0=RT_FORK=0 \
