@@ -137,6 +137,11 @@ def parse():
                          "rt_set_frame_images EVERY, only the launch boundary between frames "
                          "removed); auto = dispatch for shares of at least "
                          "CHAIN_MAX_TILES + 1 tiles (whole images), chain below")
+    ap.add_argument("--host-wait", default=os.environ.get("RT_HOST_WAIT", "spin"),
+                    choices=["spin", "block"],
+                    help="how the host waits for the timed steps: poll their end event, then "
+                         "synchronize (spin), or synchronize at once (block: the HIP "
+                         "runtime's wait, which sleeps once its short active wait runs out)")
     ap.add_argument("--scan", default="culled", choices=["culled", "exhaustive"],
                     help="sphere-list scan: exact culling (default) or the reference's "
                          "exhaustive linear walk; images are bit-identical")
@@ -474,7 +479,7 @@ def _unserializable(o):
     return f"<{type(o).__name__} {getattr(o, '__name__', '')}>"
 
 
-def timed_steps(run, sync, world, barrier=None, device=None, stamp=None):
+def timed_steps(run, sync, world, barrier=None, device=None, stamp=None, wait=None):
     """The timed region of the K steps.  Every rank leaves an opening barrier (then
     synchronises), starts its clock, issues the steps (`run`), synchronises, and stops its
     clock: its own wall time of the K steps.  The closing barrier follows outside that time
@@ -483,8 +488,10 @@ def timed_steps(run, sync, world, barrier=None, device=None, stamp=None):
     The job's time is the MAX over ranks (all ranks start together after the opening
     barrier).  Returns {"dt": max over ranks, "per_rank": [s...], "issue": this rank's host
     issue time, "barrier_s": max over ranks of the closing barrier}.  `stamp(name)` (optional)
-    is called at the start, when the issue returns and after the synchronise."""
+    is called at the start, when the issue returns and after the synchronise.  `wait`
+    (default: sync) is the closing wait of the steps; it must end in a synchronise."""
     barrier = barrier or dist.barrier
+    wait = wait or sync
     sync()
     if world > 1:
         barrier()
@@ -496,7 +503,7 @@ def timed_steps(run, sync, world, barrier=None, device=None, stamp=None):
     t_issued = time.perf_counter()
     if stamp:
         stamp("issued")
-    sync()
+    wait()
     mine = time.perf_counter() - t0
     if stamp:
         stamp("synced")
@@ -656,9 +663,19 @@ def main():
         step_block(args.steps, args.warmup == 0)
         ev1.record(stream)
 
+    def spin_wait():
+        # --host-wait spin: poll the steps' end event until it has completed, then the
+        # synchronize (which then returns at once).  A render loop that waits for each frame
+        # polls; the runtime's blocking wait sleeps on an interrupt once its short active
+        # wait has run out and wakes up several µs after the GPU finished.
+        while not ev1.query():
+            pass
+        torch.cuda.synchronize()
+
     red_dev = "cuda" if backend == "nccl" else "cpu"
     ts = timed_steps(run, torch.cuda.synchronize, world, device=red_dev,
-                     stamp=stamp if host_t is not None else None)
+                     stamp=stamp if host_t is not None else None,
+                     wait=spin_wait if args.host_wait == "spin" else None)
     dt = ts["dt"]
     info = pipe.last_launch_info()             # the last timed rt_update_frames call
     # the job's one gather of the finished tiles, timed on its own (barrier on both sides)
@@ -772,6 +789,7 @@ def main():
         # max over ranks: the K steps by HIP events; each rank's own wall time of its K steps
         # (value's time is their max); the closing barrier after them, outside value
         "timed_breakdown_ms": {"steps": round(render_s * 1e3, 4),
+                               "host_wait": args.host_wait,
                                # host time of the steps' issue (this rank): the call returned
                                "host_issue": round(ts["issue"] * 1e3, 4),
                                "per_rank_ms": [round(x * 1e3, 4) for x in ts["per_rank"]],

@@ -6,8 +6,8 @@ and quartiles of the wall time per step (perf_counter around the call and the cl
 synchronize, as bench.py's value), of the HIP-event time per step, and of the host issue
 time of the call.
 
-Variants: name=ENV=V[,ENV=V...][;queues=Q], e.g.  fork0=RT_FORK=0  q3=;queues=3
-ctypes=RT_FASTCALL=0.  The library reads its diagnostic switches (RT_FORK, ...) from the
+Variants: name=ENV=V[,ENV=V...][;queues=Q][;wait=spin|block], e.g.  fork0=RT_FORK=0
+q3=;queues=3  ctypes=RT_FASTCALL=0  spin=;wait=spin.  The library reads its diagnostic switches (RT_FORK, ...) from the
 environment on every call; each variant has its own renderer, bound under its environment.
 usage: python tools/driver_region.py [R] [CFG] variant...   (CFG K3 | K2)"""
 import json
@@ -35,10 +35,10 @@ specs = sys.argv[3:] or ["base="]
 
 def parse(spec):
     name, _, rest = spec.partition("=")
-    env, _, q = rest.partition(";")
+    env, *opts = rest.split(";")
     kv = dict(x.split("=", 1) for x in env.split(",") if x)
-    queues = int(q.split("=")[1]) if q else 0
-    return name, kv, queues
+    o = dict(x.split("=", 1) for x in opts if x)
+    return name, kv, int(o.get("queues", 0)), o.get("wait", "block")
 
 
 variants = [parse(s) for s in specs]
@@ -65,7 +65,7 @@ while time.perf_counter() - t_w < 0.05:               # bench.py's --warm-ms 50
 res = {v[0]: {"wall": [], "events": [], "issue": []} for v in variants}
 base_env = dict(os.environ)
 for rep in range(R + 1):
-    for name, kv, queues in variants:
+    for name, kv, queues, wait in variants:
         os.environ.clear()
         os.environ.update(base_env)
         os.environ.update(kv)
@@ -81,6 +81,9 @@ for rep in range(R + 1):
         r.frames(cam_t, sc, seeds[5:25])
         t1 = time.perf_counter()
         e1.record(stream)
+        if wait == "spin":                             # (bench.py --host-wait spin)
+            while not e1.query():
+                pass
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         if rep == 0:
@@ -98,9 +101,10 @@ def q(v):
     return [round(s[len(s) // 4], 2), round(st.median(s), 2), round(s[(3 * len(s)) // 4], 2)]
 
 
-for name, kv, queues in variants:
+for name, kv, queues, wait in variants:
     d = res[name]
-    print(json.dumps({"cfg": CFG, "variant": name, "env": kv, "queues": queues, "reps": R,
+    print(json.dumps({"cfg": CFG, "variant": name, "env": kv, "queues": queues, "wait": wait,
+                      "reps": R,
                       "wall_us_per_step_q1_med_q3": q(d["wall"]),
                       "events_us_per_step_q1_med_q3": q(d["events"]),
                       "issue_us_q1_med_q3": q(d["issue"])}))
