@@ -142,6 +142,10 @@ def parse():
                     help="how the host waits for the timed steps: poll their end event, then "
                          "synchronize (spin), or synchronize at once (block: the HIP "
                          "runtime's wait, which sleeps once its short active wait runs out)")
+    ap.add_argument("--gate", action="store_true",
+                    help="diagnostic for profiled runs: hold the stream while the timed steps "
+                         "are issued, then release it (StreamGate); the line is then not a "
+                         "measurement")
     ap.add_argument("--scan", default="culled", choices=["culled", "exhaustive"],
                     help="sphere-list scan: exact culling (default) or the reference's "
                          "exhaustive linear walk; images are bit-identical")
@@ -523,6 +527,38 @@ def timed_steps(run, sync, world, barrier=None, device=None, stamp=None, wait=No
             "barrier_s": max(bars)}
 
 
+class StreamGate:
+    """--gate (diagnostic, never a measurement): the stream waits on a host-memory word
+    (hipStreamWaitValue32) while the timed steps are issued, and the host opens it after the
+    issue, so that the GPU runs the steps back to back however slowly the host issues them —
+    under rocprofv3's kernel trace every dispatch costs the host ~8 µs more, which starves a
+    one-launch-per-frame chain and distorts the trace (tools/timeline.py).  Uses the HIP
+    runtime torch loaded (same soname)."""
+
+    def __init__(self):
+        import ctypes
+        self.ct = ctypes
+        self.hip = ctypes.CDLL("libamdhip64.so.7")
+        p = ctypes.c_void_p()
+        if self.hip.hipHostMalloc(ctypes.byref(p), ctypes.c_size_t(64), 0) != 0:
+            raise RuntimeError("hipHostMalloc failed")
+        self.ptr = p
+        self.word = ctypes.c_uint32.from_address(p.value)
+        self.word.value = 0
+        self.n = 0
+
+    def hold(self, stream):
+        self.n += 1
+        rc = self.hip.hipStreamWaitValue32(self.ct.c_void_p(stream.cuda_stream), self.ptr,
+                                           self.ct.c_uint32(self.n), 0,        # >= n
+                                           self.ct.c_uint32(0xFFFFFFFF))
+        if rc != 0:
+            raise RuntimeError(f"hipStreamWaitValue32 failed ({rc})")
+
+    def release(self):
+        self.word.value = self.n
+
+
 def timed(stream, fn):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -658,9 +694,17 @@ def main():
         host_t[name] = (time.clock_gettime_ns(time.CLOCK_MONOTONIC),
                         time.clock_gettime_ns(time.CLOCK_BOOTTIME))
 
+    gate = StreamGate() if args.gate else None
+
     def run():
+        if gate:
+            gate.hold(stream)
         ev0.record(stream)
-        step_block(args.steps, args.warmup == 0)
+        try:
+            step_block(args.steps, args.warmup == 0)
+        finally:
+            if gate:
+                gate.release()
         ev1.record(stream)
 
     def spin_wait():
@@ -772,7 +816,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded scene + per-frame seeds; SURVEY §8d)"
-                + ("" if backend == "nccl" else f"; REHEARSAL over {backend}, not a measurement"),
+                + ("" if backend == "nccl" else f"; REHEARSAL over {backend}, not a measurement")
+                + ("; GATED issue (--gate): a profiling diagnostic, not a measurement"
+                   if args.gate else ""),
         "config": {"workload": f"{cfg} {desc}, max_depth {depth}",
                    "width": w, "height": h, "spheres": nsph, "spp_per_step": spf,
                    "max_depth": depth, "parallelism": f"stripes{world}",
