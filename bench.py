@@ -137,11 +137,6 @@ def parse():
                          "rt_set_frame_images EVERY, only the launch boundary between frames "
                          "removed); auto = dispatch for shares of at least "
                          "CHAIN_MAX_TILES + 1 tiles (whole images), chain below")
-    ap.add_argument("--host-wait", default=os.environ.get("RT_HOST_WAIT", "spin"),
-                    choices=["spin", "block"],
-                    help="how the host waits for the timed steps: poll their end event, then "
-                         "synchronize (spin), or synchronize at once (block: the HIP "
-                         "runtime's wait, which sleeps once its short active wait runs out)")
     ap.add_argument("--gate", action="store_true",
                     help="diagnostic for profiled runs: hold the stream while the timed steps "
                          "are issued, then release it (StreamGate); the line is then not a "
@@ -258,29 +253,32 @@ def cpu_baseline(cam, spheres, w, h, seconds):
                           "CPU the process can run on at once"}
 
 
-def load_pmc(config, kernel, frames_per_launch):
+def load_pmc(config, kernel, frames_per_launch, queues=1):
     """The newest committed rocprofv3 PMC summary of the timed kernel (tools/pmc_bench.sh),
-    if it was taken for the same kernel instance at the same frames per launch, and its
-    path."""
-    for rnd in ("r04", "r03", "r02"):
+    if it was taken for the same kernel instance at the same frames per launch and the same
+    concurrent parts per update (`queues`: a summary's per-launch counts are one part's), and
+    its path."""
+    for rnd in ("r05", "r04", "r03", "r02"):
         p = ROOT / "profiles" / f"pmc_{rnd}_{config}.json"
         if not p.exists():
             continue
         d = json.loads(p.read_text())
-        if d.get("kernel") == kernel and d.get("frames_per_launch") == frames_per_launch:
+        if (d.get("kernel") == kernel and d.get("frames_per_launch") == frames_per_launch
+                and d.get("queues", 1) == queues):
             return d, p.relative_to(ROOT).as_posix()
     return None, None
 
 
-def load_weighted(config, kernel):
+def load_weighted(config, kernel, pmc_path=None):
     """The weighted VALU cycles per launch of the timed kernel (tools/valu_weighted.py over
-    the PMC instruction classes and the instance's disassembly), if committed."""
-    for rnd in ("r04", "r03"):
+    the PMC instruction classes and the instance's disassembly), if committed — and, when the
+    file names the PMC summary it was computed from, only for that summary."""
+    for rnd in ("r05", "r04", "r03"):
         p = ROOT / "profiles" / f"valu_weighted_{rnd}_{config}.json"
         if not p.exists():
             continue
         d = json.loads(p.read_text())
-        if d.get("kernel") == kernel:
+        if d.get("kernel") == kernel and (pmc_path is None or d.get("pmc", pmc_path) == pmc_path):
             return d, p.relative_to(ROOT).as_posix()
     return None, None
 
@@ -707,19 +705,9 @@ def main():
                 gate.release()
         ev1.record(stream)
 
-    def spin_wait():
-        # --host-wait spin: poll the steps' end event until it has completed, then the
-        # synchronize (which then returns at once).  A render loop that waits for each frame
-        # polls; the runtime's blocking wait sleeps on an interrupt once its short active
-        # wait has run out and wakes up several µs after the GPU finished.
-        while not ev1.query():
-            pass
-        torch.cuda.synchronize()
-
     red_dev = "cuda" if backend == "nccl" else "cpu"
     ts = timed_steps(run, torch.cuda.synchronize, world, device=red_dev,
-                     stamp=stamp if host_t is not None else None,
-                     wait=spin_wait if args.host_wait == "spin" else None)
+                     stamp=stamp if host_t is not None else None)
     dt = ts["dt"]
     info = pipe.last_launch_info()             # the last timed rt_update_frames call
     # the job's one gather of the finished tiles, timed on its own (barrier on both sides)
@@ -766,12 +754,15 @@ def main():
         # (a load and a store per dispatch) is reported beside it, not as `achieved`.
         bytes_launch = local_px * (16 * fpl + 16)
         ref_bytes_launch = local_px * BYTES_PER_PIXEL_LAUNCH * fpl
-    pmc, pmc_path = load_pmc(cfg, kernel, fpl) if world == 1 else (None, None)
-    wgt, wgt_path = load_weighted(cfg, kernel) if pmc else (None, None)
+    pmc, pmc_path = load_pmc(cfg, kernel, fpl, queues) if world == 1 else (None, None)
+    wgt, wgt_path = load_weighted(cfg, kernel, pmc_path) if pmc else (None, None)
+    # (a summary's counts are per launch, i.e. per concurrent part: times the parts per update)
+    pq = pmc.get("queues", 1) if pmc else 1
     roof = {"bound": "hbm", "achieved": round(bytes_launch / launch_s / 1e9, 1),
             "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(bytes_launch / launch_s / 1e9 / PEAK_HBM_GBS, 4),
-            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+            "traffic": pmc["hbm_bytes_per_launch"] * pq if pmc and "hbm_bytes_per_launch" in pmc
+                       else None,
             "kernel": kernel, "kernel_avg_us": round(launch_s * 1e6, 2),
             "frames_per_launch": fpl, "launches_per_step": launches_per_step,
             "queues": queues, "submit": info.get("submit"),
@@ -783,7 +774,7 @@ def main():
                               "frac": round(bytes_launch / launch_s / 1e9 / RMW_FLOOR_GBS, 4),
                               "source": "tools/rmw_floor.hip, profiles/archive/r02_rmw_floor.jsonl"}}
     if pmc and pmc.get("valu_insts_per_launch"):
-        insts = pmc["valu_insts_per_launch"]
+        insts = pmc["valu_insts_per_launch"] * pq
         avail = SIMDS * CLOCK_GHZ * 1e9 * launch_s
         roof["valu"] = {"insts_per_launch": insts,
                         "issue_cycles": insts * VALU_ISSUE_CYCLES,
@@ -796,10 +787,11 @@ def main():
             # each PMC instruction class priced at the measured issue cost of the kernel's
             # own forms of that class (profiles/r0*_valu_rates.txt): the SIMD cycles the
             # VALU work holds, against what 1024 SIMDs offer at the 2.4-GHz peak clock
-            wc = wgt["weighted_cycles"]
+            wc = wgt["weighted_cycles"] * pq
             roof["valu"].update({
                 "weighted_cycles": wc, "weighted_frac": round(wc / avail, 4),
-                "weighted_frac_bounds": [round(b / avail, 4) for b in wgt["weighted_cycles_bounds"]],
+                "weighted_frac_bounds": [round(b * pq / avail, 4)
+                                         for b in wgt["weighted_cycles_bounds"]],
                 "mean_cycles_per_valu": wgt["mean_cycles_per_valu"], "weighted": wgt_path})
             roof["binding_frac"] = roof["valu"]["weighted_frac"]
 
@@ -835,7 +827,6 @@ def main():
         # max over ranks: the K steps by HIP events; each rank's own wall time of its K steps
         # (value's time is their max); the closing barrier after them, outside value
         "timed_breakdown_ms": {"steps": round(render_s * 1e3, 4),
-                               "host_wait": args.host_wait,
                                # host time of the steps' issue (this rank): the call returned
                                "host_issue": round(ts["issue"] * 1e3, 4),
                                "per_rank_ms": [round(x * 1e3, 4) for x in ts["per_rank"]],

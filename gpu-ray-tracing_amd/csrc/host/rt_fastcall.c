@@ -3,8 +3,9 @@
  * (gpu_ray_tracing.ComputeShaderPipeline.bind_update_frames) issues it without ctypes'
  * per-argument conversion and numpy's __array_interface__ dictionaries: a ctypes call of
  * the 14-argument function with the arrays' addresses looked up costs ≈ 8.7 µs of host
- * time on this image's CPU, all of it before the call's first launch reaches the GPU — inside
- * a 20-frame timed region of ≈ 320 µs ("Fixed cost of a call").
+ * time on the build container's CPU (0.3 µs through this binding), all of it before the
+ * call's first launch reaches the GPU; on the GPU boxes' EPYC the difference measured
+ * ≈ 2 µs per call (profiles/r05/r05b_region_k3.jsonl, DESIGN.md §5 "Fixed cost of a call").
  *
  *   update_frames(ctx, a, b, w, h, rank, nranks, camera, spheres, count, seeds, stream)
  *       -> newest image (0 / 1), or -status when the library returns an error
@@ -77,10 +78,14 @@ static PyObject* update_frames(PyObject* self, PyObject* const* args, Py_ssize_t
         return NULL;
     }
     int newest = -1;
-    const rt_status st = rt_update_frames(
-        (rt_ctx*)addr[0], (float*)addr[1], (float*)addr[2], u[0], u[1], u[2], u[3],
-        (const rt_scene_camera*)cam.buf, (const rt_sphere*)sph.buf, u[4],
-        (uint32_t)(seeds.len / 4), (const float*)seeds.buf, stream, &newest);
+    rt_status st;
+    /* (the GIL released while the library issues the launches, as ctypes does: the held
+     * buffers keep the arrays alive) */
+    Py_BEGIN_ALLOW_THREADS
+    st = rt_update_frames((rt_ctx*)addr[0], (float*)addr[1], (float*)addr[2], u[0], u[1], u[2],
+                          u[3], (const rt_scene_camera*)cam.buf, (const rt_sphere*)sph.buf, u[4],
+                          (uint32_t)(seeds.len / 4), (const float*)seeds.buf, stream, &newest);
+    Py_END_ALLOW_THREADS
     PyBuffer_Release(&cam);
     PyBuffer_Release(&sph);
     PyBuffer_Release(&seeds);

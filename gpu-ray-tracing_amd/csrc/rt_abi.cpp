@@ -1045,13 +1045,6 @@ rt_status ensure_aux_streams(rt_ctx* ctx, uint32_t n) {
     return RT_OK;
 }
 
-// How the parts of a call's first update are forked from the caller's stream: 1 (default)
-// skips the fork event when the stream is idle (hipStreamQuery), 0 always records it
-// (RT_FORK=0 in the environment, diagnostic A/B: tools/driver_region.py).
-int fork_mode() {
-    const char* e = std::getenv("RT_FORK");
-    return (e && e[0] == '0') ? 0 : 1;
-}
 
 // `stream` waits for everything issued on aux[0..n) so far
 rt_status join_aux(rt_ctx* ctx, uint32_t n, hipStream_t stream) {
@@ -1561,12 +1554,12 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
             // The fork: the aux streams wait for an event recorded on `stream` — unless
             // `stream` has nothing left to run (a new call on an idle stream: then everything
             // it was given is complete and the aux streams, joined into it at the end of the
-            // previous call, are idle too), which spares the first update the event record and
-            // the waits before its second part ("Fixed cost of a call").  Part 0
-            // goes out before the waits either way.
+            // previous call, are idle too), which spares the host the event record and the
+            // waits (two HIP calls; the GPU time measured the same either way,
+            // profiles/r05/r05b_region_k3.jsonl).  Part 0 goes out before the waits.
             bool wait_fork = false;
             if (!forked) {
-                if (fork_mode() == 0 || hipStreamQuery(stream) != hipSuccess) {
+                if (hipStreamQuery(stream) != hipSuccess) {
                     hipError_t e = hipEventRecord(ctx->fork_ev, stream);
                     if (e != hipSuccess) return hip_fail(e, "fork (hipEventRecord)");
                     wait_fork = true;

@@ -173,11 +173,9 @@ _fast = False
 def fastcall():
     """The CPython binding of rt_update_frames (build/_rt_fastcall*.so, csrc/host/rt_fastcall.c:
     the same library entry point without ctypes' per-call conversion), or None when it has
-    not been built, an experiment build of the library is selected (RT_HIP_LIB: the binding
-    links the in-tree librt_hip.so) or RT_FASTCALL=0 asks for ctypes (diagnostic A/B)."""
+    not been built or an experiment build of the library is selected (RT_HIP_LIB: the binding
+    links the in-tree librt_hip.so)."""
     global _fast
-    if os.environ.get("RT_FASTCALL") == "0":
-        return None
     if _fast is False:
         _fast = None
         if "RT_HIP_LIB" not in os.environ:

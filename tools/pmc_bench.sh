@@ -4,13 +4,16 @@
 # (MI355X_MICROARCH.md §HBM), then SQ/GRBM groups and the VALU instruction classes (two
 # passes of 8 SQ counters, read by tools/valu_weighted.py).  Writes gpurun_out/TAG/pmc_${PMC_ROUND}_CFG.json
 # (copy to profiles/ to have bench.py report `traffic` and `roofline.valu` from it).
-# Usage: [PMC_ROUND=r04] bash tools/pmc_bench.sh TAG "K3 K2 K4 K5"
+# QUEUES (default 0 = the library's choice, what bench.py times: two concurrent half-image
+# parts per K3 update) is passed as --queues; the summary records it, and bench.py scales the
+# per-launch counts by it (one update = QUEUES launches of equal halves).
+# Usage: [PMC_ROUND=r05] [QUEUES=0] bash tools/pmc_bench.sh TAG "K3 K2 K4 K5"
 set -o pipefail
-TAG=$1; CFGS=$2; PMC_ROUND=${PMC_ROUND:-r04}
+TAG=$1; CFGS=$2; PMC_ROUND=${PMC_ROUND:-r05}; QUEUES=${QUEUES:-0}
 cd $GRAFT_REPO_ROOT; O=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
 for c in $CFGS; do
-  ARGS="--config $c --side 0 --cpu-seconds 0 --queues 1"
+  ARGS="--config $c --side 0 --cpu-seconds 0 --queues $QUEUES"
   [ "$c" = "K5" ] && ARGS="$ARGS --steps 1 --warmup 1"
   timeout -k 10 300 python3 bench.py $ARGS > $O/pmc_bench_$c.json 2> $O/pmc_bench_$c.err \
     || { echo "bench $c failed"; tail -3 $O/pmc_bench_$c.err; exit 1; }
@@ -26,7 +29,8 @@ for c in $CFGS; do
       > $O/pmc_${c}_p$i.log 2>&1 || { echo "pmc $c pass $i failed"; tail -5 $O/pmc_${c}_p$i.log; exit 1; }
   done
   U=$(python3 -c "import json; print(json.loads(open('$O/pmc_bench_$c.json').read())['roofline']['kernel_avg_us'])")
-  python3 tools/pmc_bench_summary.py $O/pmc_${PMC_ROUND}_$c.json "$K" "$F" $O/raw/${c}_p*_counter_collection.csv \
+  Q=$(python3 -c "import json; print(json.loads(open('$O/pmc_bench_$c.json').read())['roofline']['queues'])")
+  PMC_QUEUES=$Q python3 tools/pmc_bench_summary.py $O/pmc_${PMC_ROUND}_$c.json "$K" "$F" $O/raw/${c}_p*_counter_collection.csv \
     || exit 1
   python3 -c "import json; d=json.load(open('$O/pmc_${PMC_ROUND}_$c.json')); d['kernel_avg_us']=$U; json.dump(d, open('$O/pmc_${PMC_ROUND}_$c.json','w'), indent=1)"
 done

@@ -6,6 +6,7 @@ usage: python tools/pmc_bench_summary.py OUT.json KERNEL FRAMES_PER_LAUNCH file.
 import collections
 import csv
 import json
+import os
 import statistics
 import sys
 
@@ -22,15 +23,20 @@ for f in files:
     for (_, c), v in per.items():
         vals[c].append(v)
 med = {c: statistics.median(v) for c, v in vals.items()}
-res = {"kernel": kernel, "frames_per_launch": fpl,
+# launches per timed unit (PMC_QUEUES: concurrent parts of one one-frame update, each a launch
+# over an equal share of the image's workgroups)
+queues = int(os.environ.get("PMC_QUEUES", "1"))
+res = {"kernel": kernel, "frames_per_launch": fpl, "queues": queues,
        "dispatches": {c: len(v) for c, v in vals.items()}, "median_per_launch": med}
 if "FETCH_SIZE" in med and "WRITE_SIZE" in med:
     res["hbm_read_bytes_per_launch"] = med["FETCH_SIZE"] * 2 * 1024
     res["hbm_write_bytes_per_launch"] = med["WRITE_SIZE"] * 1024
     res["hbm_bytes_per_launch"] = res["hbm_read_bytes_per_launch"] + res["hbm_write_bytes_per_launch"]
     res["correction"] = "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes"
+    res["hbm_bytes_per_update"] = res["hbm_bytes_per_launch"] * queues
 if "SQ_INSTS_VALU" in med:
     res["valu_insts_per_launch"] = med["SQ_INSTS_VALU"]
+    res["valu_insts_per_update"] = med["SQ_INSTS_VALU"] * queues
     res["valu_insts_per_wave"] = med["SQ_INSTS_VALU"] / max(1.0, med.get("SQ_WAVES", 1.0))
 if "GRBM_GUI_ACTIVE" in med:
     res["gui_active_cycles_per_xcd"] = med["GRBM_GUI_ACTIVE"] / 8
