@@ -1128,8 +1128,6 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
 #ifndef RT_TRACE_MIN_WAVES
 #define RT_TRACE_MIN_WAVES 7
 #endif
-// Waves (tiles) per workgroup: the culled instance shares the LDS copy of the records
-// among 4 waves; the others use RT_WG_WAVES (rt_kernels.h).
 // Kernel-argument prefetch (single-frame list instance, one tile per wave): the launch
 // parameters a wave reads are spread over ~12 cache lines of the 2.6-KB kernarg segment and
 // the compiler loads each just before its use — a chain of dependent scalar-cache misses at
@@ -1138,17 +1136,6 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
 // 23.40, profiles/r02_ab_single_frame.log).  Adding the first lines of the tile's candidate
 // and sphere records to it measured +1.0 us (the wave then waits for two HBM misses before
 // its first instruction of ray setup).
-// Image accesses of the trace kernel as non-temporal (streaming) loads (bit 1) / stores
-// (bit 2), so that the per-frame image traffic does not evict the candidate lists from L2.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 nt_load(const float4* a) {
-    const f32x4 v = __builtin_nontemporal_load((const f32x4*)a);
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void nt_store(float4 v, float4* a) {
-    const f32x4 w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, (f32x4*)a);
-}
 // Leading scalar arguments of rt_trace_kernel (before the TraceParams block): what a wave
 // needs before its first ray — the tile's candidate count, the seed-hash tables, the
 // accumulator and the tile geometry.  Built with -mllvm -amdgpu-kernarg-preload-count=9
@@ -1183,6 +1170,8 @@ __device__ __forceinline__ void karg_prefetch() {
     (void)d6; (void)d7; (void)d8; (void)d9; (void)d10;
 }
 
+// Waves (tiles) per workgroup: the culled instance shares the LDS copy of the records among
+// 4 waves; a frame-group instance is one tile's group; the others RT_WG_WAVES (rt_kernels.h).
 template <int kScan>
 constexpr uint32_t wg_waves() {
     return kScan == kTraceCulled ? 4u : is_group_kernel(kScan) ? frame_group<kScan>() : RT_WG_WAVES;
