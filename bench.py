@@ -682,6 +682,8 @@ def main():
         r.finish()
     # (HIP events created before the timed region: their creation is host work, not steps)
     ev0, ev1, ev2, ev3 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+    for e in (ev0, ev1, ev2, ev3):
+        e.record(stream)      # (torch creates an event at its first record: not in the region)
 
     # timed: K steps issued by rt_update_frames (timed_steps: opening barrier, each rank's
     # own clock around its steps and synchronize, the max over ranks; the closing barrier

@@ -160,15 +160,13 @@ class StripeRenderer:
     def frames(self, camera, spheres, seeds) -> None:
         """len(seeds) progressive frames, one `update` dispatch each, from a single call."""
         if self.rows:
-            run = self._runs[self.cur] if self._runs else None
             bind = getattr(self.pipe, "bind_update_frames", None)
-            if run is None and bind is not None:
-                # (bound once per ping-pong direction: the buffers are this renderer's own)
-                run = bind(self.buf[self.cur], self.buf[1 - self.cur], self.width, self.height,
-                           self.rank, self.world)
-                if self._runs is None:
-                    self._runs = [None, None]
-                self._runs[self.cur] = run
+            if self._runs is None and bind is not None:
+                # both ping-pong directions bound at the first call (the buffers are this
+                # renderer's own), so that no later call — a timed one — pays for a binding
+                self._runs = [bind(self.buf[k], self.buf[1 - k], self.width, self.height,
+                                   self.rank, self.world) for k in (0, 1)]
+            run = self._runs[self.cur] if self._runs else None
             if run is not None:
                 newest = run(camera, spheres, seeds)
             else:
