@@ -370,21 +370,33 @@ def driver_record_sides(device, stream, main_cfg, main_us):
                 sc, seeds, cam = rt.SphereCollection(g["spheres"]), g["seeds"], rt.SceneCamera(g["camera"])
             return w, h, sc, seeds, cam
 
-        def dispatch_share(cfg, world, mode, rank=0):
-            # the driver's structure: 5 frames from a reset, then 20 timed (25-frame fixture);
-            # one untimed pass first on scratch images (the share's lists, order, code)
+        def dispatch_share(cfg, world, mode, rank=0, reps=3, warm_s=0.005):
+            # the driver's structure: 5 frames from a reset, then 20 timed (25-frame fixture),
+            # as each rank of bench.py --gpus N runs it after its warm-up: untimed frames on
+            # scratch images first (the share's lists, order and code, and warm_s of the same
+            # frames, so that the GPU is not coming out of idle — DESIGN.md §7), then `reps`
+            # timed regions, each from a reset; the median
             w, h, sc, seeds, cam = setup(cfg)
             set_frame_launch(pipe, mode)
             cam_t = cam.with_fields(camera_has_moved=0.0)
             scratch = StripeRenderer(pipe, w, h, rank, world)
-            scratch.frames(cam, sc, seeds[:20])
+            t_w = time.perf_counter()
+            while True:
+                scratch.frames(cam, sc, seeds[:20])
+                torch.cuda.synchronize()
+                if time.perf_counter() - t_w >= warm_s:
+                    break
             del scratch
             r = StripeRenderer(pipe, w, h, rank, world)
-            r.frames(cam, sc, seeds[:5])
-            t = timed(stream, lambda: r.frames(cam_t, sc, seeds[5:25])) / 20
+            runs = []
+            for _ in range(reps):
+                r.frames(cam, sc, seeds[:5])
+                runs.append(timed(stream, lambda: r.frames(cam_t, sc, seeds[5:25])) / 20)
+            t = sorted(runs)[len(runs) // 2]
             info = pipe.last_launch_info()
             return {"us_per_step": round(t * 1e6, 2), "kernel": info["kernel_name"],
                     "launches_per_step": round(info["launches"] / 20, 3),
+                    "runs_us": [round(x * 1e6, 2) for x in runs],
                     "image_ok": share_pixels_ok(cfg, r.local, 25, world, rank)}
 
         def k5_share(world, rank=0):
