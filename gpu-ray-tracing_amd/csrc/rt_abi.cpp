@@ -868,7 +868,8 @@ uint32_t fill_hint(rtk::TraceParams& p, uint32_t n_in) {
     for (uint32_t f = 0; f < p.frames; ++f) {
         if (f < hf) {
             p.hint_n[f] = n;
-            p.hint_rcp[f] = 1.0 / ((double)n + 1.0);
+            // RN32(1 / f32(n + 1)) (exact integer for n + 1 <= 2^24, where the kernels use it)
+            p.hint_rcp[f] = 1.0f / (float)(n + 1u);
             const uint32_t B = p.seed_b[f];
             for (uint32_t i = 0; i < depth; ++i) {
                 // wgsl:268 with seed + 1 = n + B + 2 (wgsl:353, 358)

@@ -123,9 +123,9 @@ struct TraceParams {
     const uint32_t* unit_count;
     uint32_t hint_frames;  // 0 = no hint
     uint32_t hint_n[kHintFrames];
-    // RN64(1 / (hint_n[f] + 1)): the accumulator's division by f32(n + 1) as one f64
-    // multiply (rt_kernels.hip, trace_pair; exact for n + 1 <= 2^24)
-    double hint_rcp[kHintFrames];
+    // RN32(1 / f32(hint_n[f] + 1)): the accumulator's division by f32(n + 1) as a Markstein
+    // division (rtd::div_rn; exact for n + 1 <= 2^24 on the checked domain)
+    float hint_rcp[kHintFrames];
     float4 hint_rs[kHintEntries];
     uint32_t seed_b[kMaxFramesPerLaunch];
 };

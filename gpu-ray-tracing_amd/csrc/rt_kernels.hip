@@ -243,31 +243,33 @@ constexpr bool kStoreEach = is_list_kernel(kScan);
 // operands), 16 the defocus disk's reciprocal table (disk_unit).  K3 per frame (fused): 21.7 us without, 20.9 / 20.1 / 20.1 us with bits
 // 1 / 1-2 / 1-4; the accumulator's three divisions by f32(n + 1) the same way (checked
 // numerators in [2^-88, 2^88)) measured +0.75 us and are left to the compiler.
-// The accumulator's division by f32(n + 1) as RN32(num * RN64(1 / (n + 1))) in the frame
-// groups, where every pixel holds the hinted count n (trace_pair: K3 16.5 against 17.3 us
-// per fused frame; the same in the one-wave loop measured +1.4 us per single-frame update,
-// from its register pressure, and is not used).
-// Exactness of acc_f64: for an integer k <= 2^24 and a quotient q = num / k in the normal
-// f32 range, q never falls on an f32 rounding midpoint (a midpoint has 25 significant bits
-// with an odd last one, so num = midpoint * k would need 25) and lies at least 2^-49
-// (relative) from every one; RN64(1 / k) and the f64 product are within 2^-52 of exact, so
-// the f64 result rounds to the same f32 as the exact quotient.  num = +-0, inf and NaN
-// pass through as in the division.  Subnormal quotients can sit exactly on a midpoint
-// (k even), so numerators in (0, 2^-102) — the only ones that give them for k <= 2^24 —
-// take the IEEE division (acc_f64_ok).  rt_selftest_fastmath replays it on random cases.
+// The accumulator's division by f32(n + 1) (wgsl:356) where every pixel of the wave holds
+// the hinted count n (the one-frame kernel, the frame groups of trace_pair): a Markstein
+// division by k = f32(n + 1) with y = RN32(1 / k) from the host (acc_rn: a multiply and two
+// fmas per channel; round 5, against round 2's RN32(num * RN64(1 / k)), acc_f64: two
+// conversions and an f64 multiply per channel, each a 4-cycle VALU form).  Exactness: for
+// an integer k <= 2^24, div_rn (rt_device.h) returns the IEEE quotient whenever num and the
+// quotient are normal; numerators in (0, 2^-102) could give subnormal quotients and take the
+// IEEE division (acc_ok: one unsigned compare per channel on the bit patterns; zero passes).
+// Zero, inf and NaN numerators need no exclusion in this use: num = col - c with the sample
+// colour col finite (|col| <= 1: a product of albedos in [0, 1] and the sky's [0.5, 1]) or
+// NaN (a degenerate refraction); -0 / k comes out +0, but num = -0 needs c = +0 and c + (+-0)
+// is +0 either way; num = +-inf needs c = -+inf, and c + num / k and c + div_rn(...) are NaN
+// both (inf - inf); NaN propagates through both.  rt_selftest_fastmath replays it on random
+// accumulators and colours.
 constexpr uint32_t kBits2m102 = 0x0C800000u;   // 2^-102
-__device__ __forceinline__ bool acc_f64_ok(v3 num) {
+__device__ __forceinline__ bool acc_ok(v3 num) {
     // |x| >= 2^-102 or x == +-0 (NaN, inf pass): one unsigned compare per channel
     return min(min(abs_bits(num.x) - 1u, abs_bits(num.y) - 1u), abs_bits(num.z) - 1u) >=
            kBits2m102 - 1u;
 }
-// (acc_f64_ok(num) == min_bits >= kBits2m102 - 1)
+// (acc_ok(num) == acc_min_bits(num) >= kBits2m102 - 1)
 __device__ __forceinline__ uint32_t acc_min_bits(v3 num) {
     return min(min(abs_bits(num.x) - 1u, abs_bits(num.y) - 1u), abs_bits(num.z) - 1u);
 }
-__device__ __forceinline__ v3 acc_f64(v3 c, v3 num, double y) {
-    return mk(c.x + (float)((double)num.x * y), c.y + (float)((double)num.y * y),
-              c.z + (float)((double)num.z * y));
+// c + num / k with y = RN32(1 / k)
+__device__ __forceinline__ v3 acc_rn(v3 c, v3 num, float k, float y) {
+    return mk(c.x + div_rn(num.x, k, y), c.y + div_rn(num.y, k, y), c.z + div_rn(num.z, k, y));
 }
 template <int kScan>
 constexpr bool fast_core(int bit) { return is_list_kernel(kScan); }
@@ -681,8 +683,8 @@ __device__ __forceinline__ Cam cam_params(const P& p) {
 // [1 - 6*2^-24, 1 + 2^-23], |sa| >= 2^-30 or sa == +0 and |ca| >= 2^-27 (checked
 // exhaustively by rt_selftest_fastmath).  kTable: 1 / sqrtf(len2) has eight values;
 // s_disk_rcp holds them as RN64(1 / len) (each workgroup fills it, init_disk_rcp), and
-// ca / len = RN32(ca * RN64(1 / len)) — the f64-reciprocal division of acc_f64, exact for
-// normal quotients and zeros.  Otherwise sqrt_core / div_core, also exact on this domain.
+// ca / len = RN32(ca * RN64(1 / len)) — an f64-reciprocal division, exact for normal
+// quotients and zeros (no f32 quotient lies within 2^-49 of a rounding midpoint).  Otherwise sqrt_core / div_core, also exact on this domain.
 __shared__ double s_disk_rcp[8];
 constexpr uint32_t kDiskLen2Lo = 0x3F7FFFFAu;   // 1 - 6 * 2^-24
 __device__ __forceinline__ void init_disk_rcp() {
@@ -1098,10 +1100,10 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
                 uint32_t na = nb;
                 if (nb < spp) {                                   // wgsl:352-358
                     const v3 num = sub(col, c);
-                    // num / f32(nb + 1) (wgsl:356) as RN32(num * RN64(1 / k)) (acc_f64)
+                    // num / f32(nb + 1) (wgsl:356) as a Markstein division (acc_rn)
                     if (nb < (1u << 24) &&
-                        rt_ballot(tc.valid && !acc_f64_ok(num)) == 0ull) {
-                        c = acc_f64(c, num, p.hint_rcp[fj]);
+                        rt_ballot(tc.valid && !acc_ok(num)) == 0ull) {
+                        c = acc_rn(c, num, (float)(nb + 1u), p.hint_rcp[fj]);
                     } else {
                         const float k = (float)(nb + 1u);         // wgsl:356
                         c = mk(c.x + num.x / k, c.y + num.y / k, c.z + num.z / k);
@@ -1307,10 +1309,8 @@ struct SingleParams {
     uint32_t n_hint;       // every pixel's count before the frame (0 on reset)
     uint32_t seed_b;       // B = u32(random_seed * 2^32) (wgsl:311, 353)
     uint32_t hy_off;       // hash(y * 51) table offset in the hx buffer
-    double rcp_hint;       // RN64(1 / (n_hint + 1))
-    // (12 unused bytes: the kernels' register allocation and kernarg loads were tuned and
-    // measured with the fields after them at these offsets)
-    uint32_t reserved[3];
+    float rcp_hint;        // RN32(1 / f32(n_hint + 1)) (acc_rn)
+    uint32_t reserved[5];  // (the fields after keep round 4's offsets)
     // local bands of a launch in raster order (no a_order): lband = first + blockIdx.y *
     // step, first | step << 16 — one of the update's concurrent parts (launch_single)
     uint32_t lbands;
@@ -1324,6 +1324,8 @@ struct SingleParams {
     // stores are dropped (rt_chain.cpp; rt_single_kernel ignores it)
     const uint32_t* abort;
 };
+static_assert(offsetof(SingleParams, lbands) == 76,
+              "SingleParams keeps round 4's offsets after rcp_hint");
 
 // Tiles per wave of the two instances: kTraceSingle (whole-image launches) and
 // kTraceSingleOne (small per-rank shares, where more, shorter waves fill the chip).
@@ -1801,7 +1803,7 @@ __device__ __forceinline__ void single_body(
                 const v3 num = sub(col[s], c[s]);
                 if (ng < (1u << 24) &&
                     (mask_ult(acc_min_bits(num), kBits2m102 - 1u) & valid_m[s]) == 0ull) {
-                    c[s] = acc_f64(c[s], num, p.rcp_hint);
+                    c[s] = acc_rn(c[s], num, (float)(ng + 1u), p.rcp_hint);
                 } else {
                     const float k = (float)(ng + 1u);             // wgsl:356
                     c[s] = mk(c[s].x + num.x / k, c[s].y + num.y / k, c[s].z + num.z / k);
@@ -2766,9 +2768,10 @@ __global__ __launch_bounds__(256) void rt_present_kernel(const float4* __restric
 //         sqrtf and the IEEE divisions (also the eight-value range of len2 the table needs).
 // cnt[1]: div_core_signed vs a / b on random a, b over div_core's domain (rt_device.h:
 //         |b| in [2^-20, 2^33), |a| in [2^-100, 2^91), exponent gap in [-120, 88]; a also
-//         +-0, b also the accumulator's n + 1 up to 2^32) and over [2^-40, 2^40]^2; and
-//         acc_f64 vs the division for numerators acc_f64_ok accepts (any f32 bits, many
-//         near the subnormal range) and k in [1, 2^24].
+//         +-0, b also the accumulator's n + 1 up to 2^32) and over [2^-40, 2^40]^2;
+//         div_rn (y = RN32(1 / b)) vs a / b beyond integer denominators (|b| in
+//         [2^-20, 2^20], |a| in [2^-100, 2^43]); and acc_rn vs c + num / k for numerators acc_ok accepts
+//         (finite f32 bits or NaN, many near the subnormal range) and k in [1, 2^24].
 // cnt[2]: sqrt_core vs sqrtf on every finite x >= 2^-96 (exhaustive).
 // cnt[3]: consider_fast vs consider (root selection, tmax and index) on random rays and
 //         spheres of the camera-ray domain (|d|^2 in [2^-11, 2^20], |O|, |C| + |R| <= 2^39),
@@ -2875,16 +2878,22 @@ __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cn
             if (dd <= 0x1p40f && (dy == 0.0f || fabsf(dy) >= 0x1p-100f))
                 bad1 += !same_bits(div_core(dy, len, y), dy / sqrtf(dd));
         }
-        // the accumulator's f64-reciprocal division: any f32 numerator (r0's bits: zeros,
-        // subnormals, inf, NaN included), k = f32(n + 1) for n + 1 in [1, 2^24]
+        {   // div_rn with real denominators (the Markstein step's general domain)
+            const float rb = with_exp(r1, -20 + (int)(r2 % 41u));
+            const float ra = with_exp(r0 ^ r2, -100 + (int)((r2 >> 8) % 144u));
+            bad1 += !same_bits(div_rn(ra, rb, 1.0f / rb), ra / rb);
+        }
+        // the accumulator's Markstein division: any finite f32 numerator or NaN (r0's bits:
+        // zeros and subnormals included; the kernels' num = col - c is never +-inf against a
+        // finite c, see acc_ok), k = f32(n + 1) for n + 1 in [1, 2^24]
         const uint32_t kk = (r2 & 0x800000u) ? 1u + (r1 & 0xFFFFFFu)
                                              : 1u + (r1 % 4096u);   // small counts too
         const v3 num = mk(__uint_as_float(r0), __uint_as_float(r0 ^ r1),
                           __uint_as_float(r2 & 0x83FFFFFFu));       // (many tiny ones)
-        if (acc_f64_ok(num)) {
+        if (acc_ok(num) && !isinf(num.x) && !isinf(num.y) && !isinf(num.z)) {
             const float kf = (float)kk;
             const v3 c0 = mk(0.0f, 0.0f, 0.0f);
-            const v3 q = acc_f64(c0, num, 1.0 / (double)kk);
+            const v3 q = acc_rn(c0, num, kf, 1.0f / kf);
             bad1 += !same_bits(q.x, 0.0f + num.x / kf) || !same_bits(q.y, 0.0f + num.y / kf) ||
                     !same_bits(q.z, 0.0f + num.z / kf);
         }
