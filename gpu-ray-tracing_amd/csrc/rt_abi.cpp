@@ -907,14 +907,6 @@ void fill_camera(rtk::TraceParams& p, const rt_scene_camera& c) {
         p.ddv[i] = c.defocus_disk_v[i];
     }
     p.defocus_angle = c.defocus_angle;
-    // the defocus disk's eight reciprocals (rt_kernels.hip init_disk_rcp): IEEE sqrtf and a
-    // correctly rounded f64 division, as the device would compute them
-    for (uint32_t k = 0; k < 8u; ++k) {
-        const uint32_t bits = 0x3F7FFFFAu + k;
-        float len2;
-        std::memcpy(&len2, &bits, 4);
-        p.disk_rcp[k] = 1.0 / (double)std::sqrt(len2);
-    }
     p.depth = host_f2u(c.max_depth);
     p.spp = host_f2u(c.samples_per_pixel);
 }

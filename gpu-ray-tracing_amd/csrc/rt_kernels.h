@@ -102,9 +102,6 @@ struct TraceParams {
     // s_memtime duration there, for launch_tile_order.
     const uint32_t* tile_order;
     uint32_t* tile_cost;
-    // RN64(1 / sqrtf(f32 bits 0x3F7FFFFA + k)), k = 0..7: the defocus disk's reciprocal
-    // table (rt_kernels.hip disk_unit), computed on the host
-    double disk_rcp[8];
     // bounce instance (kTraceBounce): compact live paths across the workgroup's waves
     // after every bounce (1), let each wave keep its own paths (0), frame pairs (2), or
     // split each tile's frames into `split` chunks traced by separate waves (3)

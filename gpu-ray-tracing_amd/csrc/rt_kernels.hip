@@ -273,9 +273,8 @@ __device__ __forceinline__ v3 acc_rn(v3 c, v3 num, float k, float y) {
 }
 template <int kScan>
 constexpr bool fast_core(int bit) { return is_list_kernel(kScan); }
-// The defocus disk's reciprocal in the camera-ray-only trace instances: the workgroup's LDS
-// table (one barrier at wave start)
-constexpr int kTraceDisk = 1;
+// The defocus disk's normalisation in the camera-ray-only trace instances (disk_unit)
+constexpr int kTraceDisk = 3;
 
 // Scan records are read through the constant address space: they do not change during a
 // launch, and only then may the compiler use scalar loads (s_load_dwordx8/16 into SGPRs)
@@ -681,52 +680,19 @@ __device__ __forceinline__ Cam cam_params(const P& p) {
 // The defocus disk's normalize((cos, sin)) (wgsl:327-331).  Over all 2^32 values of
 // hash(seed + 1), len2 = sa^2 + ca^2 takes only the eight f32 values of
 // [1 - 6*2^-24, 1 + 2^-23], |sa| >= 2^-30 or sa == +0 and |ca| >= 2^-27 (checked
-// exhaustively by rt_selftest_fastmath).  kTable: 1 / sqrtf(len2) has eight values;
-// s_disk_rcp holds them as RN64(1 / len) (each workgroup fills it, init_disk_rcp), and
-// ca / len = RN32(ca * RN64(1 / len)) — an f64-reciprocal division, exact for normal
-// quotients and zeros (no f32 quotient lies within 2^-49 of a rounding midpoint).  Otherwise sqrt_core / div_core, also exact on this domain.
-__shared__ double s_disk_rcp[8];
-constexpr uint32_t kDiskLen2Lo = 0x3F7FFFFAu;   // 1 - 6 * 2^-24
-__device__ __forceinline__ void init_disk_rcp() {
-    if (threadIdx.x < 8u)
-        s_disk_rcp[threadIdx.x] = 1.0 / (double)sqrtf(__uint_as_float(kDiskLen2Lo + threadIdx.x));
-}
-// The same table from the launch parameters (the host computes it with the same IEEE
-// operations, rt_abi.cpp fill_camera): eight selects from SGPRs at every wave start instead
-// of a square root and an f64 division.  (The self-test keeps the device computation, and
-// every parity test compares the two through the image bits.)
-__device__ __forceinline__ void init_disk_rcp(const TraceParams& p) {
-    if (threadIdx.x < 8u) {
-        double v = 0.0;
-#pragma unroll
-        for (uint32_t k = 0; k < 8u; ++k) {
-            double dk = p.disk_rcp[k];
-            asm volatile("" : "+s"(dk));   // a scalar (kernarg) value, not a per-lane load
-            if (threadIdx.x == k) v = dk;
-        }
-        s_disk_rcp[threadIdx.x] = v;
-    }
-}
-// The eight table entries in closed form: sqrtf(len2) = 1 - m 2^-24 with
-// m = (0x3F800001 - bits(len2)) >> 1 in {3, 3, 2, 2, 1, 1, 0, 0}, and
-// RN64(1 / (1 - m 2^-24)) = 1 + m 2^-24 + m^2 2^-48 exactly (the next term, m^3 2^-72, is
-// below half an ulp of 1): the f64 bits 0x3FF00000 : (m << 28 | m^2 << 4).  (rt_abi.cpp
-// fill_camera computes the table with the IEEE operations; the self-test compares the
-// register form with the IEEE division for all 2^32 seeds.)
-__device__ __forceinline__ double disk_rcp_reg(float len2) {
-    const uint32_t m = (0x3F800001u - __float_as_uint(len2)) >> 1;
-    // (m <= 3 on the domain: a 24-bit multiply, v_mul_u32_u24, instead of v_mul_lo_u32)
-    const uint32_t lo = (m << 28) | (__umul24(m, m) << 4);
-    return __hiloint2double(0x3FF00000, (int)lo);
-}
-// kTable: 0 = sqrt_core / div_core, 1 = the LDS table (s_disk_rcp), 2 = disk_rcp_reg,
+// exhaustively by rt_selftest_fastmath), so sqrtf(len2) = 1 - m 2^-24 with
+// m = (0x3F800001 - bits(len2)) >> 1 in {3, 3, 2, 2, 1, 1, 0, 0}.
+// kTable: 0 = sqrt_core / div_core (exact on this domain);
 // 3 = all-f32: len = sqrtf(len2) = 1 - m 2^-24 (bits 0x3F800000 - m) and y = RN32(1 / len)
 // = 1 + ((m + 1) >> 1) 2^-23 (m = 1: 1 + 2^-24 + 2^-48 rounds up; m = 3: 1 + 1.5 ulp + 9
 // 2^-48 rounds to 2 ulp) from the bits of len2, then one Markstein step — q0 = RN(a y), the
 // exact residual r = fma(-len, q0, a), q = RN(q0 + r y) — the correctly rounded a / len
 // for a correctly rounded y (checked against the IEEE division for all 2^32 seeds by
-// rt_selftest_fastmath).  Six f32 operations and four integer ones instead of the f64 path's
-// two conversions, multiply and conversion back per component.
+// rt_selftest_fastmath).  Six f32 operations and four integer ones.  (Rounds 2-4 also had
+// an f64 table of RN64(1 / len), per workgroup in LDS or in closed form: the all-f32 form
+// replaced it in the one-frame kernel in round 3 and in the frame groups in round 5 — no
+// table, no barrier at wave start; an 8-rank K3 chain share 2.69 -> 2.65 us per step,
+// profiles/r05/r05h/.)
 template <int kTable>
 __device__ __forceinline__ void disk_unit(float sa, float ca, float& ux, float& uy) {
     const float len2 = fmaf(sa, sa, ca * ca);
@@ -737,11 +703,6 @@ __device__ __forceinline__ void disk_unit(float sa, float ca, float& ux, float& 
         const float qx = ca * y, qy = sa * y;
         ux = fmaf(fmaf(-len, qx, ca), y, qx);
         uy = fmaf(fmaf(-len, qy, sa), y, qy);
-    } else if (kTable) {
-        const double y = kTable == 2 ? disk_rcp_reg(len2)
-                                     : s_disk_rcp[__float_as_uint(len2) - kDiskLen2Lo];
-        ux = (float)((double)ca * y);
-        uy = (float)((double)sa * y);
     } else {
         const float len = sqrt_core(len2);
         const float y = rcp_refined(len);
@@ -1249,10 +1210,6 @@ __global__ __launch_bounds__(64 * wg_waves<kScan>(), RT_TRACE_MIN_WAVES) void rt
             lds_recs[j] = g0;
             if (j + 256u < p.lds_records) lds_recs[j + 256u] = g1;
         }
-        __syncthreads();
-    }
-    if (fast_core<kScan>(16) && kTraceDisk == 1) {               // (disk_unit's table)
-        init_disk_rcp(p);
         __syncthreads();
     }
     if (!wave_in) return;                                         // whole wave exits
@@ -2765,7 +2722,7 @@ __global__ __launch_bounds__(256) void rt_present_kernel(const float4* __restric
 
 // ---- Self-test of the exact fast paths (rt_selftest_fastmath) ------------------------
 // cnt[0]: defocus normalisation, all 2^32 values of hash(seed + 1): both disk_unit forms vs
-//         sqrtf and the IEEE divisions (also the eight-value range of len2 the table needs).
+//         sqrtf and the IEEE divisions (also the eight-value range of len2 disk_unit<3> needs).
 // cnt[1]: div_core_signed vs a / b on random a, b over div_core's domain (rt_device.h:
 //         |b| in [2^-20, 2^33), |a| in [2^-100, 2^91), exponent gap in [-120, 88]; a also
 //         +-0, b also the accumulator's n + 1 up to 2^32) and over [2^-40, 2^40]^2;
@@ -2823,8 +2780,6 @@ __device__ __forceinline__ bool root_case(uint64_t i) {
     return same_bits(t1, t2) && i1 == i2;
 }
 __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cnt, uint64_t n_rand) {
-    init_disk_rcp();
-    __syncthreads();
     unsigned long long bad0 = 0, bad1 = 0, bad2 = 0, bad3 = 0, runs = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32);
@@ -2834,19 +2789,13 @@ __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cn
         sincos_c(ang, sa, ca);
         const float len_ref = sqrtf(fmaf(sa, sa, ca * ca));
         const float ux_ref = ca / len_ref, uy_ref = sa / len_ref;
-        float ux, uy, tx, ty, gx, gy, fx, fy;
+        float ux, uy, fx, fy;
         disk_unit<0>(sa, ca, ux, uy);
-        disk_unit<1>(sa, ca, tx, ty);
-        disk_unit<2>(sa, ca, gx, gy);
         disk_unit<3>(sa, ca, fx, fy);
         bad0 += (__float_as_uint(fx) != __float_as_uint(ux_ref)) ||
                 (__float_as_uint(fy) != __float_as_uint(uy_ref)) ||
                 (__float_as_uint(ux) != __float_as_uint(ux_ref)) ||
-                (__float_as_uint(uy) != __float_as_uint(uy_ref)) ||
-                (__float_as_uint(tx) != __float_as_uint(ux_ref)) ||
-                (__float_as_uint(ty) != __float_as_uint(uy_ref)) ||
-                (__float_as_uint(gx) != __float_as_uint(ux_ref)) ||
-                (__float_as_uint(gy) != __float_as_uint(uy_ref));
+                (__float_as_uint(uy) != __float_as_uint(uy_ref));
         const float x = __uint_as_float((uint32_t)i);
         if ((uint32_t)i >= 0x0F800000u && (uint32_t)i < 0x7F800000u)   // [2^-96, +inf)
             bad2 += __float_as_uint(sqrt_core(x)) != __float_as_uint(sqrtf(x));
