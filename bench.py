@@ -370,12 +370,13 @@ def driver_record_sides(device, stream, main_cfg, main_us):
                 sc, seeds, cam = rt.SphereCollection(g["spheres"]), g["seeds"], rt.SceneCamera(g["camera"])
             return w, h, sc, seeds, cam
 
-        def dispatch_share(cfg, world, mode, rank=0, reps=3, warm_s=0.005):
+        def dispatch_share(cfg, world, mode, rank=0, reps=5, warm_s=0.05):
             # the driver's structure: 5 frames from a reset, then 20 timed (25-frame fixture),
             # as each rank of bench.py --gpus N runs it after its warm-up: untimed frames on
             # scratch images first (the share's lists, order and code, and warm_s of the same
-            # frames, so that the GPU is not coming out of idle — DESIGN.md §7), then `reps`
-            # timed regions, each from a reset; the median
+            # frames — the main line's --warm-ms: the host's image check of the previous side
+            # line leaves the GPU idle, and 5 ms of warm-up measured 0.3-0.8 us per step
+            # slower), then `reps` timed regions, each from a reset; the median
             w, h, sc, seeds, cam = setup(cfg)
             set_frame_launch(pipe, mode)
             cam_t = cam.with_fields(camera_has_moved=0.0)

@@ -89,6 +89,10 @@ __device__ __forceinline__ void sst_put(int k, unsigned long long t) {
         asm volatile("" ::"s"(dep));                         \
         sst_put((k), __builtin_amdgcn_s_memtime());          \
     } while (0)
+#elif defined(RT_MARKS)
+// (asm-inspection builds: a comment in the code at each phase boundary, after its value)
+#define SST_V(k, dep) asm volatile(";MARK " #k ::"v"(dep))
+#define SST_S(k, dep) asm volatile(";MARK " #k ::"s"(dep))
 #else
 #define SST_V(k, dep) ((void)0)
 #define SST_S(k, dep) ((void)0)
