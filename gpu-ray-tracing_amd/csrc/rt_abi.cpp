@@ -36,6 +36,9 @@ struct rt_ctx {
     // |R| lies in [2^-20, 2^20]: the scene half of camera_rays_bounded
     double scene_bound = 0.0;
     bool radii_ok = true;
+    // every radius's rcp_refined is RN32(1 / R) (rt_rcp_check_kernel; TraceParams::normal_rn)
+    bool normal_rn = false;
+    uint32_t* d_flag = nullptr;     // the check's result word
     // XZ grid of the small spheres for bounce rays (build_grid; TraceParams
     // grid_*): device arrays and the parameters copied into every launch.
     void* d_grid = nullptr;  // cell ranges (uint2), item records (float4), item indices, big list
@@ -82,7 +85,7 @@ struct rt_ctx {
     };
     std::vector<CountRecord> counts;
     uint32_t frames_per_launch = 0;  // rt_update_frames fusion cap (0 = automatic)
-    rt_launch_info last = {0, 0, 0, -1, 0, 0};  // the last call's launches (rt_last_launch_info)
+    rt_launch_info last = {0, 0, 0, -1, 0, 0, 0};  // the last call's launches (rt_last_launch_info)
     int path_compaction = RT_PATHS_AUTO;
     int frame_pairs = RT_FRAME_PAIRS_AUTO;
     int single_kernel = RT_SINGLE_AUTO;
@@ -408,6 +411,7 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
     // context invalid (the next call uploads again) and retires every scene-derived cache
     // (candidate lists, tile costs) by bumping the generation.
     ctx->valid = false;
+    ctx->normal_rn = false;
     ctx->scene_gen++;
     if (count > ctx->capacity || ctx->d_geom == nullptr) {
         uint32_t cap = ctx->capacity ? ctx->capacity : 64u;
@@ -456,8 +460,22 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
         e = hipMemcpyAsync(ctx->d_sph, spheres, count * sizeof(rt_sphere),
                            hipMemcpyHostToDevice, stream);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(sphere records)");
+        // the device's refined reciprocal of every radius against the IEEE division
+        // (RT_NORMAL_RN=0 in the environment turns the Markstein normal off: a test switch)
+        if (!ctx->d_flag) {
+            e = hipMalloc(&ctx->d_flag, sizeof(uint32_t));
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc(check flag)");
+        }
+        uint32_t bad = 1u;
+        e = hipMemsetAsync(ctx->d_flag, 0, sizeof(uint32_t), stream);
+        if (e == hipSuccess) e = rtk::launch_rcp_check(ctx->d_sph, count, ctx->d_flag, stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(&bad, ctx->d_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream);
+        if (e != hipSuccess) return hip_fail(e, "radius reciprocal check");
         e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+        const char* env = std::getenv("RT_NORMAL_RN");
+        ctx->normal_rn = bad == 0u && !(env && env[0] == '0');
     }
     double bound = 0.0;
     bool radii_ok = true;
@@ -931,6 +949,7 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
     p.width = w;
     p.height = h;
     p.count = count;
+    p.normal_rn = ctx->normal_rn ? 1u : 0u;
     p.band_first = rank;
     p.band_step = nranks;
     p.local_bands = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
@@ -1056,6 +1075,7 @@ void note_launch(rt_ctx* ctx, const rtk::TraceParams& p, int kernel, uint32_t fr
     ctx->last.submit = aql ? RT_SUBMIT_AQL : RT_SUBMIT_HIP;
     ctx->last.frames += frames;
     ctx->last.max_frames_per_launch = std::max(ctx->last.max_frames_per_launch, frames);
+    ctx->last.normal_rn = p.normal_rn;
     ctx->last.kernel = kernel != rtk::kTraceBounce ? kernel
                        : p.compact == 3u             ? RT_KERNEL_BOUNCE_SPLIT
                                                      : RT_KERNEL_BOUNCE + (int)p.compact;
@@ -1148,7 +1168,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         return s;
     const float4* src = reinterpret_cast<const float4*>(in);
     float4* dst = reinterpret_cast<float4*>(out);
-    ctx->last = {0, 0, 0, -1, 0};
+    ctx->last = {0, 0, 0, -1, 0, 0, 0};
     for (uint32_t f0 = 0; f0 < frames; f0 += rtk::kMaxFramesPerLaunch) {
         const uint32_t nf = std::min<uint32_t>(frames - f0, rtk::kMaxFramesPerLaunch);
         p.in = src;
@@ -1246,6 +1266,7 @@ rt_status rt_destroy(rt_ctx* ctx) {
         if (ctx->d_geom || ctx->d_sph || ctx->cand) (void)hipDeviceSynchronize();
         (void)hipFree(ctx->d_geom);
         (void)hipFree(ctx->d_sph);
+        (void)hipFree(ctx->d_flag);
         (void)hipFree(ctx->d_srgb);
         (void)hipFree(ctx->d_hx);
         (void)hipFree(ctx->tile_cost);
@@ -1444,7 +1465,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
     // instances run one frame per launch.
     const uint32_t per = frames_per_launch_for(ctx, p);
     int cur = 0;
-    ctx->last = {0, 0, 0, -1, 0, 0};
+    ctx->last = {0, 0, 0, -1, 0, 0, 0};
     // What the call has in flight beside the caller's stream, closed on every exit path (an
     // error return included): an AQL segment still being packed is dropped (nothing of it has
     // been submitted), and the context's aux streams are joined back into `stream`, so the

@@ -789,6 +789,16 @@ __device__ __forceinline__ v3 normalize_w(v3 v) {
 // f, so the scatter step's random numbers (pixel-independent, see TraceParams::hint_n)
 // come from the host-computed hint_rs table instead of three hashes, a sqrt and a sincos
 // per lane.
+// The hit normal's (p - C) / R (wgsl:209) on div_core's domain (the callers check it),
+// y = rcp_refined(R).  rn (wave-uniform, TraceParams::normal_rn): y is RN32(1 / R) — checked
+// for every radius of the scene on the device at upload (rt_rcp_check_kernel) — so one
+// Markstein step per component is the IEEE quotient (div_rn: the numerators >= 2^-100, R in
+// [2^-20, 2^20] and |p - C| <= 2^43 keep the quotients normal); otherwise div_core's two.
+__device__ __forceinline__ v3 normal_div(v3 rel, float r, float y, bool rn) {
+    if (rn) return mk(div_rn(rel.x, r, y), div_rn(rel.y, r, y), div_rn(rel.z, r, y));
+    return mk(div_core(rel.x, r, y), div_core(rel.y, r, y), div_core(rel.z, r, y));
+}
+
 template <int kScan>
 __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uint32_t ncand,
                                         uint32_t depth, v3 o, v3 d, uint32_t seed, bool live,
@@ -844,8 +854,7 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
             rt_ballot(min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z)) <
                      kBits2m100) == 0ull) {
             const float y = rcp_refined(pr.w);
-            outward = mk(div_core(rel.x, pr.w, y), div_core(rel.y, pr.w, y),
-                         div_core(rel.z, pr.w, y));
+            outward = normal_div(rel, pr.w, y, p.normal_rn != 0u);
         } else {
             outward = divs(rel, pr.w);
         }
@@ -1271,7 +1280,8 @@ struct SingleParams {
     uint32_t seed_b;       // B = u32(random_seed * 2^32) (wgsl:311, 353)
     uint32_t hy_off;       // hash(y * 51) table offset in the hx buffer
     float rcp_hint;        // RN32(1 / f32(n_hint + 1)) (acc_rn)
-    uint32_t reserved[5];  // (the fields after keep round 4's offsets)
+    uint32_t normal_rn;    // TraceParams::normal_rn
+    uint32_t reserved[4];  // (the fields after keep round 4's offsets)
     // local bands of a launch in raster order (no a_order): lband = first + blockIdx.y *
     // step, first | step << 16 — one of the update's concurrent parts (launch_single)
     uint32_t lbands;
@@ -1356,16 +1366,16 @@ constexpr int kSingleDisk = 3;
 // sets the scattered direction and attenuation, or black (metal absorbed).  r_sb / ruv are
 // the scatter's random numbers.  Lanes with !hit compute garbage that the caller drops.
 __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, v3 d,
-                                          float r_sb, v3 ruv, bool hit, uint64_t hm, v3& nd,
-                                          v3& att, bool& black, bool& took_other, float& ndd) {
+                                          float r_sb, v3 ruv, bool hit, uint64_t hm,
+                                          bool normal_rn, v3& nd, v3& att, bool& black,
+                                          bool& took_other, float& ndd) {
     const v3 hp = fmas(t, d, o);
     const v3 rel = sub(hp, mk(pr.x, pr.y, pr.z));
     v3 outward;                                                   // wgsl:209
     const uint32_t rel_min = min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z));
     if ((mask_ult(rel_min, kBits2m100) & hm) == 0ull) {
         const float y = rcp_refined(pr.w);
-        outward = mk(div_core(rel.x, pr.w, y), div_core(rel.y, pr.w, y),
-                     div_core(rel.z, pr.w, y));
+        outward = normal_div(rel, pr.w, y, normal_rn);
     } else {
         outward = divs(rel, pr.w);
     }
@@ -1579,8 +1589,8 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
                 v3 nd, att;
                 bool blk_s, other_s;
                 float ndd;
-                shade_hit(pr[s], mat[s], tmax[s], o[s], d[s], r_sb, ruv, hit[s], hm[s], nd,
-                          att, blk_s, other_s, ndd);
+                shade_hit(pr[s], mat[s], tmax[s], o[s], d[s], r_sb, ruv, hit[s], hm[s],
+                          p.normal_rn != 0u, nd, att, blk_s, other_s, ndd);
                 any_other[s] = other_s;
                 if (hm[s] == live_m[s]) {
                     // every live lane hit (a tile inside a sphere's image): no selects
@@ -1611,6 +1621,11 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
     }
     SST_V(5, col[S - 1].x);
 }
+
+// The hinted path's count check as a range test on the loaded f32 count (A/B switch)
+#ifndef RT_PEND_RANGE
+#define RT_PEND_RANGE 0
+#endif
 
 // kReset: the frame resets the accumulator (camera_has_moved > 0.5, wgsl:345-350) — a
 // separate kernel (rt_single_reset_kernel), so that the steady-state kernel carries no
@@ -1756,9 +1771,20 @@ __device__ __forceinline__ void single_body(
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s) {
             c[s] = kReset ? mk(0.0f, 0.0f, 0.0f) : mk(acc[s].x, acc[s].y, acc[s].z);
-            n[s] = kReset ? 0u : f2u(acc[s].w);                   // wgsl:339-350
-            pending[s] = tc[s].valid && n[s] != ng;               // a foreign count
-            if (!kReset) pend_m |= mask_ne(n[s], ng) & valid_m[s];
+            if (RT_PEND_RANGE && !kReset && ng < (1u << 24)) {
+                // u32(acc.w) == ng (wgsl:339-341) holds for acc.w in [ng, ng + 1); two
+                // compares against wave-uniform bounds instead of the per-lane conversion.
+                // NaN, negative and other counts fall outside and are traced again below
+                // with their own count (u32(acc.w) there), as any foreign count is
+                const bool same = acc[s].w >= (float)ng && acc[s].w < (float)(ng + 1u);
+                n[s] = ng;
+                pending[s] = tc[s].valid && !same;
+                pend_m |= ~rt_ballot(same) & valid_m[s];
+            } else {
+                n[s] = kReset ? 0u : f2u(acc[s].w);               // wgsl:339-350
+                pending[s] = tc[s].valid && n[s] != ng;           // a foreign count
+                if (!kReset) pend_m |= mask_ne(n[s], ng) & valid_m[s];
+            }
             any_pending = any_pending || pending[s];
             if (ng < spp) {                                       // wgsl:352-357
                 const v3 num = sub(col[s], c[s]);
@@ -2859,6 +2885,23 @@ __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cn
     atomicAdd(&cnt[4], runs);
 }
 
+// TraceParams::normal_rn: is rcp_refined(R) the correctly rounded 1 / R for every radius?
+// (one thread per sphere at upload; a vector atomic OR on any miss)
+__global__ __launch_bounds__(256) void rt_rcp_check_kernel(const float4* sph, uint32_t count,
+                                                           uint32_t* bad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const float r = sph[2u * i].w;
+    if (__float_as_uint(rcp_refined(r)) != __float_as_uint(1.0f / r)) atomicOr(bad, 1u);
+}
+hipError_t launch_rcp_check(const float4* sph, uint32_t count, uint32_t* bad,
+                            hipStream_t stream) {
+    if (count == 0u) return hipSuccess;
+    hipLaunchKernelGGL(rt_rcp_check_kernel, dim3((count + 255u) / 256u), dim3(256), 0, stream,
+                       sph, count, bad);
+    return hipGetLastError();
+}
+
 hipError_t launch_selftest(unsigned long long* cnt, uint64_t n_rand, hipStream_t stream) {
     hipLaunchKernelGGL(rt_selftest_kernel, dim3(8192), dim3(256), 0, stream, cnt, n_rand);
     return hipGetLastError();
@@ -3007,6 +3050,7 @@ static bool single_args(const TraceParams& p, SingleArgs& args, dim3& grid) {
     q.seed_b = p.seed_b[0];
     q.hy_off = (uint32_t)(p.hy - p.hx);
     q.rcp_hint = p.hint_rcp[0];
+    q.normal_rn = p.normal_rn;
     q.rs = p.hint_rs[0];
     for (int i = 0; i < 3; ++i) {
         q.center[i] = p.center[i];

@@ -143,7 +143,8 @@ _SIGS = {
 class LaunchInfoC(ctypes.Structure):
     """rt_launch_info (rt_abi.h)."""
     _fields_ = [("launches", U32), ("frames", U32), ("max_frames_per_launch", U32),
-                ("kernel", ctypes.c_int32), ("queues", U32), ("submit", U32)]
+                ("kernel", ctypes.c_int32), ("queues", U32), ("submit", U32),
+                ("normal_rn", U32)]
 
 _lib = None
 

@@ -158,7 +158,7 @@ typedef struct rt_ctx rt_ctx;
 
 /* Version / introspection ------------------------------------------------------------ */
 RT_API uint32_t rt_abi_version(void); /* RT_ABI_VERSION */
-#define RT_ABI_VERSION 4u
+#define RT_ABI_VERSION 5u
 /* Text of the last error on this thread (never NULL). */
 RT_API const char* rt_last_error(void);
 /* Trace-kernel instances (rt_launch_info.kernel) and their names as rocprofv3 lists them
@@ -199,6 +199,9 @@ typedef struct rt_launch_info {
     int32_t kernel;
     uint32_t queues;
     uint32_t submit;
+    /* 1: the hit normal's division ran as one Markstein step per component (every radius's
+     * device reciprocal checked correctly rounded at upload); 0: two correction steps */
+    uint32_t normal_rn;
 } rt_launch_info;
 RT_API rt_status rt_last_launch_info(const rt_ctx* ctx, rt_launch_info* out);
 /* Diagnostic: the per-tile candidate lists of camera rays the context built last (culled

@@ -194,6 +194,37 @@ def test_bench_dispatch_chain_matches_fixture(rt, cfg, single, submit):
         p.close()
 
 
+@pytest.mark.parametrize("cfg", ["k2", "k3"])
+@pytest.mark.parametrize("normal_rn", ["on", "off"])
+def test_normal_markstein_matches_fixture(rt, cfg, normal_rn, monkeypatch):
+    """The hit normal's (p - C) / R (wgsl:209) as one Markstein step per component when the
+    device's refined reciprocal of every radius is the correctly rounded 1 / R (checked at
+    upload: TraceParams::normal_rn, reported as last_launch_info()["normal_rn"]), or with
+    div_core's two correction steps (RT_NORMAL_RN=0): the 5 + 20 frames of the bench fixture
+    as one-frame launches and as one frame chain, against the oracle's sampled pixels."""
+    if normal_rn == "off":
+        monkeypatch.setenv("RT_NORMAL_RN", "0")
+    g = load_golden(f"bench_{cfg}.npz")
+    w, h = int(g["width"]), int(g["height"])
+    cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
+    k = list(g["frame_counts"]).index(25)
+    for fpl in (1, 0):
+        p = rt.ComputeShaderPipeline(0)
+        p.set_frames_per_launch(fpl)
+        try:
+            a, b = p.new_image(w, h), p.new_image(w, h)
+            if p.update_frames(a, b, w, h, cam, sc, g["seeds"][:5]) == 1:
+                a, b = b, a
+            newest = p.update_frames(a, b, w, h, cam.with_fields(camera_has_moved=0.0), sc,
+                                     g["seeds"][5:25])
+            info = p.last_launch_info()
+            assert info["normal_rn"] == (1 if normal_rn == "on" else 0), info
+            img = host(b if newest == 1 else a)
+            assert_same(img[g["py"], g["px"]], g["pixels"][k])
+        finally:
+            p.close()
+
+
 @pytest.mark.parametrize("order", ["auto", "off"])
 @pytest.mark.parametrize("single", ["auto", "one"])
 @pytest.mark.parametrize("submit", ["auto", "aql"])
