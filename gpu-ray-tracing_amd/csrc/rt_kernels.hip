@@ -1027,6 +1027,9 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 // Called only when every valid pixel's loaded count is the hinted one (rt_trace_kernel).
 // Waves per tile: 2 (kTraceListPair) or 4 (kTraceListQuad).  K3 per frame, whole image on
 // one GPU: 16.8 / 18.8 us; 8-rank share: 3.13 / 2.95 us (`profiles/r01_rank_sim_groups_k3.txt`).
+// Round 5: one more wave per tile that only accumulates and stores, so that every group's
+// samplers all trace, measured slower at every size (8-rank share 2.91 against 2.54 us per
+// step, whole image 17.2 against 14.6; profiles/r05/r05j/).
 template <int kScan>
 constexpr uint32_t frame_group() {
     return kScan == kTraceListQuad ? 4u : 2u;
@@ -1622,11 +1625,6 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
     SST_V(5, col[S - 1].x);
 }
 
-// The hinted path's count check as a range test on the loaded f32 count (A/B switch)
-#ifndef RT_PEND_RANGE
-#define RT_PEND_RANGE 0
-#endif
-
 // kReset: the frame resets the accumulator (camera_has_moved > 0.5, wgsl:345-350) — a
 // separate kernel (rt_single_reset_kernel), so that the steady-state kernel carries no
 // per-pixel selects between the loaded and the zero accumulator, and the reset kernel no
@@ -1771,20 +1769,9 @@ __device__ __forceinline__ void single_body(
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s) {
             c[s] = kReset ? mk(0.0f, 0.0f, 0.0f) : mk(acc[s].x, acc[s].y, acc[s].z);
-            if (RT_PEND_RANGE && !kReset && ng < (1u << 24)) {
-                // u32(acc.w) == ng (wgsl:339-341) holds for acc.w in [ng, ng + 1); two
-                // compares against wave-uniform bounds instead of the per-lane conversion.
-                // NaN, negative and other counts fall outside and are traced again below
-                // with their own count (u32(acc.w) there), as any foreign count is
-                const bool same = acc[s].w >= (float)ng && acc[s].w < (float)(ng + 1u);
-                n[s] = ng;
-                pending[s] = tc[s].valid && !same;
-                pend_m |= ~rt_ballot(same) & valid_m[s];
-            } else {
-                n[s] = kReset ? 0u : f2u(acc[s].w);               // wgsl:339-350
-                pending[s] = tc[s].valid && n[s] != ng;           // a foreign count
-                if (!kReset) pend_m |= mask_ne(n[s], ng) & valid_m[s];
-            }
+            n[s] = kReset ? 0u : f2u(acc[s].w);                   // wgsl:339-350
+            pending[s] = tc[s].valid && n[s] != ng;               // a foreign count
+            if (!kReset) pend_m |= mask_ne(n[s], ng) & valid_m[s];
             any_pending = any_pending || pending[s];
             if (ng < spp) {                                       // wgsl:352-357
                 const v3 num = sub(col[s], c[s]);

@@ -51,3 +51,25 @@ for r in 1 2 3; do
     done
   done
 done
+# frame groups at small shares: two (on) against four (quad, AUTO's choice there) waves per tile
+for r in 1 2; do
+  for n in 8 4; do
+    for m in quad on; do
+      timeout -k 10 120 python tools/share_region.py $n 0 15 20 $m > $O/share_${m}_n${n}_$r.json 2> $O/share_${m}_n${n}_$r.err || { tail $O/share_${m}_n${n}_$r.err; exit 1; }
+      python -c "import json; d=json.load(open('$O/share_${m}_n${n}_$r.json')); print('$m', 'n$n', d['kernel'], 'wall', d['wall_us_per_step_q1_med_q3'], 'ev', d['events_us_per_step_q1_med_q3'])"
+    done
+  done
+done
+# frame groups with a dedicated accumulating wave (librt_hip_gacc.so, -DRT_GROUP_ACC=1: every
+# group's samplers all trace, one more wave accumulates and stores) against the tree's build
+RT_HIP_LIB=$V/librt_hip_gacc.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread \
+  -k "chain or pair or share or frames" > $O/pytest_gpu_gacc.log 2>&1 || { echo "pytest gacc failed"; tail -30 $O/pytest_gpu_gacc.log; exit 1; }
+tail -1 $O/pytest_gpu_gacc.log
+for r in 1 2; do
+  for n in 8 4 1; do
+    for lib in cur gacc; do
+      RT_HIP_LIB=$V/librt_hip_$lib.so timeout -k 10 120 python tools/share_region.py $n 0 15 20 > $O/share_${lib}_n${n}_$r.json 2> $O/share_${lib}_n${n}_$r.err || { tail $O/share_${lib}_n${n}_$r.err; exit 1; }
+      python -c "import json; d=json.load(open('$O/share_${lib}_n${n}_$r.json')); print('$lib', 'n$n', d['kernel'], 'wall', d['wall_us_per_step_q1_med_q3'], 'ev', d['events_us_per_step_q1_med_q3'])"
+    done
+  done
+done

@@ -7,7 +7,7 @@ step (median and quartiles), and, for the last repetition, `timeline_host` stamp
 so that tools/timeline.py can place the call on a rocprofv3 kernel trace of this process:
     rocprofv3 --kernel-trace -f csv -d DIR -- python3 tools/share_region.py 8 0 > line.json
     python tools/timeline.py DIR line.json
-usage: python tools/share_region.py [N] [rank] [R] [frames]"""
+usage: python tools/share_region.py [N] [rank] [R] [frames] [pairs: auto|on|quad|off]"""
 import json
 import statistics as st
 import sys
@@ -25,6 +25,7 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 RANK = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 R = int(sys.argv[3]) if len(sys.argv) > 3 else 15
 F = int(sys.argv[4]) if len(sys.argv) > 4 else 20
+PAIRS = sys.argv[5] if len(sys.argv) > 5 else "auto"
 w, h = 1920, 1080
 sc = rt.SphereCollection.generate(rt.SCENE_N, 500, 1)
 seeds = rt.frame_seeds(0x5EED, 5 + F)
@@ -35,6 +36,7 @@ pipe = rt.ComputeShaderPipeline(0)
 pipe.set_spheres(sc)
 pipe.set_frames_per_launch(0)
 pipe.set_frame_images("every")
+pipe.set_frame_pairs(PAIRS)
 stream = torch.cuda.current_stream()
 r = StripeRenderer(pipe, w, h, RANK, N)
 scratch = StripeRenderer(pipe, w, h, RANK, N)
@@ -71,7 +73,7 @@ def q(v):
     return [round(s[len(s) // 4], 2), round(st.median(s), 2), round(s[(3 * len(s)) // 4], 2)]
 
 
-print(json.dumps({"share": f"rank {RANK} of {N}", "steps": F, "reps": R,
+print(json.dumps({"share": f"rank {RANK} of {N}", "steps": F, "reps": R, "pairs": PAIRS,
                   "kernel": info["kernel_name"], "launches": info["launches"],
                   "wall_us_per_step_q1_med_q3": q(wall), "events_us_per_step_q1_med_q3": q(ev),
                   "ms_per_step": round(st.median(wall) / 1e3, 5),
