@@ -19,6 +19,19 @@
 
 #include "rt_abi.h"
 #include "rt_device.h"
+#ifdef RT_CALL_STAMPS
+// (diagnostic builds: host time stamps of rt_update_frames' phases, one stderr line per call)
+#include <chrono>
+static thread_local unsigned long long g_call_stamp[8];
+static void call_stamp(int i) {
+    g_call_stamp[i] = (unsigned long long)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                          std::chrono::steady_clock::now().time_since_epoch())
+                          .count();
+}
+#define CALL_STAMP(i) call_stamp(i)
+#else
+#define CALL_STAMP(i) ((void)0)
+#endif
 #include "rt_internal.h"
 #include "rt_kernels.h"
 
@@ -1445,9 +1458,11 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
                            uint32_t rank, uint32_t nranks, const rt_scene_camera* cam,
                            const rt_sphere* spheres, uint32_t count, uint32_t frames,
                            const float* seeds, void* stream_v, int* out_newest) {
+    CALL_STAMP(0);
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     if (image_a == image_b) return fail(RT_ERR_INVALID_ARGUMENT, "image_a and image_b alias");
     DeviceGuard guard(ctx->device);
+    CALL_STAMP(1);
     if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
     // an earlier call's AQL segment that failed is reported here, once
     if (rt_status s = chain_report(ctx)) return s;
@@ -1456,6 +1471,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
     if (rt_status s = prepare(ctx, image_a, image_b, w, h, rank, nranks, cam, spheres, count,
                               seeds, stream, p))
         return s;
+    CALL_STAMP(2);
     float4* img[2] = {reinterpret_cast<float4*>(image_a), reinterpret_cast<float4*>(image_b)};
     // Frames per launch (frames_per_launch_for).  Fusing removes the per-launch fill, tail
     // and kernel boundary (≈ 6 µs of a 30-µs K3 frame): the camera-ray-only instances
@@ -1545,9 +1561,11 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
             fl.aux_live = 0;
             forked = false;
         }
+        CALL_STAMP(3);
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         if (rt_status s = plan_wg_order(ctx, p, kernel, stream)) return s;
         if (rt_status s = plan_split(ctx, p, kernel, stream)) return s;
+        CALL_STAMP(4);
         if (aql) {
             // frame f of part k is a packet on the chain's queue k, after part k's frame f - 1
             if (!fl.seg_open) {
@@ -1595,6 +1613,7 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
             hipError_t e = rtk::launch_trace(p, kernel, stream);
             if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         }
+        CALL_STAMP(5);
         finish_tile_order(ctx, p);
         note_launch(ctx, p, kernel, nf, parts, aql);
         // frame f of the launch wrote img[(cur + 1 + f) % 2]
@@ -1618,6 +1637,13 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         if (rt_status s = join_aux(ctx, n, stream)) return s;
     }
     if (out_newest) *out_newest = cur;
+    CALL_STAMP(6);
+#ifdef RT_CALL_STAMPS
+    std::fprintf(stderr, "RT_CALL_STAMPS %u %llu %llu %llu %llu %llu %llu\n", frames,
+                 g_call_stamp[1] - g_call_stamp[0], g_call_stamp[2] - g_call_stamp[0],
+                 g_call_stamp[3] - g_call_stamp[0], g_call_stamp[4] - g_call_stamp[0],
+                 g_call_stamp[5] - g_call_stamp[0], g_call_stamp[6] - g_call_stamp[0]);
+#endif
     return RT_OK;
 }
 

@@ -29,7 +29,8 @@ W = int(sys.argv[1]) if len(sys.argv) > 1 else 1920
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 1080
 NS = int(sys.argv[3]) if len(sys.argv) > 3 else 500
 
-sc = rt.SphereCollection.generate(rt.SCENE_N, NS, 1)
+KIND = rt.SCENE_THREE if NS == 3 else rt.SCENE_N
+sc = rt.SphereCollection.generate(KIND, NS, 1)
 sph = np.frombuffer(sc.as_bytes(), dtype=np.float32).reshape(-1, 8).astype(np.float64)
 cam = rt.SceneCamera.from_settings(rt.CameraSettings(max_depth=1, samples_per_pixel=65536),
                                    W, H, 0.5).to_c()

@@ -30,5 +30,5 @@ RT_TIMELINE=1 timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $O/tl_g20 -o 
   > $O/tl_g20_line.json 2> $O/tl_g20.err || { echo "rocprof g20 failed"; tail $O/tl_g20.err; exit 1; }
 python tools/timeline.py $O/tl_g20 $O/tl_g20_line.json > $O/timeline_g20.json || exit 1
 python -c "import json; d=json.load(open('$O/timeline_g20.json')); [d.pop(k) for k in ('hip_calls','kernels')]; print('g20', json.dumps(d))"
-PMC_ROUND=r05 QUEUES=0 bash tools/pmc_bench.sh ${TAG}_pmc "K3" || exit 1
+PMC_ROUND=r05 QUEUES=0 bash tools/pmc_bench.sh ${TAG}_pmc "K3 K2" || exit 1
 echo pmc done
