@@ -899,8 +899,10 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
     float uy;
     if (fast_core<kScan>(4) &&
         rt_ballot(__float_as_uint(dd) - kBits2m20 >= kBits2p40 - kBits2m20) == 0ull) {
-        const float len = sqrt_core(dd);
-        uy = div_core(d.y, len, rcp_refined(len));
+        // (|d| and its reciprocal from one rsq, as the one-frame kernel's sky: no v_rcp)
+        float y;
+        const float len = sqrt_core_rcp(dd, y);
+        uy = div_core(d.y, len, y);
     } else {
         uy = d.y / sqrtf(dd);
     }
@@ -1029,7 +1031,9 @@ __device__ __forceinline__ float4 trace_pixel(const TraceParams& p, const Cam& c
 // one GPU: 16.8 / 18.8 us; 8-rank share: 3.13 / 2.95 us (`profiles/r01_rank_sim_groups_k3.txt`).
 // Round 5: one more wave per tile that only accumulates and stores, so that every group's
 // samplers all trace, measured slower at every size (8-rank share 2.91 against 2.54 us per
-// step, whole image 17.2 against 14.6; profiles/r05/r05j/).
+// step, whole image 17.2 against 14.6; profiles/r05/r05j/); so did tracing each frame with
+// the one-frame kernel's sample (single_sample<1>, records from LDS or by scalar loads:
+// profiles/r05/r05h/, r05m/).
 template <int kScan>
 constexpr uint32_t frame_group() {
     return kScan == kTraceListQuad ? 4u : 2u;

@@ -26,3 +26,19 @@ for r in 1 2; do
   done
 done
 unset HSA_ENABLE_INTERRUPT
+# --- session n (tools/sessions/gpu_r05n.sh) in the same call ---
+V=gpu-ray-tracing_amd/build/variants
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+  > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+RT_HIP_LIB=$V/librt_hip_gs0.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread \
+  -k "chain or pair or share or frames or normal" > $O/pytest_gpu_gs0.log 2>&1 || { echo "pytest gs0 failed"; tail -30 $O/pytest_gpu_gs0.log; exit 1; }
+tail -1 $O/pytest_gpu_gs0.log
+for r in 1 2; do
+  for n in 8 4 1; do
+    for lib in cur gs0 sky; do
+      RT_HIP_LIB=$V/librt_hip_$lib.so timeout -k 10 120 python tools/share_region.py $n 0 15 20 > $O/share_${lib}_n${n}_$r.json 2> $O/share_${lib}_n${n}_$r.err || { tail $O/share_${lib}_n${n}_$r.err; exit 1; }
+      python -c "import json; d=json.load(open('$O/share_${lib}_n${n}_$r.json')); print('$lib', 'n$n', d['kernel'], 'wall', d['wall_us_per_step_q1_med_q3'], 'ev', d['events_us_per_step_q1_med_q3'])"
+    done
+  done
+done
