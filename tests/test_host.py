@@ -215,6 +215,36 @@ def test_header_layout_locks_compile_in_c(tmp_path):
     assert ok.returncode == 0, ok.stderr
 
 
+def test_ctypes_mirrors_match_the_c_layouts(rt, tmp_path):
+    """Every struct the Python mirror passes through the C ABI (gpu_ray_tracing/_lib.py) has
+    the size and field offsets gcc gives the header's declaration — rt_scene_camera,
+    rt_sphere, rt_camera_settings and rt_launch_info (ABI 5 appended normal_rn)."""
+    L = rt._lib
+    mirrors = {"rt_scene_camera": L.SceneCameraC, "rt_sphere": L.SphereC,
+               "rt_camera_settings": L.CameraSettingsC, "rt_launch_info": L.LaunchInfoC}
+    lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "rt_abi.h"',
+             'int main(void) {']
+    for cname, py in mirrors.items():
+        lines.append(f'    printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'    printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines += ['    return 0;', '}']
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    cc = subprocess.run(["gcc", "-std=c11", "-I", str(HEADER.parent), str(src), "-o", str(exe)],
+                        capture_output=True, text=True)
+    assert cc.returncode == 0, cc.stderr
+    got = {}
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        cname, key, val = line.split()
+        got[(cname, key)] = int(val)
+    for cname, py in mirrors.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
+
+
 def test_bound_update_frames_passes_the_same_arguments(rt, monkeypatch):
     """bind_update_frames (what StripeRenderer.frames issues) hands rt_update_frames the
     same arguments as ComputeShaderPipeline.update_frames, reports the newest image the same
