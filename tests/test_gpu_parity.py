@@ -69,6 +69,30 @@ def test_update_matches_oracle(rt, oracle, pipe, scene, w, h, depth, defocus):
     assert_same(host(b), want)
 
 
+@pytest.mark.parametrize("seed", [3, 4])
+def test_random_radii_normal_paths_match_oracle(rt, oracle, pipe, seed):
+    """The hit normal's division on scenes of random radii (the seeded scene's records with
+    every radius drawn from [0.05, 4) bits at random): whether or not the upload's device
+    check finds every radius's refined reciprocal correctly rounded (last_launch_info's
+    normal_rn, one Markstein step per component, or div_core's two), the frames match the
+    oracle; depth 1 (the camera-ray-only instances) and 3."""
+    base = np.array(rt.create_default_spheres(seed).spheres, np.float32).reshape(-1, 8)
+    rng = np.random.default_rng(seed)
+    base[:, 3] = rng.uniform(0.05, 4.0, len(base)).astype(np.float32)
+    sc = rt.SphereCollection(base)
+    w, h = 72, 40
+    seen = set()
+    for depth in (1, 3):
+        cam = camera(rt, w, h, depth=depth, seed=0.40625)
+        inp = np.zeros((h, w, 4), np.float32)
+        a, b = to_dev(inp), pipe.new_image(w, h)
+        pipe.update(a, b, w, h, cam, sc)
+        seen.add(pipe.last_launch_info()["normal_rn"])
+        want, _ = oracle.update(inp, cam.blob, sc.spheres)
+        assert_same(host(b), want)
+    assert seen <= {0, 1}
+
+
 def test_update_accumulates_from_state(rt, oracle, pipe):
     """Non-zero input accumulator, no reset; samples capped at spp; reset on move."""
     w, h = 48, 40
