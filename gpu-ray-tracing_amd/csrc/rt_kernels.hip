@@ -422,14 +422,21 @@ __device__ __forceinline__ bool wave_cone(v3 o, v3 d, bool live, Cone& k) {
 }
 
 // True when sphere record g = (center, r*r) provably misses every ray of the cone.
+// lhs bounds the distance of every ray line from C from below (less 1e-5 of the magnitudes
+// for its own f32 evaluation); the computed discriminant is certainly negative when
+// dist^2 > R^2 + E, E = eps (16 |oc|^2 + 6 R^2), and m^2 >= 6.25e-6 (|oc|^2 +
+// R^2) >= E, so the test is dist > sqrt(R^2 + m^2) — round 4 used R + m, which is larger by
+// up to m, about a fifth of a small sphere's radius at the K3 camera's distances (K3's
+// candidate lists 2.68 -> 2.22 entries per tile, profiles/r05/r05t/).
 __device__ __forceinline__ bool cone_misses(const Cone& k, float4 g) {
     const v3 v = mk(g.x - k.apex.x, g.y - k.apex.y, g.z - k.apex.z);
     const float t = dot(v, k.axis);
     const float p = __builtin_amdgcn_sqrtf(fmaxf(fmaf(-t, t, dot(v, v)), 0.0f));
     const float at = fabsf(t), R = __builtin_amdgcn_sqrtf(g.w) * 1.0001f;
-    const float lhs = fmaf(p, k.cos_t, -at * k.sin_t) - k.r_o;
-    const float m = 2.5e-3f * (at + p + k.r_o + k.d_max + R);
-    return lhs > R + m;                                   // NaN anywhere -> keep
+    const float mag = at + p + k.r_o;
+    const float lhs = fmaf(p, k.cos_t, -at * k.sin_t) - k.r_o - 1e-5f * mag;
+    const float m = 2.5e-3f * (mag + k.d_max + R);
+    return lhs > R && lhs * lhs > fmaf(R, R, m * m) * 1.0001f;   // NaN anywhere -> keep
 }
 
 // Scan records staged in LDS by the workgroup (culled scan, lists up to kLdsMaxRecords).
