@@ -1502,7 +1502,7 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
     }
     if (p.depth != 0u && !(RT_SKO & 2)) {                         // wgsl:264
         // sphere_list_hit over each tile's list, the tiles' chunks interleaved
-        float tmax[S], a[S], ya[S];
+        float tmax[S], a[S];
         int idx[S];
         bool joint = true;
         uint32_t m = 0;
@@ -1511,7 +1511,6 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
             tmax[s] = 0x1.05ed2ep+118f;                           // 3.4e35 (wgsl:266)
             idx[s] = -1;
             a[s] = ddsky[s];
-            ya[s] = rcp_refined(a[s]);
             joint = joint && ncand[s] != kCandNone;
             m = max(m, ncand[s]);
         }
@@ -1540,7 +1539,9 @@ __device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& 
 #pragma unroll
                         for (int k = 0; k < K; ++k)
                             if (i + k < ncand[s])
-                                consider_fast(dd[s][k], hh[s][k], a[s], ya[s], i + k, tmax[s],
+                                // (1 / a only where some discriminant is not negative:
+                                // waves without candidates, the sky's, skip the v_rcp)
+                                consider_fast(dd[s][k], hh[s][k], a[s], rcp_refined(a[s]), i + k, tmax[s],
                                               idx[s]);
                 }
             }
