@@ -265,17 +265,19 @@ uint32_t frames_per_launch_for(const rt_ctx* ctx, const rtk::TraceParams& p) {
 // upload of at least kGridMinSpheres spheres whose |C| + |R| stay within 2^40 (so no f32
 // intermediate of the root test overflows for the rays that may use the grid).  Small:
 // |R| <= 4x the median radius; the others (the ground, the few large spheres) go to the
-// big list that every ray tests.  Cells are about two small spheres' worth of the centres'
+// big list that every ray tests.  Cells are about one small sphere's worth of the centres'
 // bounding area, at most kGridMaxDim per axis.  A ray may walk the grid when
 // 2.5e-3 (|o - c| + reach) <= m (c, reach: centre and radius of the small spheres' extent),
 // which bounds the f32 discriminant margin of every small sphere by m; each sphere is then
-// registered in every cell within |R| + m + e of its centre, e bounding the f32 error of
+// registered in every cell within sqrt(R^2 + m^2) + e of its centre, e bounding the f32 error of
 // the walk's cell positions: (steps + 16) x 8 eps x the largest coordinate magnitude it
 // handles, plus 1e-3 of a cell.  Rays further out, with |d|^2 outside [2^-20, 2^20] or
 // non-finite, keep the exhaustive scan.
 constexpr uint32_t kGridMinSpheres = 64;
+// small spheres' centres per cell (round 5, with the sqrt(R^2 + m^2) registration: 1.0 —
+// K5 436 against 445 us per fused frame at 2.0, profiles/r05/r05ab/, r05ac/)
 #ifndef RT_GRID_PER_CELL
-#define RT_GRID_PER_CELL 2.0
+#define RT_GRID_PER_CELL 1.0
 #endif
 // (A/B) round 4's registration pad, R + m
 #ifndef RT_GRID_PAD_ROUND4
