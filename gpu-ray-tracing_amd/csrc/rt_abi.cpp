@@ -83,7 +83,7 @@ struct rt_ctx {
     uint32_t cost_frames = 0;       // frames of the launch that measured it
     uint64_t order_gen = ~0ull;     // cand_gen tile_order was derived for
     uint32_t order_frames = 0;      // frames of the measurement it came from
-    bool cost_groups = false;       // tile_cost/tile_order count bounce workgroups, not tiles
+    uint32_t cost_group = 1;        // tiles per tile_cost/tile_order unit (bounce workgroups, pairs)
     int tile_order_mode = RT_TILE_ORDER_AUTO;
     float* d_srgb = nullptr;  // rt_srgb_thresholds table on the device (256 floats)
     // hash(x*73) for x < hx_len (= rtk::hy_offset(width)), then hash(y*51) for y < hy_len
@@ -601,12 +601,16 @@ rt_status plan_tile_order(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStrea
     if (!(rtk::trace_ordered(kernel) || bounce) || ctx->tile_order_mode == RT_TILE_ORDER_OFF ||
         p.cand_k == 0 || p.frames < 2)
         return RT_OK;
-    // scheduling units: 8x8 tiles, or the compacting bounce instance's workgroups of
-    // kBounceWaves tiles (costs measured in the other unit are discarded)
-    const uint32_t group = (bounce && p.compact == 1u) ? rtk::kBounceWaves : 1u;
-    if (ctx->cost_groups != (group > 1u)) {
+    // scheduling units: 8x8 tiles, the compacting bounce instance's workgroups of
+    // kBounceWaves tiles or rt_tpair_kernel's tile pairs (costs measured in another unit are
+    // discarded)
+    const uint32_t group = (bounce && p.compact == 1u)         ? rtk::kBounceWaves
+                           : (kernel == rtk::kTraceListQuad2 ||
+                              kernel == rtk::kTraceListPair2) ? 2u
+                                                            : 1u;
+    if (ctx->cost_group != group) {
         ctx->cost_gen = ctx->order_gen = ~0ull;
-        ctx->cost_groups = group > 1u;
+        ctx->cost_group = group;
     }
     const uint64_t gen = ctx->cand_gen;
     const uint32_t tiles_x0 = (p.width + 7u) >> 3;
@@ -1236,7 +1240,8 @@ const char* rt_kernel_name(int which) {
                                         "rt_bounce_kernel<1>",     "rt_bounce_kernel<2>",
                                         rtk::single_kernel_name(0),
                                         rtk::single_kernel_name(1),
-                                        "rt_bounce_kernel<3>"};
+                                        "rt_bounce_kernel<3>",     "rt_tpair_kernel<2>",
+                                        "rt_tpair_kernel<4>"};
     if (which >= 0 && which < (int)(sizeof(names) / sizeof(names[0]))) return names[which];
     return rtk::trace_kernel_name();
 }
@@ -1338,7 +1343,7 @@ rt_status rt_set_frames_per_launch(rt_ctx* ctx, uint32_t frames_per_launch) {
 rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     if (mode != RT_FRAME_PAIRS_AUTO && mode != RT_FRAME_PAIRS_OFF && mode != RT_FRAME_PAIRS_ON &&
-        mode != RT_FRAME_PAIRS_QUAD)
+        mode != RT_FRAME_PAIRS_QUAD && mode != RT_FRAME_PAIRS_ON2 && mode != RT_FRAME_PAIRS_QUAD2)
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown frame-pair mode");
     ctx->frame_pairs = mode;
     return RT_OK;
@@ -1553,11 +1558,19 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
         const bool pairable = kernel == rtk::kTraceList && p.store_each && known &&
                               p.hint_frames == nf;
         if (pairable && ctx->frame_pairs != RT_FRAME_PAIRS_OFF) {
-            // AUTO: four waves per tile when the share is small (a few tiles per SIMD)
+            // AUTO: four waves per tile when the share is small (a few tiles per SIMD), two
+            // per pair of tiles for whole-image-sized launches, else two per tile (DESIGN.md
+            // §5 "Frame groups over tile pairs")
+            const int mode = ctx->frame_pairs;
             const uint64_t tiles = (uint64_t)((w + 7u) >> 3) * p.local_bands;
-            const bool quad = ctx->frame_pairs == RT_FRAME_PAIRS_QUAD ||
-                              (ctx->frame_pairs == RT_FRAME_PAIRS_AUTO && tiles <= rtk::kQuadMaxTiles);
-            kernel = quad ? rtk::kTraceListQuad : rtk::kTraceListPair;
+            const bool quad = mode == RT_FRAME_PAIRS_QUAD || mode == RT_FRAME_PAIRS_QUAD2 ||
+                              (mode == RT_FRAME_PAIRS_AUTO && tiles <= rtk::kQuadMaxTiles);
+            // (the tile-pair instances read the candidate blocks: lists required)
+            const bool tpair = p.cand && (mode == RT_FRAME_PAIRS_ON2 || mode == RT_FRAME_PAIRS_QUAD2 ||
+                                          (mode == RT_FRAME_PAIRS_AUTO && !quad &&
+                                           tiles >= rtk::kTpairMinTiles));
+            kernel = quad ? (tpair ? rtk::kTraceListQuad2 : rtk::kTraceListQuad)
+                          : (tpair ? rtk::kTraceListPair2 : rtk::kTraceListPair);
         }
         kernel = single_or(ctx, p, kernel);
         const bool aql = chain && nf == 1u &&

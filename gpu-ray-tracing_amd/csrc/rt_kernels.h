@@ -142,6 +142,11 @@ constexpr int kTraceListPair = 3;
 // The same with four waves per tile: for small per-rank shares (few tiles per SIMD), where
 // shorter per-wave frame chains keep more waves resident (rt_abi.cpp picks it).
 constexpr int kTraceListQuad = 4;
+// The frame groups over tile pairs: two pixels per lane (rt_tpair_kernel<2 / 4>).
+constexpr int kTraceListPair2 = 11;
+constexpr int kTraceListQuad2 = 12;
+static_assert(kTraceListPair2 == RT_KERNEL_LIST_PAIR2 && kTraceListQuad2 == RT_KERNEL_LIST_QUAD2,
+              "instance ids are the ABI's RT_KERNEL_LIST_*2");
 static_assert(kTraceExhaustive == RT_KERNEL_EXHAUSTIVE && kTraceCulled == RT_KERNEL_CULLED &&
                   kTraceList == RT_KERNEL_LIST && kTraceListPair == RT_KERNEL_LIST_PAIR &&
                   kTraceListQuad == RT_KERNEL_LIST_QUAD,
@@ -177,10 +182,16 @@ constexpr bool is_list_kernel(int k) { return k == kTraceList || is_group_kernel
 // Instances that run cost-ordered tiles (one tile per workgroup): the frame groups, and
 // kTraceList when its workgroups are one wave.
 constexpr bool trace_ordered(int k) {
-    return is_list_kernel(k) && (is_group_kernel(k) || RT_WG_WAVES == 1);
+    return k == kTraceListQuad2 || k == kTraceListPair2 ||
+           (is_list_kernel(k) && (is_group_kernel(k) || RT_WG_WAVES == 1));
 }
 // Tiles per launch at or below which frame groups of four are used.
 constexpr uint64_t kQuadMaxTiles = 6144;
+// Tiles per launch from which AUTO's groups of two own a pair of tiles (rt_tpair_kernel<2>:
+// 2 waves per pair, 7 waves per SIMD).  K3 20-frame chains, µs per frame one tile / tile
+// pair: whole image 16.74 / 16.03, 2-rank share 8.62 / 8.61, 4-rank share (8 100 tiles:
+// 8 100 waves for 7 168 wave slots) 4.71 / 5.14 (profiles/r05/r05ag/pairs_chain.jsonl).
+constexpr uint64_t kTpairMinTiles = 24000;
 // The seed-hash tables share one buffer: hash(x*73) for x < hy_offset(width), then
 // hash(y*51) per row (TraceParams::hy == hx + hy_offset(width)).
 constexpr uint32_t hy_offset(uint32_t width) { return (width + 63u) & ~63u; }

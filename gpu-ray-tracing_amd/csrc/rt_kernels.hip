@@ -1458,8 +1458,8 @@ __device__ __forceinline__ v3 sky_w(v3 cf, v3 d) { return sky_w(cf, d, dot(d, d)
 // ncand[s] its count (kCandNone: the full list; 0 for a tile past the image edge).
 template <uint32_t S>
 constexpr bool kSingleLds = RT_SINGLE_LDS == 2 || (RT_SINGLE_LDS == 1 && S == 1);
-template <uint32_t S, bool kUniRs>
-__device__ __forceinline__ void single_sample(const SingleParams& p, const Cam& cam,
+template <uint32_t S, bool kUniRs, typename P>
+__device__ __forceinline__ void single_sample(const P& p, const Cam& cam,
                                               const TileCoord (&tc)[S],
                                               const uint32_t (&hxy)[S],
                                               const uint32_t (&seed)[S],
@@ -1930,6 +1930,176 @@ __global__ __launch_bounds__(64) void rt_chain_go_kernel(const uint32_t* go, uin
 __global__ __launch_bounds__(64) void rt_chain_done_kernel(uint32_t* done, uint32_t value) {
     if (threadIdx.x == 0u)
         __hip_atomic_store(done, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ---- Frame groups over tile pairs (kTraceListPair2, kTraceListQuad2) -----------------
+//
+// The frame-group schedule of trace_pair (kFrameGroup waves, wave w traces frames f + w of
+// each group, wave 0 accumulates through LDS) with the one-frame kernel's sample: each
+// workgroup owns two horizontally adjacent tiles and each lane one pixel of each, the two
+// tiles' candidate lists walked jointly (single_sample<2>) — two independent pixel chains per
+// lane instead of one, and half the waves for the same work.  Called for launches whose
+// every frame is hinted (rt_abi.cpp: the frame-group conditions); a workgroup whose loaded
+// counts differ from the hint traces each tile with the general per-tile loop (waves 0 and
+// 1).  Scheduling units (tile order, costs): tile pairs.  G: frames per group (2 or 4).
+// Waves per SIMD the register plan targets: 7 (69 VGPRs, no scratch) — at 8 the compiler
+// fits 64 VGPRs with 40 B of scratch per lane and 69 SGPR spills, and a whole-image 64-frame
+// pair launch takes 14.94 against 14.27 us per frame (profiles/r05/r05af/ab_k3_fused.log).
+#ifndef RT_TPAIR_MIN_WAVES
+#define RT_TPAIR_MIN_WAVES 7
+#endif
+// single_sample's parameters for one frame of a frame group
+struct FrameView {
+    const float4* geom;
+    const float4* sph;
+    uint32_t count, depth, seed_b, normal_rn;
+    float4 rs;
+};
+// (G an int: rocprofv3 lists the instances as rt_tpair_kernel<2> / <4>, rt_kernel_name's names)
+template <int G>
+__global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
+    const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
+    const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
+    const TraceParams p) {
+    constexpr uint32_t S = 2, Gu = (uint32_t)G;
+    static_assert(!kSingleLds<S>, "the pair sample reads its records from the candidate blocks");
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t tiles_x = (a_width + 7u) >> 3;
+    const uint32_t units_x = (tiles_x + S - 1u) / S;
+    uint32_t ux = blockIdx.x, lband = blockIdx.y;
+    const uint32_t band_first = a_bands & 0xFFFFu, band_step = (a_bands >> 16) & 0x7FFFu;
+    if (a_bands >> 31) {                                 // costliest units first (tile_order)
+        const uint32_t t =
+            __builtin_amdgcn_readfirstlane(p.tile_order[blockIdx.y * gridDim.x + blockIdx.x]);
+        ux = t & 0xFFFFu;
+        lband = t >> 16;
+    }
+    const uint32_t unit = lband * units_x + ux;
+    const uint32_t tx0 = ux * S;
+    TileCoord tc[S];
+    uint32_t ncand[S], hxy[S], tile[S];
+    const float4* blk[S];
+    float4 acc[S];
+    uint64_t valid_m[S];
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s) {
+        const uint32_t tx = tx0 + s;
+        const bool in = tx < tiles_x;
+        tile[s] = lband * tiles_x + (in ? tx : tx0);
+        tc[s] = tile_coord(a_width, a_height, band_first, band_step, tx, lband, lane);
+        blk[s] = a_cand + (size_t)tile[s] * kCandStride;
+        ncand[s] = in ? load_cnt(a_cand, tile[s]) : 0u;
+        acc[s] = a_in[tc[s].valid ? tc[s].idx : 0];               // wgsl:339
+        hxy[s] = a_hx[min(tc[s].x, a_width - 1u)] ^                // wgsl:309-310
+                 a_hx[hy_offset(a_width) + min(tc[s].y, a_height - 1u)];
+        valid_m[s] = mask_ult(tc[s].x, a_width) & mask_ult(tc[s].y, a_height);
+    }
+    if (p.tile_cost && w == 0u && lane == 0u)
+        p.tile_cost[unit] = (uint32_t)__builtin_amdgcn_s_memtime();
+    const Cam cam = cam_params(p);
+    const uint32_t n0 = p.hint_n[0];
+    if (!p.reset_first &&
+        rt_ballot((tc[0].valid && f2u(acc[0].w) != n0) || (tc[1].valid && f2u(acc[1].w) != n0)) !=
+            0ull) {
+        // a foreign count: wave s traces tile s frame after frame (stores every image itself)
+        if (w < S && tx0 + w < tiles_x) {
+            const float4 res = trace_pixel<kTraceListQuad, false>(
+                p, cam, w ? tile[1] : tile[0], w ? ncand[1] : ncand[0], w ? tc[1] : tc[0],
+                w ? hxy[1] : hxy[0], w ? acc[1] : acc[0]);
+            const TileCoord& t = w ? tc[1] : tc[0];
+            if (t.valid && !p.store_each) p.out[t.idx] = res;     // wgsl:363
+        }
+    } else {
+        const uint32_t spp = p.spp;                               // wgsl:343
+        // wave 0's accumulators stay in LDS between groups (no registers live across the
+        // samples: the instance fits 64 VGPRs, 8 waves per SIMD)
+        __shared__ float4 s_cols[2u * (Gu - 1u) * S * 64u];
+        __shared__ float4 s_acc[S * 64u];
+        if (w == 0u)
+#pragma unroll
+            for (uint32_t s = 0; s < S; ++s)
+                s_acc[s * 64u + lane] = p.reset_first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)
+                                                      : acc[s];
+        const float4 zero4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        for (uint32_t f = 0; f < p.frames; f += Gu) {
+            const uint32_t fw = f + w;
+            v3 col[S];
+#pragma unroll
+            for (uint32_t s = 0; s < S; ++s) col[s] = mk(0.0f, 0.0f, 0.0f);
+            if (fw < p.frames) {
+                const uint32_t ng = p.hint_n[fw];   // every pixel's count before frame fw
+                if (ng < spp) {                                   // wgsl:352
+                    FrameView v;
+                    v.geom = p.geom;
+                    v.sph = p.sph;
+                    v.count = p.count;
+                    v.depth = p.depth;
+                    v.seed_b = p.seed_b[fw];
+                    v.normal_rn = p.normal_rn;
+                    v.rs = p.hint_rs[fw * p.depth];
+                    uint32_t seed[S];
+                    bool live[S];
+                    const float4 bv[S] = {zero4, zero4};
+#pragma unroll
+                    for (uint32_t s = 0; s < S; ++s) {
+                        seed[s] = 1u + ng + v.seed_b;             // wgsl:353
+                        live[s] = tc[s].valid;
+                    }
+                    single_sample<S, true>(v, cam, tc, hxy, seed, blk, ncand, live, valid_m, bv,
+                                           nullptr, col);
+                }
+            }
+            // two LDS slots alternating by group (one barrier per group, as trace_pair)
+            float4* slot = s_cols + ((f / Gu) & 1u) * (Gu - 1u) * S * 64u;
+            if (w != 0u)
+#pragma unroll
+                for (uint32_t s = 0; s < S; ++s)
+                    slot[((w - 1u) * S + s) * 64u + lane] =
+                        make_float4(col[s].x, col[s].y, col[s].z, 0.0f);
+            __syncthreads();
+            if (w == 0u) {
+#pragma unroll
+                for (uint32_t j = 0; j < Gu; ++j) {
+                    const uint32_t fj = f + j;
+                    if (fj >= p.frames) break;
+                    const uint32_t nb = p.hint_n[fj];             // count before frame fj
+                    const bool acc_frame = nb < spp;              // wgsl:352-358
+                    float4* out = (fj & 1u) ? p.out2 : p.out;
+                    const bool store = p.store_each == 2u || fj + 2u >= p.frames;
+#pragma unroll
+                    for (uint32_t s = 0; s < S; ++s) {
+                        const float4 ca = s_acc[s * 64u + lane];
+                        v3 cs = mk(ca.x, ca.y, ca.z);
+                        v3 cj = col[s];
+                        if (j != 0) {
+                            const float4 t = slot[((j - 1u) * S + s) * 64u + lane];
+                            cj = mk(t.x, t.y, t.z);
+                        }
+                        if (acc_frame) {
+                            const v3 num = sub(cj, cs);
+                            // num / f32(nb + 1) (wgsl:356) as a Markstein division (acc_rn)
+                            if (nb < (1u << 24) &&
+                                rt_ballot(tc[s].valid && !acc_ok(num)) == 0ull) {
+                                cs = acc_rn(cs, num, (float)(nb + 1u), p.hint_rcp[fj]);
+                            } else {
+                                const float k = (float)(nb + 1u);   // wgsl:356
+                                cs = mk(cs.x + num.x / k, cs.y + num.y / k, cs.z + num.z / k);
+                            }
+                        }
+                        s_acc[s * 64u + lane] = make_float4(cs.x, cs.y, cs.z, 0.0f);
+                        // wgsl:362-363: the images that survive (or every frame's)
+                        if (store && tc[s].valid)
+                            out[tc[s].idx] =
+                                make_float4(cs.x, cs.y, cs.z,
+                                            (float)(acc_frame ? nb + 1u : nb));
+                    }
+                }
+            }
+        }
+    }
+    if (p.tile_cost && w == 0u && lane == 0u)
+        p.tile_cost[unit] = (uint32_t)__builtin_amdgcn_s_memtime() - p.tile_cost[unit];
 }
 
 // ---- Bounce paths with workgroup-wide compaction (kTraceBounce) -----------------------
@@ -2915,7 +3085,7 @@ static dim3 tile_grid(const TraceParams& p, uint32_t waves = 4) {
 // Launches through hipModuleLaunchKernel with the arguments packed in the kernel's layout and
 // a function handle cached per device and kernel (the launch_single path below): no
 // per-launch symbol lookup or per-argument marshalling of the 2.6-KB TraceParams block.
-// Slots: 0-4 and 11 rt_trace_kernel<k>, 5-8 rt_bounce_kernel<m>.
+// Slots: 0-4 rt_trace_kernel<k>, 5-8 rt_bounce_kernel<m>, 9-10 rt_tpair_kernel<4 / 2>.
 constexpr int kLaunchSlots = 12;
 static hipError_t launch_packed(int slot, const void* sym, dim3 grid, dim3 block, size_t lds,
                                 hipStream_t stream, void* args, size_t bytes) {
@@ -2966,6 +3136,26 @@ static hipError_t launch_trace_as(const TraceParams& p, size_t lds, hipStream_t 
     args.p = p;
     return launch_packed(kScan, reinterpret_cast<const void*>(&rt_trace_kernel<kScan>), grid,
                          dim3(64 * w), lds, stream, &args, sizeof(args));
+}
+
+// rt_tpair_kernel<G>: one workgroup of G waves per pair of tiles along a stripe band, grid
+// (tile pairs, bands) — or the tile order's units in that shape.
+template <int G>
+static hipError_t launch_tpair(const TraceParams& p, hipStream_t stream) {
+    const dim3 grid((((p.width + 7u) >> 3) + 1u) >> 1, p.local_bands);
+    if (grid.x == 0 || grid.y == 0 || !p.cand) return grid.x && grid.y ? hipErrorInvalidValue
+                                                                      : hipSuccess;
+    TraceArgs args;
+    std::memset(&args, 0, offsetof(TraceArgs, p));
+    args.cand = p.cand;
+    args.hx = p.hx;
+    args.in = p.in;
+    args.width = p.width;
+    args.height = p.height;
+    args.bands = pack_bands(p.band_first, p.band_step, p.tile_order != nullptr);
+    args.p = p;
+    return launch_packed(G == 4 ? 9 : 10, reinterpret_cast<const void*>(&rt_tpair_kernel<G>),
+                         grid, dim3(64 * G), 0, stream, &args, sizeof(args));
 }
 
 // Workgroups of kBounceWaves tiles along a stripe band: grid (column groups, bands).
@@ -3175,6 +3365,8 @@ hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream) {
     if (kernel == kTraceBounce) return launch_bounce(p, stream);
     if (kernel == kTraceListQuad)
         return launch_trace_as<kTraceListQuad>(p, group_lds_bytes<kTraceListQuad>(), stream);
+    if (kernel == kTraceListQuad2) return launch_tpair<4>(p, stream);
+    if (kernel == kTraceListPair2) return launch_tpair<2>(p, stream);
     return launch_trace_as<kTraceExhaustive>(p, 0, stream);
 }
 

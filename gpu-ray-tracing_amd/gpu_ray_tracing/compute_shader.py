@@ -94,9 +94,10 @@ class ComputeShaderPipeline:
 
     def set_frame_pairs(self, mode: str) -> None:
         """rt_set_frame_pairs: 'auto' | 'off' | 'on' (two waves per tile, alternate frames)
-        | 'quad' (four waves per tile)."""
+        | 'quad' (four waves per tile) | 'on2' / 'quad2' (two / four waves per pair of tiles,
+        two pixels per lane)."""
         _lib.call("rt_set_frame_pairs", self._ctx,
-                  {"auto": 0, "off": 1, "on": 2, "quad": 3}[mode])
+                  {"auto": 0, "off": 1, "on": 2, "quad": 3, "on2": 4, "quad2": 5}[mode])
 
     def set_frame_images(self, mode: str) -> None:
         """rt_set_frame_images: the images a fused multi-frame launch writes — "last_two"

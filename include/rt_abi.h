@@ -158,14 +158,14 @@ typedef struct rt_ctx rt_ctx;
 
 /* Version / introspection ------------------------------------------------------------ */
 RT_API uint32_t rt_abi_version(void); /* RT_ABI_VERSION */
-#define RT_ABI_VERSION 5u
+#define RT_ABI_VERSION 6u
 /* Text of the last error on this thread (never NULL). */
 RT_API const char* rt_last_error(void);
 /* Trace-kernel instances (rt_launch_info.kernel) and their names as rocprofv3 lists them
  * (rt_kernel_name).  The library picks the instance per launch: the reference's exhaustive
  * scan, the culled scan (bounce rays), the camera-ray-only instance with candidate lists
  * (max_depth <= 1; one wave per tile), and its frame groups of two / four waves per tile
- * (fused multi-frame launches). */
+ * (fused multi-frame launches) or per pair of tiles (two pixels per lane). */
 #define RT_KERNEL_EXHAUSTIVE 0
 #define RT_KERNEL_CULLED 1
 #define RT_KERNEL_LIST 2
@@ -184,8 +184,12 @@ RT_API const char* rt_last_error(void);
 /* bounce rays, each tile's frames split into chunks traced by separate waves, the last
  * finisher accumulating them in order (RT_PATHS_SPLIT) */
 #define RT_KERNEL_BOUNCE_SPLIT 10
+/* frame groups of two / four waves per pair of horizontally adjacent tiles: each lane traces
+ * one pixel of each tile (ABI 6) */
+#define RT_KERNEL_LIST_PAIR2 11
+#define RT_KERNEL_LIST_QUAD2 12
 /* The instance's name as rocprofv3 lists it ("rt_trace_kernel<k>", "rt_bounce_kernel<m>",
- * "rt_single_kernel<p>"), "rt_trace_kernel" for an unknown id. */
+ * "rt_single_kernel<p>", "rt_tpair_kernel<g>"), "rt_trace_kernel" for an unknown id. */
 RT_API const char* rt_kernel_name(int which);
 /* What the last rt_update / rt_render / rt_render_stripes / rt_update_frames call on this
  * context launched: trace launches, frames traced, the most frames one launch carried, the
@@ -302,12 +306,17 @@ RT_API rt_status rt_set_frame_images(rt_ctx* ctx, int mode);
  * a different frame of each group of frames (the others hand their colours to wave 0,
  * which accumulates every frame in order: the same bits), whenever every pixel
  * holds the sample count the context expects (otherwise the launch falls back to one wave
- * per tile).  AUTO (default): 2 waves per tile, 4 for launches of at most 6144 tiles (small
- * per-rank shares); ON: 2; QUAD: 4; OFF: one wave per tile. */
+ * per tile).  The groups' waves own one tile (ON: 2 waves, QUAD: 4) or a pair of adjacent
+ * tiles, each lane tracing one pixel of each (ON2: 2 waves, QUAD2: 4; ABI 6).  AUTO
+ * (default): 4 waves per tile for launches of at most 6144 tiles (small per-rank shares),
+ * 2 waves per pair of tiles from 24000 tiles (whole images), else 2 waves per tile; OFF:
+ * one wave per tile. */
 #define RT_FRAME_PAIRS_AUTO 0
 #define RT_FRAME_PAIRS_OFF 1
 #define RT_FRAME_PAIRS_ON 2
 #define RT_FRAME_PAIRS_QUAD 3
+#define RT_FRAME_PAIRS_ON2 4
+#define RT_FRAME_PAIRS_QUAD2 5
 RT_API rt_status rt_set_frame_pairs(rt_ctx* ctx, int mode);
 /* Tile scheduling (culled scan mode).  AUTO (default): fused multi-frame launches (the
  * camera-ray-only kernels and the bounce instance): the first such launch for a camera

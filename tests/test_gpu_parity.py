@@ -152,10 +152,11 @@ def test_golden_k4_fused_64spp(rt, pipe):
     assert hashlib.sha256(img.tobytes()).hexdigest() == str(g["sha256"])
 
 
-@pytest.mark.parametrize("pairs", ["auto", "quad"])
+@pytest.mark.parametrize("pairs", ["auto", "on", "quad", "quad2"])
 def test_bench_k4_launches_match_golden(rt, pairs):
     """The kernel bench.py --config K4 times, at the timed size: rt_update_frames of 64
-    frames from a reset at 1920x1080 / 500 spheres (AUTO: frame pairs, kTraceListPair; the
+    frames from a reset at 1920x1080 / 500 spheres (AUTO: frame pairs over tile pairs,
+    kTraceListPair2; the
     first launch records tile costs, the second runs cost-ordered tiles).  Both launches'
     newest image hashes to k4.npz's, the other buffer holds frame 63."""
     g = load_golden("k4.npz")
@@ -169,8 +170,10 @@ def test_bench_k4_launches_match_golden(rt, pairs):
             newest = p.update_frames(a, b, w, h, cam, sc, g["seeds"])
             info = p.last_launch_info()
             assert info["launches"] == 1 and info["max_frames_per_launch"] == 64
-            assert info["kernel_name"] == {"auto": "rt_trace_kernel<3>",
-                                           "quad": "rt_trace_kernel<4>"}[pairs]
+            assert info["kernel_name"] == {"auto": "rt_tpair_kernel<2>",
+                                           "on": "rt_trace_kernel<3>",
+                                           "quad": "rt_trace_kernel<4>",
+                                           "quad2": "rt_tpair_kernel<4>"}[pairs]
             img = host(b if newest == 1 else a)
             assert hashlib.sha256(img.tobytes()).hexdigest() == str(g["sha256"]), launch
             other = host(a if newest == 1 else b)
@@ -823,7 +826,7 @@ def test_candidate_list_overflow_falls_back(rt, depth):
                                                   (7, 1, 4, 0), (4, 1, 500, 1), (6, 3, 500, 4),
                                                   (5, 8, 500, 4), (9, 2, 3, 3), (14, 1, 500, 4),
                                                   (11, 1, 6, 3)])
-@pytest.mark.parametrize("pairs", ["off", "on", "quad"])
+@pytest.mark.parametrize("pairs", ["off", "on", "quad", "on2", "quad2"])
 @pytest.mark.parametrize("images", ["last_two", "every"])
 def test_update_frames_equals_chained_updates(rt, pipe, nranks, frames, depth, spp, per, pairs,
                                               images):
@@ -1078,7 +1081,7 @@ def test_hinted_chain_matches_oracle(rt, oracle, pipe, depth, spp):
         assert_same(host(cur), ref)
 
 
-@pytest.mark.parametrize("pairs", ["off", "on", "quad"])
+@pytest.mark.parametrize("pairs", ["off", "on", "quad", "on2", "quad2"])
 def test_update_frames_with_foreign_counts(rt, oracle, pipe, pairs):
     """rt_update_frames on an image whose counts the library did not write (mixed per-pixel
     counts behind its back, after init_image): the hinted / frame-pair launch falls back to

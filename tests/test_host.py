@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol(rt):
     assert set(declared) <= exported, set(declared) - exported
     # the ctypes binding covers exactly the header
     assert set(rt._lib.exported_symbols()) == set(declared)
-    assert rt._lib.lib().rt_abi_version() == 5
+    assert rt._lib.lib().rt_abi_version() == 6
 
 
 def test_scene_camera_layout_matches_reference(rt):
