@@ -452,10 +452,11 @@ extern __shared__ float4 lds_recs[];
 // valid but not below the running tmax has a second root at least as large (h + q >= h - q,
 // a > 0), and a tie keeps the earlier index.  So the spheres may be tested in any order with
 // consider_any's rule.  A sphere can be accepted only at a root t > 0 whose point lies
-// within R + m of its centre (m the f32 margin of the discriminant, as in the cone test), so
-// the grid walk visits every cell the ray passes through for t >= 0 inside the gridded
-// spheres' slab, and each sphere is registered in every cell within R + grid_m + grid_e of
-// its centre (rt_abi.cpp): no sphere that could be accepted is skipped.
+// within sqrt(R^2 + m^2) of its centre (m the f32 margin of the discriminant, as in the cone
+// test), so the grid walk visits every cell the ray passes through for t >= 0 inside the
+// gridded spheres' slab, and each sphere is registered in every cell within
+// sqrt(R^2 + grid_m^2) + grid_e of its centre (rt_abi.cpp): no sphere that could be accepted
+// is skipped.
 __device__ __forceinline__ void consider_any(float disc, float h, float a, uint32_t i,
                                              float& tmax, int& idx) {
     if (!(disc < 0.0f)) {                                               // wgsl:189
