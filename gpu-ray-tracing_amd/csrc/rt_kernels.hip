@@ -1943,7 +1943,7 @@ __global__ __launch_bounds__(64) void rt_chain_done_kernel(uint32_t* done, uint3
 // every frame is hinted (rt_abi.cpp: the frame-group conditions); a workgroup whose loaded
 // counts differ from the hint traces each tile with the general per-tile loop (waves 0 and
 // 1).  Scheduling units (tile order, costs): tile pairs.  G: frames per group (2 or 4).
-// Waves per SIMD the register plan targets: 7 (69 VGPRs, no scratch) — at 8 the compiler
+// Waves per SIMD the register plan targets: 7 (71 VGPRs, no scratch) — at 8 the compiler
 // fits 64 VGPRs with 40 B of scratch per lane and 69 SGPR spills, and a whole-image 64-frame
 // pair launch takes 14.94 against 14.27 us per frame (profiles/r05/r05af/ab_k3_fused.log).
 #ifndef RT_TPAIR_MIN_WAVES
@@ -2014,7 +2014,7 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
     } else {
         const uint32_t spp = p.spp;                               // wgsl:343
         // wave 0's accumulators stay in LDS between groups (no registers live across the
-        // samples: the instance fits 64 VGPRs, 8 waves per SIMD)
+        // samples; the foreign-count fallback above sets the register peak)
         __shared__ float4 s_cols[2u * (Gu - 1u) * S * 64u];
         __shared__ float4 s_acc[S * 64u];
         if (w == 0u)
