@@ -5,37 +5,43 @@
 Configs (BASELINE.json `configs`):
   K2, K3 (default)  1920x1080, 3 / 500 spheres, max_depth 1.  A step is ONE progressive
                     `update` (wgsl:333-364): one camera sample per pixel of this rank's stripe
-                    bands, accumulated into the RGBA32F image.  The whole image (N=1) runs
-                    one launch per frame, the reference's dispatch structure (lib.rs:408-417);
-                    rank shares of at most CHAIN_MAX_TILES tiles run the steps' frames as
-                    frame chains — fused launches that still write every frame's image to the
-                    ping-pong buffer its dispatch would write (rt_set_frame_images EVERY), so
-                    only the launch boundary between frames goes (--frame-launch).
+                    bands, accumulated into the RGBA32F image, the image of every frame written
+                    to the ping-pong buffer the reference's dispatch writes (lib.rs:218-227,
+                    366-374).  The K steps are one rt_update_frames call; the SAME launch
+                    structure runs at every N (--frame-launch chain, default): fused launches
+                    of up to 64 frames that write every frame's image (rt_set_frame_images
+                    EVERY) — the reference's per-frame loop with only the launch boundary
+                    between frames removed.  --frame-launch dispatch: one launch per frame,
+                    the reference's own structure (reported as the `dispatch` side line at N=1).
   K4                1920x1080, 500 spheres, 64 spp anti-aliased accumulate, max_depth 1.  A
-                    step is one 64-spp render from a reset accumulator: 64 chained updates
-                    issued by one rt_update_frames call (fused launches of up to 64 frames).
+                    step is one 64-spp render from a reset accumulator (fused launches).
   K5                3840x2160, 500 spheres, 64 spp, 8 bounces — the multi-GPU config.  A step
                     is one 64-spp render (one 64-frame launch of the bounce instance).
 With N GPUs (one process per GPU, torch.distributed.run) the image is split into 8-row bands
 dealt round-robin; the steps have no collective (a rank's bands need nothing from another
 rank).  After the K timed steps the finished tiles are gathered to rank 0 with ONE RCCL
 gather + the de-interleave kernel (rt_gather_stripes, the ncclGather behind librt_hip.so's C
-ABI; RT_GATHER=torch: torch.distributed.gather instead): the job's output collection, timed
-on its own between barriers and reported as `gather` next to the job-level rate that includes
-it (`job`), not inside the K steps.
+ABI; RT_GATHER=torch: torch.distributed.gather instead), timed on its own and reported as
+`gather` and in the job-level rate `job`, not inside the K steps.
 
-value = W*H*spp_per_step*K camera rays / max-over-ranks wall time of the K steps (Mrays/s,
-all ranks together).
-image_ok: the timed image against committed fixtures (K2/K3: 4096 sampled pixels after W+K
-frames, tests/golden/bench_k*.npz; K4: the full-image SHA-256 of tests/golden/k4.npz; K5:
-the 512 sampled pixels of k5.npz) — null when no fixture covers the run's frame count.
-roofline (the timed trace-kernel launches, HIP events on the stream they run on): the
-algorithmic bytes of the reference's progressive update, 32 B per pixel per launch (16 B
-load + 16 B store of the accumulator), against 8 TB/s; `traffic` = the PMC
-bytes of the same kernel at the same frames per launch (profiles/pmc_r02_<config>.json,
-FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM); `valu` = the binding resource: VALU
-wave-instructions per launch (same PMC file) x 2 cycles (a wave64 VALU op on a SIMD-32) over
-the cycles 1024 SIMDs offer at 2.4 GHz during the measured launch time.
+Timed region (timed_steps): barrier + synchronize, every rank reads CLOCK_MONOTONIC, issues
+its K steps, synchronizes and reads it again; the job's time is max(end) - min(start) over
+ranks (one host: one clock).  Nothing else runs inside it (no events: HIP event markers cost
+~2.5 µs per region on an idle GPU, profiles/r06/r06b/).
+value = W*H*spp_per_step*K camera rays / that time (Mrays/s, all ranks together).
+segments_per_s: sphere_list_hit calls (SURVEY §8a "seg") per second — the fixture's exact
+count for the rendered frames (the oracle counts them over the whole image).
+image_ok: the timed image's SHA-256 (NaN canonical) against the fixture's whole-image digest
+(tests/golden/*.npz `sha256`, oracle-generated), else its sampled pixels; rank shares are
+checked band by band against the fixture's per-band digests (`band_sha`).
+roofline: the timed kernel's launch duration by HIP events over an identical repetition after
+the timed region (same renderer state, same frames); `bound: "valu"` when a committed PMC
+summary of that kernel instance exists (profiles/pmc_<round>_<config>.json): achieved = the
+VALU lane-operations per second it issues (SQ_INSTS_VALU x 64 / launch time) against 1024
+SIMDs x 32 lanes x 2.4 GHz (a wave64 VALU op holds a SIMD-32 two cycles); `hbm` = the
+algorithmic bytes actually moved (chain: 16 B load once + 16 B store per pixel and frame;
+dispatch: 16 B load + 16 B store per pixel and frame) against 8 TB/s, `traffic`
+= the PMC bytes (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM).
 cpu_baseline: the scalar C oracle on the box's host cores over a bounded sample (rank 0, N=1).
 """
 from __future__ import annotations
@@ -45,6 +51,7 @@ import hashlib
 import json
 import math
 import os
+import statistics
 import sys
 import time
 from pathlib import Path
@@ -70,10 +77,13 @@ RMW_FLOOR_GBS = 6518.0
 CLOCK_GHZ = 2.4               # MI355X max engine clock
 SIMDS = 1024                  # 256 CUs x 4 SIMDs
 VALU_ISSUE_CYCLES = 2         # one wave64 VALU instruction on a SIMD-32
+PEAK_VALU_TOPS = SIMDS * 32 * CLOCK_GHZ / 1e3   # 78.64 T lane-ops/s
 FLOP_PER_TEST = 23            # oc 3, a 5, h 5, c 7, D 3 (wgsl:183-187)
 BYTES_PER_PIXEL_LAUNCH = 32   # 16 B load + 16 B store of the accumulator (wgsl:339, 363)
 FRAME_SEED = 0x5EED
 BENCH_SPP = 65536             # the dispatch configs' spp cap (never reached; fixtures agree)
+ROWS = 8                      # RT_STRIPE_ROWS
+CANON_NAN = np.uint32(0x7FC00000)
 
 CONFIGS = {
     # name: width, height, scene kind, spheres, max_depth, frames per step, description
@@ -87,21 +97,6 @@ CONFIGS = {
            "configs[4]: 3840x2160, 500 spheres, 64 spp, 8 bounces per step"),
 }
 DEFAULT_STEPS = {"K2": (200, 20), "K3": (200, 20), "K4": (8, 2), "K5": (2, 1)}
-# K2/K3 steps of a rank share of at most this many 8x8 tiles run as frame chains (fused
-# launches writing every frame's image) under --frame-launch auto; larger shares (the whole
-# image: 32 400 tiles) one update launch per frame.  DESIGN.md §6.
-CHAIN_MAX_TILES = 20000
-
-
-def share_tiles(w, rows):
-    return ((w + 7) // 8) * ((rows + 7) // 8)
-
-
-def frame_launch_mode(policy, w, rows):
-    """The K2/K3 step structure for a share of `rows` local rows: 'dispatch' or 'chain'."""
-    if policy != "auto":
-        return policy
-    return "chain" if share_tiles(w, rows) <= CHAIN_MAX_TILES else "dispatch"
 
 
 def set_frame_launch(pipe, mode):
@@ -111,32 +106,28 @@ def set_frame_launch(pipe, mode):
     pipe.set_frame_images("every" if mode == "chain" else "last_two")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--config", default="K3", choices=sorted(CONFIGS))
+    ap.add_argument("--frame-launch", default=os.environ.get("RT_FRAME_LAUNCH", "chain"),
+                    choices=["chain", "dispatch"],
+                    help="K2/K3 steps at every N: the K frames in fused launches that write "
+                         "every frame's image (chain, default), or one update launch per frame "
+                         "(dispatch, the reference's structure)")
     ap.add_argument("--queues", type=int, default=int(os.environ.get("RT_QUEUES", "0")),
-                    help="concurrent parts per one-frame update (rt_set_update_queues; "
-                         "0 = the library's choice)")
+                    help="dispatch structure: concurrent parts per one-frame update "
+                         "(rt_set_update_queues; 0 = the library's choice)")
     ap.add_argument("--submit", default=os.environ.get("RT_SUBMIT", "auto"),
                     choices=["auto", "hip", "aql"],
-                    help="how one-frame updates are submitted (rt_set_update_submit): HIP "
-                         "launches (auto) or AQL packets on the context's HSA queues")
+                    help="dispatch structure: how one-frame updates are submitted "
+                         "(rt_set_update_submit)")
     ap.add_argument("--warm-ms", type=float, default=float(os.environ.get("RT_WARM_MS", "50")),
-                    help="before the warmup steps, render this long with the same update "
-                         "frames on scratch images (untimed: a running render's steps, not a "
-                         "freshly started process's first launches, are what is timed; 0 = "
-                         "off)")
-    ap.add_argument("--frame-launch", default=os.environ.get("RT_FRAME_LAUNCH", "auto"),
-                    choices=["auto", "dispatch", "chain"],
-                    help="K2/K3 steps: one update launch per frame (dispatch, the reference's "
-                         "structure), or the rank's consecutive frames in fused launches that "
-                         "still write every frame's image to its ping-pong buffer (chain: "
-                         "rt_set_frame_images EVERY, only the launch boundary between frames "
-                         "removed); auto = dispatch for shares of at least "
-                         "CHAIN_MAX_TILES + 1 tiles (whole images), chain below")
+                    help="before the warmup steps, render this long with the same frames on "
+                         "scratch images (untimed: a running render's steps, not a freshly "
+                         "started process's first launches, are what is timed; 0 = off)")
     ap.add_argument("--gate", action="store_true",
                     help="diagnostic for profiled runs: hold the stream while the timed steps "
                          "are issued, then release it (StreamGate); the line is then not a "
@@ -145,11 +136,10 @@ def parse():
                     help="sphere-list scan: exact culling (default) or the reference's "
                          "exhaustive linear walk; images are bit-identical")
     ap.add_argument("--side", type=int, default=20,
-                    help="frames for each side measurement (exhaustive scan, fused frames, "
-                         "moving camera; 0 = none)")
+                    help="frames for each side measurement (0 = none)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="CPU baseline budget in seconds (0 = skip)")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     d_steps, d_warm = DEFAULT_STEPS[a.config]
     a.steps = d_steps if a.steps is None else a.steps
     a.warmup = d_warm if a.warmup is None else a.warmup
@@ -174,9 +164,7 @@ def host_threads():
 
 def cgroup_cpus():
     """The CPU bandwidth limit of this process's cgroup (cgroup v2 cpu.max: quota / period)
-    in CPUs, or None when unlimited or unreadable.  (A box may show every host core in nproc
-    and the affinity set while its cgroup allows far fewer: the all-cores sample then runs
-    more threads than the quota schedules at once.)"""
+    in CPUs, or None when unlimited or unreadable."""
     try:
         q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
         return None if q == "max" else round(int(q) / int(per), 2)
@@ -199,7 +187,7 @@ def cpu_baseline(cam, spheres, w, h, seconds):
     native threads (oracle_update_threads: 8-row bands claimed from a shared counter):
     (i) one thread on a row band (~seconds/5), (ii) host_threads() threads over whole frames
     (~2*seconds/5, at least one frame; the reported value: a GPU's share of the host), (iii)
-    every core of the process's affinity set (~seconds/5, 2-row bands)."""
+    every CPU the process can run on at once (~seconds/5, 2-row bands)."""
     from oracle import oracle as O
     img = np.zeros((h, w, 4), np.float32)
     O.lib()
@@ -228,7 +216,7 @@ def cpu_baseline(cam, spheres, w, h, seconds):
     frames, dt = threaded(T, 2 * seconds / 5, 8)
     # every CPU the process may run on at once: the affinity set, capped by the cgroup's CPU
     # bandwidth quota (a GPU box shows 256 CPUs in its affinity set while its cgroup
-    # schedules 16: 256 threads there time-slice 16 CPUs and measure the oversubscription)
+    # schedules 16: 256 threads there would measure the oversubscription)
     aff, quota = host_cpus()[1], cgroup_cpus()
     A = max(1, min(aff, int(quota))) if quota else aff
     band = max(1, min(8, h // (2 * A)))        # at least two bands per thread
@@ -249,16 +237,15 @@ def cpu_baseline(cam, spheres, w, h, seconds):
             "nproc": host_cpus()[0], "affinity_cpus": aff,
             "cgroup_cpu_quota": quota,
             "cores_rule": "value: min(16, affinity) threads, the per-GPU share of the box's host "
-                          "cores; all_cores: min(affinity set, cgroup CPU quota) threads — every "
-                          "CPU the process can run on at once"}
+                          "cores; all_cores: min(affinity set, cgroup CPU quota) threads"}
 
 
 def load_pmc(config, kernel, frames_per_launch, queues=1):
     """The newest committed rocprofv3 PMC summary of the timed kernel (tools/pmc_bench.sh),
     if it was taken for the same kernel instance at the same frames per launch and the same
-    concurrent parts per update (`queues`: a summary's per-launch counts are one part's), and
-    its path."""
-    for rnd in ("r05", "r04", "r03", "r02"):
+    concurrent parts per update (a summary's per-launch counts are one part's), and its
+    path."""
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):
         p = ROOT / "profiles" / f"pmc_{rnd}_{config}.json"
         if not p.exists():
             continue
@@ -269,281 +256,167 @@ def load_pmc(config, kernel, frames_per_launch, queues=1):
     return None, None
 
 
-def load_weighted(config, kernel, pmc_path=None):
-    """The weighted VALU cycles per launch of the timed kernel (tools/valu_weighted.py over
-    the PMC instruction classes and the instance's disassembly), if committed — and, when the
-    file names the PMC summary it was computed from, only for that summary."""
-    for rnd in ("r05", "r04", "r03"):
-        p = ROOT / "profiles" / f"valu_weighted_{rnd}_{config}.json"
-        if not p.exists():
-            continue
-        d = json.loads(p.read_text())
-        if d.get("kernel") == kernel and (pmc_path is None or d.get("pmc", pmc_path) == pmc_path):
-            return d, p.relative_to(ROOT).as_posix()
-    return None, None
+# ---- image checks against the committed fixtures ---------------------------------------
+def canon_sha(a) -> str:
+    """SHA-256 of a float32 image's bytes with every NaN as 0x7FC00000 (the parity tests
+    treat any NaN as equal to any NaN; tests/golden/make_band_digests.py digests the same)."""
+    a = np.ascontiguousarray(a, np.float32).copy()
+    a.view(np.uint32)[np.isnan(a)] = CANON_NAN
+    return hashlib.sha256(a.tobytes()).hexdigest()
 
 
-def image_check(config, image, frames, cam, w, h):
-    """The timed image against the committed fixtures (see the module docstring)."""
-    if image is None:
-        return None, "not the gathering rank"
-    img = image.detach().cpu().numpy()
-    if config in ("K2", "K3"):
-        g = dict(np.load(GOLDEN / f"bench_{config.lower()}.npz"))
-        if not np.array_equal(g["camera"].view(np.uint32), cam.blob.view(np.uint32)):
-            return False, "camera blob differs from the fixture's"
-        counts = [int(c) for c in g["frame_counts"]]
-        if frames not in counts:
-            return None, f"no fixture for {frames} frames (have {counts})"
-        want = g["pixels"][counts.index(frames)]
-        got = img[g["py"], g["px"]]
-        same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
-        return bool(same.all()), f"{want.shape[0]} sampled pixels after {frames} frames"
-    g = dict(np.load(GOLDEN / f"{config.lower()}.npz"))
-    if "sha256" in g:
-        ok = hashlib.sha256(np.ascontiguousarray(img, np.float32).tobytes()).hexdigest() == \
-            str(g["sha256"])
-        return ok, "full-image SHA-256 of the 64-spp render"
-    got = img[g["py"], g["px"]]
-    want = g["pixels"]
-    same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
-    return bool(same.all()), f"{want.shape[0]} sampled pixels of the 64-spp render"
+def _fixture(config):
+    name = f"bench_{config.lower()}.npz" if config in ("K2", "K3") else f"{config.lower()}.npz"
+    return dict(np.load(GOLDEN / name))
 
 
-def share_pixels_ok(config, local, frames, world, rank=0):
-    """A rank's share (local rows of bands rank, rank + world, ...) against the fixture's
-    sampled pixels that fall in those bands (the K2/K3 fixtures after `frames` frames, K5's
-    64-spp render)."""
-    img = local.detach().cpu().numpy()
-    if config in ("K2", "K3"):
-        g = dict(np.load(GOLDEN / f"bench_{config.lower()}.npz"))
+def _fixture_at(g, frames):
+    """(whole-image sha, band digests [bands, 32] or None, sampled pixels, segments) of a
+    fixture after `frames` frames, or None when it holds no such frame count."""
+    if "frame_counts" in g:                       # bench_k2 / bench_k3: several frame counts
         counts = [int(c) for c in g["frame_counts"]]
         if frames not in counts:
             return None
-        want = g["pixels"][counts.index(frames)]
-    else:
-        g = dict(np.load(GOLDEN / f"{config.lower()}.npz"))
-        want = g["pixels"]
-    py, px = g["py"], g["px"]
-    mine = (py // 8) % world == rank
-    ly = (py[mine] // 8 // world) * 8 + py[mine] % 8
-    got, want = img[ly, px[mine]], want[mine]
+        k = counts.index(frames)
+        sha = str(g["sha256"][k]) if "sha256" in g else None
+        bands = g["band_sha"][k] if "band_sha" in g else None
+        segs = int(g["segments"][k]) if "segments" in g else None
+        return sha, bands, g["pixels"][k], segs
+    sha = str(g["sha256"]) if "sha256" in g else None
+    segs = int(g["segments"]) if "segments" in g else None
+    return sha, g.get("band_sha"), g["pixels"], segs
+
+
+def _pixels_same(got, want):
     same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
-    return bool(same.all()) and int(mine.sum()) > 0
+    return bool(same.all())
 
 
+def image_check(config, image, frames, cam):
+    """The timed image against the committed fixture: its whole-image digest when the
+    fixture has one for this frame count, else its sampled pixels."""
+    if image is None:
+        return None, "not the gathering rank"
+    g = _fixture(config)
+    if not np.array_equal(g["camera"].view(np.uint32), cam.blob.view(np.uint32)):
+        return False, "camera blob differs from the fixture's"
+    at = _fixture_at(g, frames)
+    if at is None:
+        return None, f"no fixture for {frames} frames"
+    sha, _, want, _ = at
+    img = image.detach().cpu().numpy()
+    if sha is not None:
+        return canon_sha(img) == sha, f"whole-image SHA-256 after {frames} frames"
+    return _pixels_same(img[g["py"], g["px"]], want), \
+        f"{want.shape[0]} sampled pixels after {frames} frames"
+
+
+def stripe_bands(height, rank, world):
+    """The global 8-row bands of `rank` (band b -> rank b % world), in local order."""
+    return list(range(rank, (height + ROWS - 1) // ROWS, world))
+
+
+def share_check(config, local, frames, bands):
+    """A rank's share (its local rows: global band bands[j] at local rows 8j..8j+7) against
+    the fixture: every band's digest when the fixture has per-band digests, else the sampled
+    pixels that fall in those bands.  None when no fixture covers the frame count."""
+    g = _fixture(config)
+    at = _fixture_at(g, frames)
+    if at is None:
+        return None
+    _, band_sha, want, _ = at
+    img = local.detach().cpu().numpy()
+    if band_sha is not None:
+        for j, b in enumerate(bands):
+            d = np.frombuffer(bytes.fromhex(canon_sha(img[ROWS * j:ROWS * (j + 1)])), np.uint8)
+            if not np.array_equal(d, band_sha[b]):
+                return False
+        return True
+    py, px = g["py"], g["px"]
+    where = {b: j for j, b in enumerate(bands)}
+    mine = np.array([int(y) // ROWS in where for y in py])
+    if not mine.any():
+        return None
+    ly = np.array([where[int(y) // ROWS] * ROWS + int(y) % ROWS for y in py[mine]])
+    return _pixels_same(img[ly, px[mine]], want[mine])
+
+
+def fixture_segments(config, frames):
+    at = _fixture_at(_fixture(config), frames)
+    return at[3] if at else None
+
+
+# ---- timing --------------------------------------------------------------------------
 def over_ranks(share, world):
     """share(rank) -> {"us_per_step", ...} for every rank of a world-size run, timed one after
     another on this GPU: the job's step is the slowest rank's (bench.py --gpus N takes the
-    max over ranks), so `us_per_step` is the max; each rank's own time and pixel check are
-    kept (rank_us, image_ok = every rank's share matches the fixture)."""
+    max over ranks), so `us_per_step` is the max; each rank's own time and check are kept."""
     per = [share(r) for r in range(world)]
     slow = max(range(world), key=lambda r: per[r]["us_per_step"])
     out = dict(per[slow])
+    us = [d["us_per_step"] for d in per]
     out.update({"us_per_step": per[slow]["us_per_step"], "max_over_ranks": True,
-                "slowest_rank": slow, "rank_us": [d["us_per_step"] for d in per],
-                "rank0_us": per[0]["us_per_step"],
+                "slowest_rank": slow, "rank_us": us, "rank0_us": per[0]["us_per_step"],
+                "rank_spread": round(max(us) / min(us) - 1.0, 4) if min(us) > 0 else None,
                 "image_ok": all(d["image_ok"] for d in per) if all(
                     d["image_ok"] is not None for d in per) else None})
     return out
 
 
-def driver_record_sides(device, stream, main_cfg, main_us):
-    """Side measurements for the driver's N=1 record (after the timed region), each with its
-    image check: the other per-dispatch config (K2 next to K3), one K5 64-spp step, and every
-    rank's 1/2, 1/4, 1/8 share of K3 (one update launch per frame, and frame chains) and K5
-    timed alone on this GPU — what each rank of `bench.py --gpus N` computes per step, the
-    slowest rank setting the step — so the strong-scaling curve has a per-rank measurement
-    behind it (tools/rank_sim.py's method)."""
-    out = {}
-    pipe = rt.ComputeShaderPipeline(device)
-    try:
-        def setup(cfg):
-            w, h, kind, nsph, depth, spf, _ = CONFIGS[cfg]
-            if spf == 1:
-                sc = rt.SphereCollection.generate(kind, nsph, 1)
-                seeds = rt.frame_seeds(FRAME_SEED, 25)
-                st = rt.CameraSettings(max_depth=depth, samples_per_pixel=BENCH_SPP)
-                cam = rt.SceneCamera.from_settings(st, w, h, float(seeds[0]))
-            else:
-                g = dict(np.load(GOLDEN / f"{cfg.lower()}.npz"))
-                sc, seeds, cam = rt.SphereCollection(g["spheres"]), g["seeds"], rt.SceneCamera(g["camera"])
-            return w, h, sc, seeds, cam
-
-        def dispatch_share(cfg, world, mode, rank=0, reps=5, warm_s=0.05):
-            # the driver's structure: 5 frames from a reset, then 20 timed (25-frame fixture),
-            # as each rank of bench.py --gpus N runs it after its warm-up: untimed frames on
-            # scratch images first (the share's lists, order and code, and warm_s of the same
-            # frames — the main line's --warm-ms: the host's image check of the previous side
-            # line leaves the GPU idle, and 5 ms of warm-up measured 0.3-0.8 us per step
-            # slower, DESIGN.md §7), then `reps` timed regions, each from a reset; the median
-            w, h, sc, seeds, cam = setup(cfg)
-            set_frame_launch(pipe, mode)
-            cam_t = cam.with_fields(camera_has_moved=0.0)
-            scratch = StripeRenderer(pipe, w, h, rank, world)
-            t_w = time.perf_counter()
-            while True:
-                scratch.frames(cam, sc, seeds[:20])
-                torch.cuda.synchronize()
-                if time.perf_counter() - t_w >= warm_s:
-                    break
-            del scratch
-            r = StripeRenderer(pipe, w, h, rank, world)
-            runs = []
-            for _ in range(reps):
-                r.frames(cam, sc, seeds[:5])
-                runs.append(timed(stream, lambda: r.frames(cam_t, sc, seeds[5:25])) / 20)
-            t = sorted(runs)[len(runs) // 2]
-            info = pipe.last_launch_info()
-            return {"us_per_step": round(t * 1e6, 2), "kernel": info["kernel_name"],
-                    "launches_per_step": round(info["launches"] / 20, 3),
-                    "runs_us": [round(x * 1e6, 2) for x in runs],
-                    "image_ok": share_pixels_ok(cfg, r.local, 25, world, rank)}
-
-        def k5_share(world, rank=0):
-            w, h, sc, seeds, cam = setup("K5")
-            pipe.set_frames_per_launch(0)
-            pipe.set_frame_images("last_two")
-            r = StripeRenderer(pipe, w, h, rank, world)
-            r.frames(cam, sc, seeds)                   # records the tile costs
-            r.frames(cam, sc, seeds)                   # builds the order (and its buffers)
-            # (each call restarts from the camera's reset; the median of five launches)
-            runs = sorted(timed(stream, lambda: r.frames(cam, sc, seeds)) for _ in range(5))
-            t = runs[2]
-            info = pipe.last_launch_info()
-            return {"us_per_step": round(t * 1e6, 1), "us_per_spp": round(t / 64 * 1e6, 2),
-                    "runs_us": [round(x * 1e6, 1) for x in runs],
-                    "kernel": info["kernel_name"],
-                    "image_ok": share_pixels_ok("K5", r.local, 64, world, rank)}
-
-        other = "K2" if main_cfg == "K3" else "K3"
-        d = dispatch_share(other, 1, "dispatch")
-        w, h = CONFIGS[other][:2]
-        out[other.lower()] = dict(d, Mrays_per_s=round(w * h / d["us_per_step"], 1),
-                                  hbm_frac=round(w * h * BYTES_PER_PIXEL_LAUNCH /
-                                                 (d["us_per_step"] * 1e3) / PEAK_HBM_GBS, 4),
-                                  what=f"{other}: 5 + 20 frames from a reset, one update "
-                                       f"launch per frame, µs per update by HIP events")
-        # K4: one 64-spp 1920x1080 render from a reset (fused frames), as --config K4 steps,
-        # the full-image SHA-256 of k4.npz
-        w4, h4, sc4, seeds4, cam4 = setup("K4")
-        pipe.set_frames_per_launch(0)
-        pipe.set_frame_images("last_two")
-        r4 = StripeRenderer(pipe, w4, h4, 0, 1)
-        for _ in range(2):
-            r4.frames(cam4, sc4, seeds4)               # costs recorded, order built
-        runs4 = sorted(timed(stream, lambda: r4.frames(cam4, sc4, seeds4)) for _ in range(5))
-        info4 = pipe.last_launch_info()
-        ok4, what4 = image_check("K4", r4.local[:h4], 64, cam4, w4, h4)
-        out["k4"] = {"us_per_step": round(runs4[2] * 1e6, 1),
-                     "us_per_frame": round(runs4[2] / 64 * 1e6, 2),
-                     "runs_us": [round(x * 1e6, 1) for x in runs4],
-                     "kernel": info4["kernel_name"], "launches_per_step": info4["launches"],
-                     "image_ok": ok4, "image_check": what4,
-                     "Mrays_per_s": round(w4 * h4 * 64 / (runs4[2] * 1e6), 1),
-                     "what": "K4: one 64-spp 1920x1080 render from a reset (fused frames, "
-                             "cost-ordered after two untimed renders), the median of five"}
-        del r4
-        k5 = k5_share(1)
-        out["k5"] = dict(k5, Mrays_per_s=round(3840 * 2160 * 64 / k5["us_per_step"], 1),
-                         what="one 64-spp 3840x2160 depth-8 step (one 64-frame bounce launch, "
-                              "cost-ordered by the steps before; the median of five), 512 "
-                              "sampled pixels")
-        shares = {"K3": {}, "K5": {}}
-        base = {"dispatch": main_us if main_cfg == "K3" else None}
-        for mode in ("dispatch", "chain"):
-            rows = {}
-            for world in (1, 2, 4, 8):
-                if world == 1 and mode == "dispatch" and base["dispatch"]:
-                    rows["1"] = {"us_per_step": round(base["dispatch"], 2), "kernel": "(the timed steps)"}
-                    continue
-                rows[str(world)] = over_ranks(
-                    lambda rk: dispatch_share("K3", world, mode, rk), world)
-            ref = rows["1"]["us_per_step"]
-            for k, v in rows.items():
-                v["predicted_efficiency"] = round(ref / (int(k) * v["us_per_step"]), 3)
-            shares["K3"][mode] = rows
-        # efficiency of each share against the 1-GPU step as the line times it
-        one = shares["K3"]["dispatch"]["1"]["us_per_step"]
-        for mode in ("dispatch", "chain"):
-            for k, v in shares["K3"][mode].items():
-                v["efficiency_vs_1gpu_step"] = round(one / (int(k) * v["us_per_step"]), 3)
-        k5rows = {"1": {"us_per_step": k5["us_per_step"], "us_per_spp": k5["us_per_spp"]}}
-        for world in (2, 4, 8):
-            k5rows[str(world)] = over_ranks(lambda rk: k5_share(world, rk), world)
-        for k, v in k5rows.items():
-            v["predicted_efficiency"] = round(k5["us_per_step"] / (int(k) * v["us_per_step"]), 3)
-        shares["K5"]["fused_64"] = k5rows
-        shares["what"] = ("every rank's stripe share (8-row bands dealt round-robin) timed alone "
-                          "on this GPU, i.e. each rank's step of bench.py --gpus N; us_per_step "
-                          "= the slowest rank's (max_over_ranks; rank_us lists them all); "
-                          "predicted_efficiency = the 1-rank time / (N x that time) in "
-                          "the same launch structure; K3 'dispatch' = one update launch per "
-                          "frame, 'chain' = fused launches writing every frame's image "
-                          "(--frame-launch auto takes chain for shares <= %d tiles)"
-                          % CHAIN_MAX_TILES)
-        out["rank_shares"] = shares
-    finally:
-        pipe.close()
-    return out
-
-
-def _unserializable(o):
-    """json default: a value the line cannot hold is named, not fatal (the line still
-    prints; the bad path shows in its place)."""
-    return f"<{type(o).__name__} {getattr(o, '__name__', '')}>"
-
-
 def timed_steps(run, sync, world, barrier=None, device=None, stamp=None, wait=None):
     """The timed region of the K steps.  Every rank leaves an opening barrier (then
-    synchronises), starts its clock, issues the steps (`run`), synchronises, and stops its
-    clock: its own wall time of the K steps.  The closing barrier follows outside that time
-    and is reported on its own (`barrier_s`), so that at N > 1 the value measures the render,
-    not the collective's latency (a 8-rank K3 step is ~3 µs, the same order as one barrier).
-    The job's time is the MAX over ranks (all ranks start together after the opening
-    barrier).  Returns {"dt": max over ranks, "per_rank": [s...], "issue": this rank's host
-    issue time, "barrier_s": max over ranks of the closing barrier}.  `stamp(name)` (optional)
-    is called at the start, when the issue returns and after the synchronise.  `wait`
-    (default: sync) is the closing wait of the steps; it must end in a synchronise."""
+    synchronises), reads CLOCK_MONOTONIC, issues the steps (`run`), synchronises (`wait`,
+    default sync) and reads the clock again.  At N > 1 the ranks' start and end stamps are
+    all-gathered and the job's time is max(end) - min(start): all ranks run on one host, so
+    one clock covers them, and the skew with which they leave the opening barrier stays
+    inside the job's time.  The closing barrier follows outside that time and is reported on
+    its own (`barrier_s`).  Returns {"dt": the job's time, "per_rank": [each rank's own
+    end - start], "max_rank_s": their max, "start_skew_s": max - min start, "issue": this
+    rank's host issue time, "barrier_s": max over ranks of the closing barrier}.
+    `stamp(name)` (optional) is called at the start, when the issue returns and after the
+    synchronise."""
     barrier = barrier or dist.barrier
     wait = wait or sync
+    clock = time.clock_gettime_ns
+    mono = time.CLOCK_MONOTONIC
     sync()
     if world > 1:
         barrier()
         sync()
     if stamp:
         stamp("t0")
-    t0 = time.perf_counter()
+    t0 = clock(mono)
     run()
-    t_issued = time.perf_counter()
+    t_issued = clock(mono)
     if stamp:
         stamp("issued")
     wait()
-    mine = time.perf_counter() - t0
+    t1 = clock(mono)
     if stamp:
         stamp("synced")
-    bar = 0.0
-    per_rank, bars = [mine], [0.0]
+    starts, ends, bars = [t0], [t1], [0]
     if world > 1:
-        tb = time.perf_counter()
+        tb = clock(mono)
         barrier()
         sync()
-        bar = time.perf_counter() - tb
-        t = torch.tensor([mine, bar], dtype=torch.float64, device=device)
+        bar = clock(mono) - tb
+        t = torch.tensor([t0, t1, bar], dtype=torch.int64, device=device)
         got = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(got, t)
-        per_rank = [float(g[0]) for g in got]
-        bars = [float(g[1]) for g in got]
-    return {"dt": max(per_rank), "per_rank": per_rank, "issue": t_issued - t0,
-            "barrier_s": max(bars)}
+        starts = [int(g[0]) for g in got]
+        ends = [int(g[1]) for g in got]
+        bars = [int(g[2]) for g in got]
+    per_rank = [(e - s) / 1e9 for s, e in zip(starts, ends)]
+    return {"dt": (max(ends) - min(starts)) / 1e9, "per_rank": per_rank,
+            "max_rank_s": max(per_rank), "start_skew_s": (max(starts) - min(starts)) / 1e9,
+            "issue": (t_issued - t0) / 1e9, "barrier_s": max(bars) / 1e9}
 
 
 class StreamGate:
     """--gate (diagnostic, never a measurement): the stream waits on a host-memory word
     (hipStreamWaitValue32) while the timed steps are issued, and the host opens it after the
-    issue, so that the GPU runs the steps back to back however slowly the host issues them —
-    under rocprofv3's kernel trace every dispatch costs the host ~8 µs more, which starves a
-    one-launch-per-frame chain and distorts the trace (tools/timeline.py).  Uses the HIP
+    issue, so that the GPU runs the steps back to back however slowly the host issues them
+    (under rocprofv3's kernel trace every dispatch costs the host ~8 µs more).  Uses the HIP
     runtime torch loaded (same soname)."""
 
     def __init__(self):
@@ -571,6 +444,8 @@ class StreamGate:
 
 
 def timed(stream, fn):
+    """HIP events on `stream` around fn(), seconds (the side lines' and the roofline's kernel
+    time; never inside the main timed region)."""
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     fn()
@@ -579,8 +454,226 @@ def timed(stream, fn):
     return e0.elapsed_time(e1) / 1e3
 
 
-def main():
-    args = parse()
+def wall(fn):
+    """Host wall clock around fn() and a synchronize, seconds (synchronized before)."""
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def runtime_floor_us(reps=50):
+    """The host's round trip to an idle GPU: one 1-element kernel (torch's fill) launched and
+    synchronized, median µs — the fixed cost any timed region of one launch pays."""
+    x = torch.zeros(1, device="cuda")
+    t = []
+    for _ in range(reps):
+        t.append(wall(lambda: x.fill_(1.0)))
+    return round(statistics.median(t) * 1e6, 2)
+
+
+def roofline(kernel, launch_s, bytes_launch, pmc, pmc_path, parts=1, extra=None):
+    """The roofline object of the timed kernel: HBM bytes moved against 8 TB/s, and — when a
+    PMC summary of that kernel instance is committed — the VALU issue it measured against
+    the VALU peak (then the bound: these kernels issue far more VALU than they move bytes)."""
+    gbs = bytes_launch / launch_s / 1e9
+    hbm = {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+           "frac": round(gbs / PEAK_HBM_GBS, 4),
+           "algorithmic_bytes_per_launch": int(bytes_launch),
+           "practical_floor_frac": round(gbs / RMW_FLOOR_GBS, 4)}
+    traffic = None
+    if pmc and "hbm_bytes_per_launch" in pmc:
+        traffic = pmc["hbm_bytes_per_launch"] * parts
+    roof = {"bound": "hbm", **hbm, "traffic": traffic, "kernel": kernel,
+            "kernel_avg_us": round(launch_s * 1e6, 2)}
+    if pmc and pmc.get("valu_insts_per_launch"):
+        insts = pmc["valu_insts_per_launch"] * parts
+        ach = insts * 64 / launch_s / 1e12
+        roof = {"bound": "valu", "achieved": round(ach, 3), "peak": round(PEAK_VALU_TOPS, 2),
+                "unit": "TOP/s (VALU lane-ops)",
+                "frac": round(insts * VALU_ISSUE_CYCLES / (SIMDS * CLOCK_GHZ * 1e9 * launch_s), 4),
+                "traffic": traffic, "kernel": kernel, "kernel_avg_us": round(launch_s * 1e6, 2),
+                "valu_insts_per_launch": insts, "pmc": pmc_path,
+                "rule": "frac = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x 2.4 GHz x "
+                        "kernel_avg_us); achieved = SQ_INSTS_VALU x 64 lanes / kernel_avg_us",
+                "hbm": hbm}
+    if extra:
+        roof.update(extra)
+    return roof
+
+
+# ---- side measurements of the N=1 record -----------------------------------------------
+def _setup(cfg):
+    w, h, kind, nsph, depth, spf, _ = CONFIGS[cfg]
+    if spf == 1:
+        sc = rt.SphereCollection.generate(kind, nsph, 1)
+        seeds = rt.frame_seeds(FRAME_SEED, 220)
+        st = rt.CameraSettings(max_depth=depth, samples_per_pixel=BENCH_SPP)
+        cam = rt.SceneCamera.from_settings(st, w, h, float(seeds[0]))
+    else:
+        g = _fixture(cfg)
+        sc, seeds, cam = rt.SphereCollection(g["spheres"]), g["seeds"], rt.SceneCamera(g["camera"])
+    return w, h, sc, seeds, cam
+
+
+def driver_record_sides(device, stream, main_cfg):
+    """Side measurements for the driver's N=1 record (after the timed region), each with its
+    image check:
+      dispatch     the main config with one update launch per frame (the reference's own
+                   structure), 5 + 20 frames, µs per update by events and wall, HBM fraction;
+      k2 / k3      the other per-update config the same way;
+      k4, k5       one 64-spp step each (K5: with segments/s);
+      rank_shares  every rank's share of K3 (frame chains, the main line's structure) and of
+                   K5 at 1 / 2 / 4 / 8 ranks timed alone on this GPU, WALL-CLOCK around the
+                   call and a synchronize as timed_steps times a rank, at the driver's 20
+                   steps and at bench.py's default 200; the job's step is the slowest rank's
+                   (max over ranks); efficiency against the 1-rank share timed the same way."""
+    out = {}
+    pipe = rt.ComputeShaderPipeline(device)
+    try:
+        def share_run(cfg, world, mode, rank=0, steps=20, reps=5, warm_s=0.05):
+            # reset + warm frames, then `steps` timed frames in one call, as each rank of
+            # bench.py --gpus N runs them after its warm-up (untimed frames on scratch images
+            # first: the share's lists, order and code, and warm_s of the same frames)
+            w, h, sc, seeds, cam = _setup(cfg)
+            set_frame_launch(pipe, mode)
+            cam_t = cam.with_fields(camera_has_moved=0.0)
+            lead = 5 if steps <= 20 else 20
+            scratch = StripeRenderer(pipe, w, h, rank, world)
+            t_w = time.perf_counter()
+            while True:
+                scratch.frames(cam, sc, seeds[:20])
+                torch.cuda.synchronize()
+                if time.perf_counter() - t_w >= warm_s:
+                    break
+            del scratch
+            r = StripeRenderer(pipe, w, h, rank, world)
+            walls, evs = [], []
+            for k in range(reps):
+                r.frames(cam, sc, seeds[:lead])
+                walls.append(wall(lambda: r.frames(cam_t, sc, seeds[lead:lead + steps])) / steps)
+            ok = share_check(cfg, r.local, lead + steps, stripe_bands(h, rank, world))
+            for k in range(3):
+                r.frames(cam, sc, seeds[:lead])
+                evs.append(timed(stream, lambda: r.frames(cam_t, sc, seeds[lead:lead + steps])) / steps)
+            info = pipe.last_launch_info()
+            t = statistics.median(walls)
+            return {"us_per_step": round(t * 1e6, 3),
+                    "events_us_per_step": round(statistics.median(evs) * 1e6, 3),
+                    "kernel": info["kernel_name"],
+                    "launches_per_step": round(info["launches"] / steps, 3),
+                    "wall_runs_us": [round(x * 1e6, 3) for x in walls],
+                    "image_ok": ok}
+
+        def k5_run(world, rank=0):
+            w, h, sc, seeds, cam = _setup("K5")
+            pipe.set_frames_per_launch(0)
+            pipe.set_frame_images("last_two")
+            r = StripeRenderer(pipe, w, h, rank, world)
+            r.frames(cam, sc, seeds)                   # records the tile costs
+            r.frames(cam, sc, seeds)                   # builds the order (and its buffers)
+            # (each call restarts from the camera's reset; wall-clock, the median of five)
+            runs = sorted(wall(lambda: r.frames(cam, sc, seeds)) for _ in range(5))
+            info = pipe.last_launch_info()
+            return {"us_per_step": round(runs[2] * 1e6, 1),
+                    "runs_us": [round(x * 1e6, 1) for x in runs],
+                    "kernel": info["kernel_name"],
+                    "image_ok": share_check("K5", r.local, 64, stripe_bands(h, rank, world))}
+
+        # the reference's structure (one launch per frame) for the main and the other config
+        other = "K2" if main_cfg == "K3" else "K3"
+        for cfg, key in ((main_cfg, "dispatch"), (other, other.lower())):
+            pipe.set_update_queues(0)
+            d = share_run(cfg, 1, "dispatch")
+            w, h = CONFIGS[cfg][:2]
+            ev = d["events_us_per_step"]
+            out[key] = dict(d, config=cfg, Mrays_per_s=round(w * h / d["us_per_step"], 1),
+                            hbm_frac_events=round(w * h * BYTES_PER_PIXEL_LAUNCH /
+                                                  (ev * 1e3) / PEAK_HBM_GBS, 4),
+                            what=f"{cfg}: 5 + 20 frames from a reset, one update launch per "
+                                 f"frame (the reference's dispatch structure); us_per_step wall "
+                                 f"(synchronize on both sides), events_us_per_step by HIP "
+                                 f"events; HBM: 32 B per pixel per update")
+        # K4: one 64-spp 1920x1080 render from a reset (fused frames)
+        w4, h4, sc4, seeds4, cam4 = _setup("K4")
+        pipe.set_frames_per_launch(0)
+        pipe.set_frame_images("last_two")
+        r4 = StripeRenderer(pipe, w4, h4, 0, 1)
+        for _ in range(2):
+            r4.frames(cam4, sc4, seeds4)               # costs recorded, order built
+        runs4 = sorted(wall(lambda: r4.frames(cam4, sc4, seeds4)) for _ in range(5))
+        info4 = pipe.last_launch_info()
+        ok4, what4 = image_check("K4", r4.local[:h4], 64, cam4)
+        out["k4"] = {"us_per_step": round(runs4[2] * 1e6, 1),
+                     "us_per_frame": round(runs4[2] / 64 * 1e6, 2),
+                     "runs_us": [round(x * 1e6, 1) for x in runs4],
+                     "kernel": info4["kernel_name"], "launches_per_step": info4["launches"],
+                     "image_ok": ok4, "image_check": what4,
+                     "Mrays_per_s": round(w4 * h4 * 64 / (runs4[2] * 1e6), 1),
+                     "what": "K4: one 64-spp 1920x1080 render from a reset (fused frames, "
+                             "cost-ordered after two untimed renders), wall, the median of five"}
+        del r4
+        k5 = k5_run(1)
+        segs5 = fixture_segments("K5", 64)
+        out["k5"] = dict(k5, Mrays_per_s=round(3840 * 2160 * 64 / k5["us_per_step"], 1),
+                         segments_per_s=(round(segs5 / (k5["us_per_step"] / 1e6), 1)
+                                         if segs5 else None),
+                         what="one 64-spp 3840x2160 depth-8 step (one 64-frame bounce launch, "
+                              "cost-ordered by the steps before), wall, the median of five")
+
+        # rank shares: the main line's structure (frame chains) at every N, wall-clock
+        shares = {}
+        for steps in (20, 200):
+            rows = {}
+            for world in (1, 2, 4, 8):
+                rows[str(world)] = over_ranks(
+                    lambda rk: share_run("K3", world, "chain", rk, steps=steps), world)
+            one = rows["1"]["us_per_step"]
+            for k, v in rows.items():
+                v["efficiency"] = round(one / (int(k) * v["us_per_step"]), 4)
+                if v.get("events_us_per_step"):
+                    v["events_efficiency"] = round(rows["1"]["events_us_per_step"] /
+                                                   (int(k) * v["events_us_per_step"]), 4)
+            shares[f"K3_chain_{steps}_steps"] = rows
+        # the fixed cost of one call: wall(steps) = fixed + steps * per_step, from the two
+        # step counts of the slowest rank
+        fixed = {}
+        for k in ("1", "2", "4", "8"):
+            a, b = (shares[f"K3_chain_{s}_steps"][k]["us_per_step"] for s in (20, 200))
+            per = (200 * b - 20 * a) / 180
+            fixed[k] = {"fixed_us": round(20 * a - 20 * per, 2), "per_step_us": round(per, 3)}
+        shares["K3_call_model"] = fixed
+        shares["runtime_floor_us"] = runtime_floor_us()
+        k5rows = {"1": {"us_per_step": k5["us_per_step"], "image_ok": k5["image_ok"]}}
+        for world in (2, 4, 8):
+            k5rows[str(world)] = over_ranks(lambda rk: k5_run(world, rk), world)
+        for k, v in k5rows.items():
+            v["efficiency"] = round(k5["us_per_step"] / (int(k) * v["us_per_step"]), 4)
+        shares["K5_fused_64"] = k5rows
+        shares["what"] = (
+            "every rank's stripe share (8-row bands dealt round-robin) timed alone on this GPU "
+            "in the main line's structure, each rank's step of bench.py --gpus N: us_per_step = "
+            "the slowest rank's (max_over_ranks; rank_us lists them all) wall-clock per step "
+            "(host clock around one call of the steps and a synchronize, the median of five "
+            "calls; events_us_per_step: HIP events, three more calls); efficiency = the 1-rank "
+            "time / (N x that time) in the same structure and step count; K3 at the driver's 20 "
+            "steps and at the default 200; K3_call_model: fixed_us + steps x per_step_us fitted "
+            "to the two; runtime_floor_us: one 1-element kernel launched and synchronized on "
+            "the idle GPU (the floor of any call's fixed cost); K5: one 64-spp step per call")
+        out["rank_shares"] = shares
+    finally:
+        pipe.close()
+    return out
+
+
+def _unserializable(o):
+    """json default: a value the line cannot hold is named, not fatal."""
+    return f"<{type(o).__name__} {getattr(o, '__name__', '')}>"
+
+
+def main(argv=None):
+    args = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -605,13 +698,13 @@ def main():
     if dispatch:
         # progressive frames: frame 0 resets, one seed per frame
         spheres = rt.SphereCollection.generate(kind, nsph, 1)
-        seeds = rt.frame_seeds(FRAME_SEED, args.warmup + args.steps + 5 * args.side)
+        seeds = rt.frame_seeds(FRAME_SEED, args.warmup + args.steps + 3 * args.side)
         settings = rt.CameraSettings(max_depth=depth, samples_per_pixel=BENCH_SPP)
         cam0 = rt.SceneCamera.from_settings(settings, w, h, float(seeds[0]))
         cam_t = cam0.with_fields(camera_has_moved=0.0)
     else:
         # every step renders the golden 64-spp image from a reset accumulator
-        g = dict(np.load(GOLDEN / f"{cfg.lower()}.npz"))
+        g = _fixture(cfg)
         spheres = rt.SphereCollection(g["spheres"])
         seeds = g["seeds"]
         cam0 = cam_t = rt.SceneCamera(g["camera"])
@@ -622,9 +715,7 @@ def main():
     pipe.set_spheres(spheres)
     launch_mode = None
     if dispatch:
-        # one `update` launch per frame, or (small rank shares) frame chains
-        launch_mode = frame_launch_mode(args.frame_launch, w,
-                                        rt.stripe_local_rows(h, rank, world))
+        launch_mode = args.frame_launch
         set_frame_launch(pipe, launch_mode)
     pipe.set_update_queues(args.queues)
     pipe.set_update_submit(args.submit)
@@ -638,44 +729,19 @@ def main():
     stream = torch.cuda.current_stream()
     local_px = w * min(r.rows, h)
 
-    def step_block(n, first):
+    def step_block(rend, n, first):
         if dispatch:
             off = 0 if first else args.warmup
-            r.frames(cam0 if first else cam_t, spheres, seeds[off:off + n])
+            rend.frames(cam0 if first else cam_t, spheres, seeds[off:off + n])
         else:
             for _ in range(n):
-                r.frames(cam0, spheres, seeds)
+                rend.frames(cam0, spheres, seeds)
 
-    # Cold start (N=1 side line, before anything else ran on the GPU in this process): the
-    # same W + K frames on scratch images, timed the same way — what the line's value would
-    # be without the warm-up below.
-    cold_start = None
-    if args.side > 0 and world == 1 and dispatch:
-        cr = StripeRenderer(pipe, w, h, rank, world, comm=None)
-        torch.cuda.synchronize()
-        if args.warmup:
-            cr.frames(cam0, spheres, seeds[:args.warmup])
-        torch.cuda.synchronize()
-        tc0 = time.perf_counter()
-        t_cold = timed(torch.cuda.current_stream(), lambda: cr.frames(
-            cam0 if args.warmup == 0 else cam_t, spheres,
-            seeds[args.warmup:args.warmup + args.steps]))
-        dt_cold = time.perf_counter() - tc0
-        ok, what = image_check(cfg, cr.local, args.warmup + args.steps, cam0, w, h)
-        cold_start = {"us_per_step_events": round(t_cold / args.steps * 1e6, 2),
-                "us_per_step_wall": round(dt_cold / args.steps * 1e6, 2),
-                "Mrays_per_s": round(w * h * args.steps / dt_cold / 1e6, 1),
-                "image_ok": ok, "image_check": what,
-                "what": "the same warmup + steps frames on scratch images at process start, "
-                        "before the --warm-ms warm-up (wall: synchronize on both sides)"}
-        del cr
     # Warm-up (untimed, scratch images): a progressive render's steps run back to back in a
-    # process that has long been issuing them; a 20-step timed region (~0.4 ms) right after
-    # process start would otherwise time the chip's start from idle (K3: 22.2 against 16.2 µs
-    # per update, profiles/r03/r03w_driver_warm.log; not the waves' clock, 1.83 GHz cold and 1.88
-    # warm, profiles/r03/r03zb_stamps_single_k3_*.jsonl, nor the host's issue rate,
-    # profiles/r03/r03zc_driver_cold_warm_hip_aql.log).  The same frames on
-    # separate images: the timed images, their counts and the fixture check are untouched.
+    # process that has long been issuing them; a 20-step timed region (~0.3 ms) right after
+    # process start would otherwise time the chip's start from idle.  The same
+    # frames on separate images: the timed images, their counts and the fixture check are
+    # untouched.
     warm_s = 0.0
     if args.warm_ms > 0:
         scratch = StripeRenderer(pipe, w, h, rank, world, comm=None)
@@ -688,19 +754,12 @@ def main():
         del scratch
     # warmup (untimed); the dispatch configs' frame 0 resets the accumulator
     if args.warmup:
-        step_block(args.warmup, True)
+        step_block(r, args.warmup, True)
         # one untimed gather + de-interleave: RCCL sets up its point-to-point connections
         # and the de-interleave kernel's code object loads on first use, neither of which
-        # belongs to a step (the timed region still ends with the job's own gather)
+        # belongs to a step (the job's own gather follows the timed steps)
         r.finish()
-    # (HIP events created before the timed region: their creation is host work, not steps)
-    ev0, ev1, ev2, ev3 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
-    for e in (ev0, ev1, ev2, ev3):
-        e.record(stream)      # (torch creates an event at its first record: not in the region)
 
-    # timed: K steps issued by rt_update_frames (timed_steps: opening barrier, each rank's
-    # own clock around its steps and synchronize, the max over ranks; the closing barrier
-    # reported apart)
     host_t = {} if os.environ.get("RT_TIMELINE") is not None else None   # tools/timeline.py
 
     def stamp(name):
@@ -712,104 +771,88 @@ def main():
     def run():
         if gate:
             gate.hold(stream)
-        ev0.record(stream)
         try:
-            step_block(args.steps, args.warmup == 0)
+            step_block(r, args.steps, args.warmup == 0)
         finally:
             if gate:
                 gate.release()
-        ev1.record(stream)
 
+    # timed: the K steps (timed_steps: opening barrier, CLOCK_MONOTONIC around each rank's
+    # steps and synchronize, the job's time max(end) - min(start); the closing barrier apart)
     red_dev = "cuda" if backend == "nccl" else "cpu"
     ts = timed_steps(run, torch.cuda.synchronize, world, device=red_dev,
                      stamp=stamp if host_t is not None else None)
     dt = ts["dt"]
     info = pipe.last_launch_info()             # the last timed rt_update_frames call
     # the job's one gather of the finished tiles, timed on its own (barrier on both sides)
+    e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t1 = time.perf_counter()
-    ev2.record(stream)
+    e2.record(stream)
     image = r.finish()
-    ev3.record(stream)
+    e3.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt_gather = time.perf_counter() - t1
-    render_s, gather_s = ev0.elapsed_time(ev1) / 1e3, ev2.elapsed_time(ev3) / 1e3
+    gather_s = e2.elapsed_time(e3) / 1e3
     if world > 1:
-        t = torch.tensor([dt, render_s, gather_s, dt_gather], dtype=torch.float64,
-                         device=red_dev)
+        t = torch.tensor([gather_s, dt_gather], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, render_s, gather_s, dt_gather = (float(x) for x in t.tolist())
+        gather_s, dt_gather = (float(x) for x in t.tolist())
     frames_total = (args.warmup + args.steps) if dispatch else spf
-    image_ok, image_what = image_check(cfg, image, frames_total, cam0, w, h)
-    # this rank's per-tile candidate lists of the timed camera (a tile with more than
-    # kCandMax = 19 candidates has none: its camera rays scan the whole scene, same pixels)
+    image_ok, image_what = image_check(cfg, image, frames_total, cam0)
+    share_ok = share_check(cfg, r.local, frames_total, stripe_bands(h, rank, world))
+    if world > 1:
+        flag = torch.tensor([{True: 1, False: 0, None: 2}[share_ok]], dtype=torch.int32,
+                            device=red_dev)
+        got = [torch.zeros_like(flag) for _ in range(world)]
+        dist.all_gather(got, flag)
+        vals = [int(g[0]) for g in got]
+        share_ok = None if 2 in vals else all(v == 1 for v in vals)
     cand_stats = pipe.candidate_stats()
 
-    # dispatch configs: the timed steps are ONE rt_update_frames call (one launch per
-    # frame); 64-spp configs: one call per step, all alike
+    # the roofline's kernel time: HIP events over an identical repetition of the timed call
+    # (a scratch renderer, the same reset and frames), never inside the timed region
+    rep = StripeRenderer(pipe, w, h, rank, world, comm=None)
+    if dispatch:
+        step_block(rep, args.warmup, True)
+    rep_s = timed(stream, lambda: step_block(rep, args.steps, args.warmup == 0))
+    rep_info = pipe.last_launch_info()
+    del rep
     total_launches = info["launches"] * (1 if dispatch else args.steps)
     launches_per_step = total_launches / args.steps
-    # a one-frame update may run as `queues` concurrent launches (parts of the image on
-    # their own streams): the roofline's unit is then the update, all its parts together
     queues = max(1, info.get("queues", 1))
-    launch_s = ev0.elapsed_time(ev1) / 1e3 / max(1, total_launches // queues)
+    launch_s = rep_s / max(1, total_launches // queues)
     value = w * h * spf * args.steps / dt / 1e6
 
-    # roofline of the timed trace kernel
     kernel = info["kernel_name"]
     fpl = info["max_frames_per_launch"]
-    bytes_launch = local_px * BYTES_PER_PIXEL_LAUNCH
-    ref_bytes_launch = bytes_launch
     if launch_mode == "chain":
-        # a frame chain carries fpl progressive updates but keeps the accumulator in
-        # registers between them: it reads the input once (16 B per pixel) and writes every
-        # frame's image (16 B per pixel per frame).  The reference's 32 B per pixel per frame
-        # (a load and a store per dispatch) is reported beside it, not as `achieved`.
+        # a frame chain carries fpl progressive updates, the accumulator in registers between
+        # them: it reads the input once (16 B per pixel) and writes every frame's image (16 B
+        # per pixel per frame)
         bytes_launch = local_px * (16 * fpl + 16)
-        ref_bytes_launch = local_px * BYTES_PER_PIXEL_LAUNCH * fpl
+    elif dispatch:
+        bytes_launch = local_px * BYTES_PER_PIXEL_LAUNCH
+    else:
+        # 64-spp steps: one read and the last two frames' images per launch
+        bytes_launch = local_px * 16 * 3
     pmc, pmc_path = load_pmc(cfg, kernel, fpl, queues) if world == 1 else (None, None)
-    wgt, wgt_path = load_weighted(cfg, kernel, pmc_path) if pmc else (None, None)
-    # (a summary's counts are per launch, i.e. per concurrent part: times the parts per update)
     pq = pmc.get("queues", 1) if pmc else 1
-    roof = {"bound": "hbm", "achieved": round(bytes_launch / launch_s / 1e9, 1),
-            "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(bytes_launch / launch_s / 1e9 / PEAK_HBM_GBS, 4),
-            "traffic": pmc["hbm_bytes_per_launch"] * pq if pmc and "hbm_bytes_per_launch" in pmc
-                       else None,
-            "kernel": kernel, "kernel_avg_us": round(launch_s * 1e6, 2),
-            "frames_per_launch": fpl, "launches_per_step": launches_per_step,
-            "queues": queues, "submit": info.get("submit"),
-            "algorithmic_bytes_per_launch": bytes_launch,
-            "reference_bytes_per_launch": ref_bytes_launch,
-            "binding": "valu",
-            # the same bytes against the measured streaming floor of the pattern (no tracing)
-            "practical_hbm": {"floor_GBs": RMW_FLOOR_GBS,
-                              "frac": round(bytes_launch / launch_s / 1e9 / RMW_FLOOR_GBS, 4),
-                              "source": "tools/rmw_floor.hip, profiles/archive/r02_rmw_floor.jsonl"}}
-    if pmc and pmc.get("valu_insts_per_launch"):
-        insts = pmc["valu_insts_per_launch"] * pq
-        avail = SIMDS * CLOCK_GHZ * 1e9 * launch_s
-        roof["valu"] = {"insts_per_launch": insts,
-                        "issue_cycles": insts * VALU_ISSUE_CYCLES,
-                        "available_cycles": round(avail),
-                        "frac": round(insts * VALU_ISSUE_CYCLES / avail, 4),
-                        "pmc": pmc_path,
-                        "rule": "VALU wave-instructions x 2 cycles / (1024 SIMDs x 2.4 GHz x "
-                                "kernel_avg_us)"}
-        if wgt:
-            # each PMC instruction class priced at the measured issue cost of the kernel's
-            # own forms of that class (profiles/r0*_valu_rates.txt): the SIMD cycles the
-            # VALU work holds, against what 1024 SIMDs offer at the 2.4-GHz peak clock
-            wc = wgt["weighted_cycles"] * pq
-            roof["valu"].update({
-                "weighted_cycles": wc, "weighted_frac": round(wc / avail, 4),
-                "weighted_frac_bounds": [round(b * pq / avail, 4)
-                                         for b in wgt["weighted_cycles_bounds"]],
-                "mean_cycles_per_valu": wgt["mean_cycles_per_valu"], "weighted": wgt_path})
-            roof["binding_frac"] = roof["valu"]["weighted_frac"]
+    roof = roofline(kernel, launch_s, bytes_launch, pmc, pmc_path, pq,
+                    {"frames_per_launch": fpl, "launches_per_step": launches_per_step,
+                     "queues": queues, "submit": info.get("submit"),
+                     "events_repetition": {"us_per_step": round(rep_s / args.steps * 1e6, 3),
+                                           "kernel": rep_info["kernel_name"]}})
 
+    segs = fixture_segments(cfg, frames_total)
+    if dispatch and depth == 1:
+        seg_step = w * h            # one sphere_list_hit per camera ray at max_depth 1
+    elif segs:
+        seg_step = segs             # one step = the fixture's 64-spp render
+    else:
+        seg_step = None
     line = {
         "metric": BASELINE["metric"],
         "value": round(value, 2),
@@ -833,20 +876,20 @@ def main():
                    "frame_launch": launch_mode or "fused_64",
                    "step": ("one progressive update (1 spp) of every pixel of the rank's "
                             "bands; " + {"dispatch": "one update launch per frame",
-                                         "chain": "the steps' frames in fused launches, every "
+                                         "chain": "the K steps' frames in fused launches, every "
                                                   "frame's image written",
                                          None: "64 frames per step"}[launch_mode])},
         "roofline": roof,
+        "segments_per_s": (round(seg_step * args.steps / dt, 1) if seg_step else None),
         "image_ok": image_ok,
         "image_check": image_what,
-        # max over ranks: the K steps by HIP events; each rank's own wall time of its K steps
-        # (value's time is their max); the closing barrier after them, outside value
-        "timed_breakdown_ms": {"steps": round(render_s * 1e3, 4),
-                               # host time of the steps' issue (this rank): the call returned
-                               "host_issue": round(ts["issue"] * 1e3, 4),
+        "share_ok": share_ok,
+        "timed_breakdown_ms": {"job": round(dt * 1e3, 4),
+                               "max_rank": round(ts["max_rank_s"] * 1e3, 4),
                                "per_rank_ms": [round(x * 1e3, 4) for x in ts["per_rank"]],
+                               "start_skew": round(ts["start_skew_s"] * 1e3, 4),
+                               "host_issue": round(ts["issue"] * 1e3, 4),
                                "barrier_ms": round(ts["barrier_s"] * 1e3, 4)},
-        # the job's output collection after the timed steps, and the job-level rate with it
         "gather": {"how": gather_how, "wall_ms": round(dt_gather * 1e3, 4),
                    "events_ms": round(gather_s * 1e3, 4),
                    "bytes_to_root": 16 * w * r.rows0 * (world - 1)},   # (padded bands)
@@ -854,16 +897,9 @@ def main():
                 "Mrays_per_s": round(w * h * spf * args.steps / (dt + dt_gather) / 1e6, 2),
                 "what": "the K steps plus the one gather of the finished tiles"},
         "candidate_lists": cand_stats,
-        "warm_up": {"ms": round(warm_s * 1e3, 2), "steps": args.warmup,
-                    "what": "untimed update frames on scratch images before the warmup steps "
-                            "(--warm-ms): the timed steps are a running render's, not a "
-                            "freshly started process's first launches"},
+        "warm_up": {"ms": round(warm_s * 1e3, 2), "steps": args.warmup},
     }
-
     if host_t is not None:
-        # host clocks (CLOCK_MONOTONIC, CLOCK_BOOTTIME ns) at the timed region's start, when
-        # the steps' issue returned, and after the closing synchronize: tools/timeline.py
-        # places them on a rocprofv3 trace of the same run
         line["timeline_host"] = host_t
 
     # ---- side measurements (after the timed region and its image check) -------------
@@ -883,33 +919,6 @@ def main():
                 "achieved": round(flops / t_exh / 1e12, 3), "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(flops / t_exh / 1e12 / PEAK_FP32_TFLOPS, 4),
                 "flop_per_frame": flops}
-            # the same frames fused (up to 64 per launch; K4's launches, the last two
-            # frames' images written), after one untimed fused call that records the tile
-            # costs the fused instances order by (the dispatch steps record none); then as a
-            # frame chain writing every frame's image (what rank shares run)
-            set_frame_launch(pipe, "dispatch")
-            pipe.set_frames_per_launch(0)
-            s1 = base + args.side
-            r.frames(cam_t, spheres, seeds[s1:s1 + args.side])
-            s1 += args.side
-            t_f = timed(stream, lambda: r.frames(cam_t, spheres, seeds[s1:s1 + args.side]))
-            fi = pipe.last_launch_info()
-            set_frame_launch(pipe, "chain")
-            s2 = s1 + args.side
-            t_c = timed(stream, lambda: r.frames(cam_t, spheres, seeds[s2:s2 + args.side]))
-            ci = pipe.last_launch_info()
-            set_frame_launch(pipe, launch_mode)
-            side["fused_frames"] = {"kernel": fi["kernel_name"],
-                                    "frames_per_launch": fi["max_frames_per_launch"],
-                                    "us_per_frame": round(t_f / args.side * 1e6, 2),
-                                    "Mrays_per_s": round(local_px * args.side / t_f / 1e6, 1),
-                                    "what": "the last two frames' images written per launch"}
-            side["chain_frames"] = {"kernel": ci["kernel_name"],
-                                    "frames_per_launch": ci["max_frames_per_launch"],
-                                    "us_per_frame": round(t_c / args.side * 1e6, 2),
-                                    "Mrays_per_s": round(local_px * args.side / t_c / 1e6, 1),
-                                    "what": "every frame's image written (rt_set_frame_images "
-                                            "EVERY): the structure of the rank shares' steps"}
             # moving camera: every frame a new camera (the reference's WASD movement resets
             # the accumulator, camera.rs:243-252, wgsl:345-350): candidate lists rebuilt
             # every frame, one update dispatch each
@@ -944,14 +953,11 @@ def main():
                                      "achieved": round(w * h * 20 / t_p / 1e9, 1),
                                      "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                      "frac": round(w * h * 20 / t_p / 1e9 / PEAK_HBM_GBS, 4)}
-        if cold_start is not None:
-            side["cold_start"] = cold_start
         if dispatch and depth == 1:
-            # K2 / K5 / rank shares: each with its image check
+            # the dispatch structure, K2 / K4 / K5, rank shares: each with its image check
             # (a side measurement that fails is reported in the line, never costs the line)
             try:
-                side.update(driver_record_sides(device, stream, cfg,
-                                                render_s / args.steps * 1e6))
+                side.update(driver_record_sides(device, stream, cfg))
             except Exception as e:          # noqa: BLE001
                 torch.cuda.synchronize()
                 side["side_error"] = f"{type(e).__name__}: {e}"[:400]

@@ -49,9 +49,10 @@ struct rt_ctx {
     // |R| lies in [2^-20, 2^20]: the scene half of camera_rays_bounded
     double scene_bound = 0.0;
     bool radii_ok = true;
-    // every radius's rcp_refined is RN32(1 / R) (rt_rcp_check_kernel; TraceParams::normal_rn)
+    // one Markstein step from rcp_refined(R) is the IEEE division by every distinct radius
+    // (rt_rcp_check_kernel, exhaustive over the numerators; TraceParams::normal_rn)
     bool normal_rn = false;
-    uint32_t* d_flag = nullptr;     // the check's result word
+    uint32_t* d_flag = nullptr;     // the check's result word, then up to kRcpRadii radii
     // XZ grid of the small spheres for bounce rays (build_grid; TraceParams
     // grid_*): device arrays and the parameters copied into every launch.
     void* d_grid = nullptr;  // cell ranges (uint2), item records (float4), item indices, big list
@@ -491,18 +492,40 @@ rt_status upload_spheres(rt_ctx* ctx, const rt_sphere* spheres, uint32_t count,
         e = hipMemcpyAsync(ctx->d_sph, spheres, count * sizeof(rt_sphere),
                            hipMemcpyHostToDevice, stream);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(sphere records)");
-        // the device's refined reciprocal of every radius against the IEEE division
+        // the hit normal's one-step division by each distinct radius, checked on the device
+        // against the IEEE division for every numerator significand (2^24 divisions per
+        // radius); scenes with more than kRcpRadii distinct radii keep the two-step form.
         // (RT_NORMAL_RN=0 in the environment turns the Markstein normal off: a test switch)
-        if (!ctx->d_flag) {
-            e = hipMalloc(&ctx->d_flag, sizeof(uint32_t));
-            if (e != hipSuccess) return hip_fail(e, "hipMalloc(check flag)");
-        }
+        constexpr size_t kRcpRadii = 16;
+        std::vector<float> radii(count);
+        for (uint32_t i = 0; i < count; ++i) radii[i] = spheres[i].radius;
+        std::sort(radii.begin(), radii.end(), [](float a, float b) {
+            uint32_t x, y;
+            std::memcpy(&x, &a, 4);
+            std::memcpy(&y, &b, 4);
+            return x < y;
+        });
+        radii.erase(std::unique(radii.begin(), radii.end(), [](float a, float b) {
+                        return std::memcmp(&a, &b, 4) == 0;
+                    }), radii.end());
         uint32_t bad = 1u;
-        e = hipMemsetAsync(ctx->d_flag, 0, sizeof(uint32_t), stream);
-        if (e == hipSuccess) e = rtk::launch_rcp_check(ctx->d_sph, count, ctx->d_flag, stream);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(&bad, ctx->d_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream);
-        if (e != hipSuccess) return hip_fail(e, "radius reciprocal check");
+        if (radii.size() <= kRcpRadii) {
+            if (!ctx->d_flag) {
+                e = hipMalloc(&ctx->d_flag, sizeof(uint32_t) * (1 + kRcpRadii));
+                if (e != hipSuccess) return hip_fail(e, "hipMalloc(check flag)");
+            }
+            float* d_radii = reinterpret_cast<float*>(ctx->d_flag + 1);
+            e = hipMemsetAsync(ctx->d_flag, 0, sizeof(uint32_t), stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(d_radii, radii.data(), radii.size() * sizeof(float),
+                                   hipMemcpyHostToDevice, stream);
+            if (e == hipSuccess)
+                e = rtk::launch_rcp_check(d_radii, (uint32_t)radii.size(), ctx->d_flag, stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(&bad, ctx->d_flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   stream);
+            if (e != hipSuccess) return hip_fail(e, "radius reciprocal check");
+        }
         e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
         const char* env = std::getenv("RT_NORMAL_RN");

@@ -118,13 +118,13 @@ struct TraceParams {
     // has tiles * split workgroups and those past the count exit at once
     const uint32_t* unit_order;
     const uint32_t* unit_count;
-    // 1: rcp_refined(R) == RN32(1 / R) for every sphere's radius (rt_rcp_check_kernel at
-    // upload), so the hit normal's (p - C) / R is one Markstein step per component
+    // 1: one Markstein step from rcp_refined(R) is the IEEE (p - C) / R for every radius of
+    // the scene (rt_rcp_check_kernel at upload: exhaustive over the numerators' significands)
     uint32_t normal_rn;
     uint32_t hint_frames;  // 0 = no hint
     uint32_t hint_n[kHintFrames];
     // RN32(1 / f32(hint_n[f] + 1)): the accumulator's division by f32(n + 1) as a Markstein
-    // division (rtd::div_rn; exact for n + 1 <= 2^24 on the checked domain)
+    // division (rtd::div_rn; exact for integer n + 1 < 2^22, rt_kernels.hip kAccRnMax)
     float hint_rcp[kHintFrames];
     float4 hint_rs[kHintEntries];
     uint32_t seed_b[kMaxFramesPerLaunch];
@@ -255,8 +255,8 @@ hipError_t launch_unit_order(const uint32_t* tile_cost, uint32_t* unit_order,
                              uint32_t split, float k_thr, hipStream_t stream);
 // Exact fast-path self-test (rt_selftest_fastmath): cnt[5] device counters, zeroed.
 hipError_t launch_selftest(unsigned long long* cnt, uint64_t n_rand, hipStream_t stream);
-// bad[0] |= 1 unless rcp_refined(R) is the correctly rounded 1 / R for every sphere's radius
-hipError_t launch_rcp_check(const float4* sph, uint32_t count, uint32_t* bad,
-                            hipStream_t stream);
+// bad[0] |= 1 unless div_rn(a, R, rcp_refined(R)) == a / R for every numerator significand
+// (binades 2^0 and 2^-100) and each of the n distinct radii (device array)
+hipError_t launch_rcp_check(const float* radii, uint32_t n, uint32_t* bad, hipStream_t stream);
 
 }  // namespace rtk

@@ -252,8 +252,8 @@ constexpr bool kStoreEach = is_list_kernel(kScan);
 // division by k = f32(n + 1) with y = RN32(1 / k) from the host (acc_rn: a multiply and two
 // fmas per channel; round 5, against round 2's RN32(num * RN64(1 / k)), acc_f64: two
 // conversions and an f64 multiply per channel, each a 4-cycle VALU form).  Exactness: for
-// an integer k <= 2^24, div_rn (rt_device.h) returns the IEEE quotient whenever num and the
-// quotient are normal; numerators in (0, 2^-102) could give subnormal quotients and take the
+// an integer k < 2^22 (kAccRnMax below), div_rn (rt_device.h) returns the IEEE quotient
+// whenever num and the quotient are normal; numerators in (0, 2^-102) could give subnormal quotients and take the
 // IEEE division (acc_ok: one unsigned compare per channel on the bit patterns; zero passes).
 // Zero, inf and NaN numerators need no exclusion in this use: num = col - c with the sample
 // colour col finite (|col| <= 1: a product of albedos in [0, 1] and the sky's [0.5, 1]) or
@@ -262,6 +262,12 @@ constexpr bool kStoreEach = is_list_kernel(kScan);
 // both (inf - inf); NaN propagates through both.  rt_selftest_fastmath replays it on random
 // accumulators and colours.
 constexpr uint32_t kBits2m102 = 0x0C800000u;   // 2^-102
+// The Markstein step by k = f32(n + 1) is the IEEE quotient for integer k < 2^22 even where
+// q = RN(num y) is 1.5 ulp off (Markstein's hypothesis needs one): num - mid k is a nonzero
+// multiple of ulp(num / k) / 2 for every rounding midpoint mid, so |num / k - mid| >=
+// ulp / (2 k) > 2^-23 ulp, more than the corrected quotient's error |q - num / k| |k y - 1|
+// <= 1.5 ulp 2^-24 (round-5 ADVICE).  Counts of 2^22 or more take the IEEE division.
+constexpr uint32_t kAccRnMax = 1u << 22;
 __device__ __forceinline__ bool acc_ok(v3 num) {
     // |x| >= 2^-102 or x == +-0 (NaN, inf pass): one unsigned compare per channel
     return min(min(abs_bits(num.x) - 1u, abs_bits(num.y) - 1u), abs_bits(num.z) - 1u) >=
@@ -798,10 +804,11 @@ __device__ __forceinline__ v3 normalize_w(v3 v) {
 // come from the host-computed hint_rs table instead of three hashes, a sqrt and a sincos
 // per lane.
 // The hit normal's (p - C) / R (wgsl:209) on div_core's domain (the callers check it),
-// y = rcp_refined(R).  rn (wave-uniform, TraceParams::normal_rn): y is RN32(1 / R) — checked
-// for every radius of the scene on the device at upload (rt_rcp_check_kernel) — so one
-// Markstein step per component is the IEEE quotient (div_rn: the numerators >= 2^-100, R in
-// [2^-20, 2^20] and |p - C| <= 2^43 keep the quotients normal); otherwise div_core's two.
+// y = rcp_refined(R).  rn (wave-uniform, TraceParams::normal_rn): one Markstein step per
+// component from y is the IEEE quotient for every numerator of the domain (the numerators
+// >= 2^-100, R in [2^-20, 2^20] and |p - C| <= 2^43 keep the quotients normal) — checked
+// exhaustively for every distinct radius of the scene on the device at upload
+// (rt_rcp_check_kernel); otherwise div_core's two.
 __device__ __forceinline__ v3 normal_div(v3 rel, float r, float y, bool rn) {
     if (rn) return mk(div_rn(rel.x, r, y), div_rn(rel.y, r, y), div_rn(rel.z, r, y));
     return mk(div_core(rel.x, r, y), div_core(rel.y, r, y), div_core(rel.z, r, y));
@@ -1090,7 +1097,7 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
                 if (nb < spp) {                                   // wgsl:352-358
                     const v3 num = sub(col, c);
                     // num / f32(nb + 1) (wgsl:356) as a Markstein division (acc_rn)
-                    if (nb < (1u << 24) &&
+                    if (nb < kAccRnMax &&
                         rt_ballot(tc.valid && !acc_ok(num)) == 0ull) {
                         c = acc_rn(c, num, (float)(nb + 1u), p.hint_rcp[fj]);
                     } else {
@@ -1788,7 +1795,7 @@ __device__ __forceinline__ void single_body(
             any_pending = any_pending || pending[s];
             if (ng < spp) {                                       // wgsl:352-357
                 const v3 num = sub(col[s], c[s]);
-                if (ng < (1u << 24) &&
+                if (ng < kAccRnMax &&
                     (mask_ult(acc_min_bits(num), kBits2m102 - 1u) & valid_m[s]) == 0ull) {
                     c[s] = acc_rn(c[s], num, (float)(ng + 1u), p.rcp_hint);
                 } else {
@@ -2080,7 +2087,7 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
                         if (acc_frame) {
                             const v3 num = sub(cj, cs);
                             // num / f32(nb + 1) (wgsl:356) as a Markstein division (acc_rn)
-                            if (nb < (1u << 24) &&
+                            if (nb < kAccRnMax &&
                                 rt_ballot(tc[s].valid && !acc_ok(num)) == 0ull) {
                                 cs = acc_rn(cs, num, (float)(nb + 1u), p.hint_rcp[fj]);
                             } else {
@@ -2927,8 +2934,9 @@ __global__ __launch_bounds__(256) void rt_present_kernel(const float4* __restric
 //         |b| in [2^-20, 2^33), |a| in [2^-100, 2^91), exponent gap in [-120, 88]; a also
 //         +-0, b also the accumulator's n + 1 up to 2^32) and over [2^-40, 2^40]^2;
 //         div_rn (y = RN32(1 / b)) vs a / b beyond integer denominators (|b| in
-//         [2^-20, 2^20], |a| in [2^-100, 2^43]); and acc_rn vs c + num / k for numerators acc_ok accepts
-//         (finite f32 bits or NaN, many near the subnormal range) and k in [1, 2^24].
+//         [2^-20, 2^20], |a| in [2^-100, 2^43], where |b y - 1| <= 2^-25; half of them with
+//         both significands near 2); and acc_rn vs c + num / k for numerators acc_ok accepts
+//         (finite f32 bits or NaN, many near the subnormal range) and k in [1, 2^22).
 // cnt[2]: sqrt_core vs sqrtf on every finite x >= 2^-96 (exhaustive).
 // cnt[3]: consider_fast vs consider (root selection, tmax and index) on random rays and
 //         spheres of the camera-ray domain (|d|^2 in [2^-11, 2^20], |O|, |C| + |R| <= 2^39),
@@ -3027,15 +3035,26 @@ __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cn
             if (dd <= 0x1p40f && (dy == 0.0f || fabsf(dy) >= 0x1p-100f))
                 bad1 += !same_bits(div_core(dy, len, y), dy / sqrtf(dd));
         }
-        {   // div_rn with real denominators (the Markstein step's general domain)
-            const float rb = with_exp(r1, -20 + (int)(r2 % 41u));
-            const float ra = with_exp(r0 ^ r2, -100 + (int)((r2 >> 8) % 144u));
-            bad1 += !same_bits(div_rn(ra, rb, 1.0f / rb), ra / rb);
+        {   // div_rn with real denominators where Markstein's hypothesis holds: y = RN32(1 / b)
+            // and |b y - 1| <= 2^-25, so q = RN(a y) is within an ulp of a / b; every other
+            // case the kernels' callers rule out (the radii are checked exhaustively at
+            // upload, rt_rcp_check_kernel; the accumulator's k is an integer < 2^22).  Half
+            // the cases in the corner where |b y - 1| approaches 2^-24: divisor significands
+            // in [1.99, 2), numerator significands within 2^-11 of 2.
+            const bool corner = (r2 >> 20) & 1u;
+            const uint32_t mb = corner ? 0x7EB852u + r1 % (0x800000u - 0x7EB852u) : r1;
+            const uint32_t ma = corner ? 0x7FFFFFu - (r0 % 4096u) : (r0 ^ r2);
+            const float rb = with_exp((r1 & 0x80000000u) | (mb & 0x7FFFFFu), -20 + (int)(r2 % 41u));
+            const float ra = with_exp((r0 & 0x80000000u) | (ma & 0x7FFFFFu),
+                                      -100 + (int)((r2 >> 8) % 144u));
+            const float yb = 1.0f / rb;
+            if (fabsf(fmaf(rb, yb, -1.0f)) <= 0x1p-25f)
+                bad1 += !same_bits(div_rn(ra, rb, yb), ra / rb);
         }
         // the accumulator's Markstein division: any finite f32 numerator or NaN (r0's bits:
         // zeros and subnormals included; the kernels' num = col - c is never +-inf against a
-        // finite c, see acc_ok), k = f32(n + 1) for n + 1 in [1, 2^24]
-        const uint32_t kk = (r2 & 0x800000u) ? 1u + (r1 & 0xFFFFFFu)
+        // finite c, see acc_ok), k = f32(n + 1) for n + 1 in [1, 2^22) (kAccRnMax)
+        const uint32_t kk = (r2 & 0x800000u) ? 1u + (r1 % (kAccRnMax - 1u))
                                              : 1u + (r1 % 4096u);   // small counts too
         const v3 num = mk(__uint_as_float(r0), __uint_as_float(r0 ^ r1),
                           __uint_as_float(r2 & 0x83FFFFFFu));       // (many tiny ones)
@@ -3055,20 +3074,36 @@ __global__ __launch_bounds__(256) void rt_selftest_kernel(unsigned long long* cn
     atomicAdd(&cnt[4], runs);
 }
 
-// TraceParams::normal_rn: is rcp_refined(R) the correctly rounded 1 / R for every radius?
-// (one thread per sphere at upload; a vector atomic OR on any miss)
-__global__ __launch_bounds__(256) void rt_rcp_check_kernel(const float4* sph, uint32_t count,
+// TraceParams::normal_rn: is one Markstein step from y = rcp_refined(R) the IEEE quotient
+// a / R for every numerator the kernels divide, for every distinct radius R of the scene?
+// Markstein's theorem needs y within half an ulp of 1 / R AND q = RN(a y) within one ulp of
+// a / R; a correctly rounded y alone gives |R y - 1| <= 2^-24, and with a divisor's and a
+// quotient's significands both near 2 q can then be 1.5 ulp off (round-5 ADVICE).  So the
+// check is exhaustive instead of sufficient: for each radius every numerator significand
+// (2^23 of them) in two binades, [1, 2) and [2^-100, 2^-99) (the kernels' smallest
+// numerators), against the IEEE division.  A step and its operands scale exactly by powers of
+// two while q, the residual and the result stay normal (numerators in [2^-100, 2^43], R in
+// [2^-20, 2^20]: the callers' domain), so these two binades cover every numerator; the sign
+// is symmetric.  One thread per (radius, significand, binade), a vector atomic OR on a miss.
+constexpr uint32_t kRcpCheckPerRadius = 2u << 23;
+__global__ __launch_bounds__(256) void rt_rcp_check_kernel(const float* radii, uint32_t n,
                                                            uint32_t* bad) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    const float r = sph[2u * i].w;
-    if (__float_as_uint(rcp_refined(r)) != __float_as_uint(1.0f / r)) atomicOr(bad, 1u);
+    const uint64_t total = (uint64_t)n * kRcpCheckPerRadius;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t miss = 0u;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const float r = radii[i / kRcpCheckPerRadius];
+        const uint32_t j = (uint32_t)(i % kRcpCheckPerRadius);
+        // significand j & 0x7FFFFF; binade 2^0 or 2^-100
+        const float a = __uint_as_float(((j >> 23) ? 0x0D800000u : 0x3F800000u) | (j & 0x7FFFFFu));
+        const float y = rcp_refined(r);
+        miss |= __float_as_uint(div_rn(a, r, y)) != __float_as_uint(a / r);
+    }
+    if (miss) atomicOr(bad, 1u);
 }
-hipError_t launch_rcp_check(const float4* sph, uint32_t count, uint32_t* bad,
-                            hipStream_t stream) {
-    if (count == 0u) return hipSuccess;
-    hipLaunchKernelGGL(rt_rcp_check_kernel, dim3((count + 255u) / 256u), dim3(256), 0, stream,
-                       sph, count, bad);
+hipError_t launch_rcp_check(const float* radii, uint32_t n, uint32_t* bad, hipStream_t stream) {
+    if (n == 0u) return hipSuccess;
+    hipLaunchKernelGGL(rt_rcp_check_kernel, dim3(2048), dim3(256), 0, stream, radii, n, bad);
     return hipGetLastError();
 }
 

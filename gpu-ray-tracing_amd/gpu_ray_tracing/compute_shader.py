@@ -306,15 +306,25 @@ class ComputeShaderPipeline:
         # alive until the next call replaces it (a converted copy included)
         last = {"arr": None, "ptr": None, "n": 0, "held": None}
 
+        # arrays the binding refused (by identity): they take the converting path below from
+        # then on instead of raising and catching on every call
+        refused = {"arr": None, "seeds": None}
+
         def run(camera: SceneCamera, spheres: SphereCollection, seeds) -> int:
-            if fast is not None:
-                arr = spheres.spheres
+            arr = spheres.spheres
+            # the binding takes exactly what the ctypes path passes unconverted: contiguous
+            # float32 (N, 8) spheres (an (N, 16) array would otherwise be read as N records of
+            # a 32-byte stride) and contiguous float32 seeds
+            if (fast is not None and arr is not refused["arr"] and seeds is not refused["seeds"]
+                    and _is_f32c(arr) and arr.ndim == 2 and arr.shape[1] == 8
+                    and _is_f32c(seeds)):
                 try:
                     r = fast.update_frames(ictx, ia, ib, width, height, rank, nranks,
                                            camera.blob, arr, len(arr), seeds,
                                            raw(dev) if raw else stream().value)
                 except (TypeError, ValueError, BufferError):
-                    r = None               # (not C-contiguous float32: converted below)
+                    refused.update(arr=arr, seeds=seeds)
+                    r = None
                 if r is not None:
                     if r < 0:
                         _lib.check(-r, "rt_update_frames")

@@ -203,8 +203,9 @@ typedef struct rt_launch_info {
     int32_t kernel;
     uint32_t queues;
     uint32_t submit;
-    /* 1: the hit normal's division ran as one Markstein step per component (every radius's
-     * device reciprocal checked correctly rounded at upload); 0: two correction steps */
+    /* 1: the hit normal's division ran as one Markstein step per component (checked at
+     * upload to give the IEEE quotient for every numerator and each of the scene's distinct
+     * radii, at most 16 of them); 0: two correction steps */
     uint32_t normal_rn;
 } rt_launch_info;
 RT_API rt_status rt_last_launch_info(const rt_ctx* ctx, rt_launch_info* out);

@@ -58,3 +58,27 @@ def bits_equal(a, b):
     b = np.ascontiguousarray(b, np.float32)
     same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
     return bool(same.all()), int((~same).sum())
+
+
+CANON_NAN = 0x7FC00000
+
+
+def canon_sha(img) -> str:
+    """SHA-256 of a float32 image's bytes with every NaN as 0x7FC00000: the digest the
+    fixtures' `sha256` / `band_sha` hold (tests/golden/make_band_digests.py), so NaN == NaN
+    whatever its payload, as bits_equal compares."""
+    import hashlib
+    import numpy as np
+    a = np.ascontiguousarray(img, np.float32).copy()
+    a.view(np.uint32)[np.isnan(a)] = CANON_NAN
+    return hashlib.sha256(a.tobytes()).hexdigest()
+
+
+def bands_match(local, bands, band_sha, rows=8):
+    """A rank's compact local image (global band bands[j] at local rows rows*j ...) against
+    the fixture's per-band digests: the list of global bands that differ."""
+    bad = []
+    for j, b in enumerate(bands):
+        if canon_sha(local[rows * j:rows * (j + 1)]) != bytes(band_sha[b]).hex():
+            bad.append(int(b))
+    return bad

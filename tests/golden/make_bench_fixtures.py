@@ -9,7 +9,7 @@ bench.py's defaults).  The values come from the CPU oracle (test infrastructure)
 the rt_render contract (oracle.render_pixels: frames chained updates of the given pixels).
 K4 and K5 need no extra fixture: bench.py checks them against k4.npz / k5.npz.
 
-    python tests/golden/make_bench_fixtures.py        # ~10 s on 8 cores
+    python tests/golden/make_bench_fixtures.py        # ~2 min on 8 cores (with the digests)
 """
 from __future__ import annotations
 
@@ -70,6 +70,10 @@ def fixture(name, kind, n):
 def main():
     fixture("bench_k2.npz", 0, 0)
     fixture("bench_k3.npz", 2, 500)
+    # whole-image and per-band digests at both frame counts (make_band_digests.py)
+    sys.path.insert(0, str(OUT))
+    import make_band_digests
+    make_band_digests.main(["bench"])
 
 
 if __name__ == "__main__":

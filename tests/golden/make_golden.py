@@ -7,6 +7,9 @@ stores the exact 176-byte camera blob, the sphere bytes and the per-frame seeds,
 fixtures do not depend on any product code.
 
     python tests/golden/make_golden.py            # all fixtures (K4 full hash: ~1 min, 8 cores)
+
+The whole-image and per-band digests of K4 / K5 (and K5's 16 384 sampled pixels and exact
+segment count) are added by make_band_digests.py, which main() runs last (K5: ~12 min).
 """
 from __future__ import annotations
 
@@ -136,6 +139,9 @@ def main():
     }
     (OUT / "kat.json").write_text(json.dumps(kat, indent=1))
     print("wrote kat.json")
+
+    import make_band_digests
+    make_band_digests.main(["k5", "k4"])
 
 
 if __name__ == "__main__":

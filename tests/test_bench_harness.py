@@ -32,8 +32,8 @@ def test_over_ranks_takes_the_slowest_rank(bench):
 
 
 def test_timed_steps_one_rank(bench):
-    """At N = 1 there is no barrier: the time is the steps plus the closing wait, and the
-    wait hook (bench.py --host-wait spin) runs instead of the plain synchronize."""
+    """At N = 1 there is no barrier: the time is the steps plus the closing wait (the wait
+    hook runs instead of the plain synchronize), on CLOCK_MONOTONIC."""
     import time
     calls = []
     ts = bench.timed_steps(lambda: time.sleep(0.01), lambda: calls.append("sync"), 1,
@@ -41,14 +41,49 @@ def test_timed_steps_one_rank(bench):
                            wait=lambda: calls.append("wait"))
     assert calls == ["sync", "wait"]
     assert 0.01 <= ts["dt"] < 0.2 and ts["per_rank"] == [ts["dt"]] and ts["barrier_s"] == 0.0
+    assert ts["start_skew_s"] == 0.0 and ts["max_rank_s"] == ts["dt"]
     assert 0.01 <= ts["issue"] <= ts["dt"]
 
 
-def test_frame_launch_policy(bench):
-    """--frame-launch auto: the whole 1920x1080 image (32 400 tiles) one launch per frame,
-    every rank share of N >= 2 (at most 17 280 tiles) frame chains."""
-    from gpu_ray_tracing import stripe_local_rows
-    assert bench.frame_launch_mode("auto", 1920, 1080) == "dispatch"
-    for n in (2, 4, 8):
-        assert bench.frame_launch_mode("auto", 1920, stripe_local_rows(1080, 0, n)) == "chain"
-    assert bench.frame_launch_mode("dispatch", 1920, 136) == "dispatch"
+def test_one_launch_structure_at_every_n(bench):
+    """Round 6 (verdict item 1): K2/K3 run the same launch structure at every N — frame
+    chains by default, one launch per frame on request — with no size-dependent switch."""
+    assert bench.parse([]).frame_launch == "chain"
+    assert bench.parse(["--frame-launch", "dispatch"]).frame_launch == "dispatch"
+    assert not hasattr(bench, "frame_launch_mode")
+
+
+def test_stripe_bands_round_robin(bench):
+    assert bench.stripe_bands(1080, 0, 8)[:3] == [0, 8, 16]
+    assert bench.stripe_bands(1080, 7, 8)[-1] == 127
+    bands = sorted(b for r in range(8) for b in bench.stripe_bands(1080, r, 8))
+    assert bands == list(range(135))
+
+
+def test_canon_sha_matches_fixture_script(bench):
+    """bench.py's digest and the fixture generator's (tests/golden/make_band_digests.py)
+    agree, NaN payloads canonical: any NaN hashes as 0x7FC00000."""
+    import hashlib
+    import numpy as np
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    import make_band_digests as M
+    a = np.arange(64, dtype=np.float32).reshape(2, 8, 4)
+    a.view(np.uint32)[0, 3, 1] = 0xFFC00001          # a negative NaN with a payload
+    b = a.copy()
+    b.view(np.uint32)[0, 3, 1] = 0x7FC00000
+    assert bench.canon_sha(a) == bench.canon_sha(b) == hashlib.sha256(b.tobytes()).hexdigest()
+    assert bytes(M.band_digests(np.concatenate([a[0:1]] * 8).reshape(8, 8, 4))[0]).hex() == \
+        bench.canon_sha(np.concatenate([b[0:1]] * 8).reshape(8, 8, 4))
+
+
+def test_fixtures_carry_band_digests(bench):
+    """Every full-size fixture has a whole-image digest and one digest per 8-row band (K5:
+    the exact segment count too), so bench.py checks every rank's share band by band."""
+    for cfg, frames in (("K2", 25), ("K3", 25), ("K3", 220), ("K4", 64), ("K5", 64)):
+        g = bench._fixture(cfg)
+        sha, bands, pixels, segs = bench._fixture_at(g, frames)
+        h = int(g["height"])
+        assert sha is not None and len(sha) == 64, cfg
+        assert bands is not None and bands.shape == (h // 8, 32), cfg
+        assert segs is not None and segs > 0, cfg
+    assert bench._fixture("K5")["px"].size >= 16384

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import bits_equal, load_golden
+from conftest import bands_match, bits_equal, canon_sha, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -217,6 +217,7 @@ def test_bench_dispatch_chain_matches_fixture(rt, cfg, single, submit):
         img = host(b if newest == 1 else a)
         k = list(g["frame_counts"]).index(25)
         assert_same(img[g["py"], g["px"]], g["pixels"][k])
+        assert canon_sha(img) == str(g["sha256"][k])
     finally:
         p.close()
 
@@ -248,6 +249,7 @@ def test_normal_markstein_matches_fixture(rt, cfg, normal_rn, monkeypatch):
             assert info["normal_rn"] == (1 if normal_rn == "on" else 0), info
             img = host(b if newest == 1 else a)
             assert_same(img[g["py"], g["px"]], g["pixels"][k])
+            assert canon_sha(img) == str(g["sha256"][k])
         finally:
             p.close()
 
@@ -439,8 +441,9 @@ def test_aql_go_wait_gives_up_and_falls_back(rt, monkeypatch):
 
 def test_bench_k5_launches_match_golden(rt):
     """bench.py --config K5's timed structure on one GPU: rt_update_frames of 64 frames
-    (the bounce instance, all 64 fused in one launch) at 3840x2160, depth 8, sampled
-    pixels."""
+    (the bounce instance, all 64 fused in one launch) at 3840x2160, depth 8: the whole
+    image's digest and every band's (the oracle rendered all 8.3 M pixels), and the 16 384
+    sampled pixels for locating a difference."""
     g = load_golden("k5.npz")
     w, h = int(g["width"]), int(g["height"])
     p = rt.ComputeShaderPipeline(0)
@@ -452,6 +455,8 @@ def test_bench_k5_launches_match_golden(rt):
         assert info["frames"] == 64 and info["kernel_name"] == "rt_bounce_kernel<0>"
         img = host(b if newest == 1 else a)
         assert_same(img[g["py"], g["px"]], g["pixels"])
+        assert bands_match(img, range(h // 8), g["band_sha"]) == []
+        assert canon_sha(img) == str(g["sha256"])
     finally:
         p.close()
 
@@ -459,38 +464,41 @@ def test_bench_k5_launches_match_golden(rt):
 @pytest.mark.parametrize("world,paths", [(1, "split"), (4, "split"), (4, "auto"), (8, "auto"),
                                          (8, "per_wave")])
 def test_bench_k5_shares_match_golden(rt, world, paths):
-    """bench.py --config K5 per rank: rank 0's stripe share of the 64-spp 3840x2160 depth-8
-    render (one 64-frame bounce launch) — the fixture's sampled pixels that fall in rank 0's
-    bands, bit for bit, on two consecutive steps: the first runs per wave under AUTO and
-    measures the tile costs, the second runs the cost order (AUTO on an 8-rank share: the split
-    schedule's unit order, the costliest tiles in four chunks on separate waves; the arrival
-    counters are reused).  Forced splits on the whole image and a 4-rank share."""
+    """bench.py --config K5 per rank: EVERY rank's stripe share of the 64-spp 3840x2160
+    depth-8 render (one 64-frame bounce launch), every pixel, against the fixture's per-band
+    digests (each 8-row band of the oracle's whole image), on two consecutive steps: the
+    first runs per wave under AUTO and measures the tile costs, the second runs the cost order
+    (AUTO on an 8-rank share: the split schedule's unit order, the costliest tiles in four
+    chunks on separate waves; the arrival counters are reused).  Forced splits on the whole
+    image and a 4-rank share.  Every band boundary of the 4- and 8-rank partitions is a rank
+    boundary, so this covers the pixels on both sides of each."""
     g = load_golden("k5.npz")
     w, h = int(g["width"]), int(g["height"])
-    p = rt.ComputeShaderPipeline(0)
-    p.set_path_compaction(paths)
-    try:
-        rows = rt.stripe_local_rows(h, 0, world)
-        a, b = p.new_image(w, rows), p.new_image(w, rows)
-        py, px = g["py"], g["px"]
-        mine = (py // 8) % world == 0
-        ly = (py[mine] // 8 // world) * 8 + py[mine] % 8
-        for step in range(2):
-            newest = p.update_frames(a, b, w, h, rt.SceneCamera(g["camera"]),
-                                     rt.SphereCollection(g["spheres"]), g["seeds"], 0, world)
-            info = p.last_launch_info()
-            split = paths == "split" or (paths == "auto" and world >= 8 and step == 1)
-            assert info["kernel_name"] == ("rt_bounce_kernel<3>" if split
-                                           else "rt_bounce_kernel<0>"), info
-            img = host(b if newest == 1 else a)
-            assert_same(img[ly, px[mine]], g["pixels"][mine])
-            assert np.all(img[:rows, :, 3] == 64)
-    finally:
-        p.close()
+    cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
+    for rank in range(world):
+        p = rt.ComputeShaderPipeline(0)
+        p.set_path_compaction(paths)
+        try:
+            rows = rt.stripe_local_rows(h, rank, world)
+            bands = list(range(rank, h // 8, world))
+            assert rows == 8 * len(bands)
+            a, b = p.new_image(w, rows), p.new_image(w, rows)
+            for step in range(2):
+                newest = p.update_frames(a, b, w, h, cam, sc, g["seeds"], rank, world)
+                info = p.last_launch_info()
+                split = paths == "split" or (paths == "auto" and world >= 8 and step == 1)
+                assert info["kernel_name"] == ("rt_bounce_kernel<3>" if split
+                                               else "rt_bounce_kernel<0>"), info
+                img = host(b if newest == 1 else a)
+                assert bands_match(img, bands, g["band_sha"]) == [], (rank, step)
+                assert np.all(img[:rows, :, 3] == 64)
+        finally:
+            p.close()
 
 
-def test_golden_k5_sampled(rt, pipe):
-    """configs[4] shape on one GPU: 3840x2160, 500 spheres, 64 spp, depth 8 (sampled)."""
+def test_golden_k5_whole_image(rt, pipe):
+    """configs[4] shape on one GPU through rt_render: 3840x2160, 500 spheres, 64 spp, depth
+    8 — the whole image's digest (the oracle's 8.3 M pixels), in every scan mode."""
     g = load_golden("k5.npz")
     w, h = int(g["width"]), int(g["height"])
     a = pipe.new_image(w, h)
@@ -499,6 +507,7 @@ def test_golden_k5_sampled(rt, pipe):
     img = host(a)
     assert_same(img[g["py"], g["px"]], g["pixels"])
     assert np.all(img[..., 3] == 64)
+    assert canon_sha(img) == str(g["sha256"])
 
 
 @pytest.mark.parametrize("frames", [1, 3, 130])
