@@ -566,11 +566,11 @@ def driver_record_sides(device, stream, main_cfg):
                     "wall_runs_us": [round(x * 1e6, 3) for x in walls],
                     "image_ok": ok}
 
-        def k5_run(world, rank=0):
+        def k5_run(world, rank=0, partition=None):
             w, h, sc, seeds, cam = _setup("K5")
             pipe.set_frames_per_launch(0)
             pipe.set_frame_images("last_two")
-            r = StripeRenderer(pipe, w, h, rank, world)
+            r = StripeRenderer(pipe, w, h, rank, world, partition=partition)
             r.frames(cam, sc, seeds)                   # records the tile costs
             r.frames(cam, sc, seeds)                   # builds the order (and its buffers)
             # (each call restarts from the camera's reset; wall-clock, the median of five)
@@ -579,7 +579,8 @@ def driver_record_sides(device, stream, main_cfg):
             return {"us_per_step": round(runs[2] * 1e6, 1),
                     "runs_us": [round(x * 1e6, 1) for x in runs],
                     "kernel": info["kernel_name"],
-                    "image_ok": share_check("K5", r.local, 64, stripe_bands(h, rank, world))}
+                    "bands": list(r.bands),
+                    "image_ok": share_check("K5", r.local, 64, r.band_list())}
 
         # the reference's structure (one launch per frame) for the main and the other config
         other = "K2" if main_cfg == "K3" else "K3"
@@ -615,6 +616,9 @@ def driver_record_sides(device, stream, main_cfg):
                              "cost-ordered after two untimed renders), wall, the median of five"}
         del r4
         k5 = k5_run(1)
+        # the whole image's per-band costs, as its first (cost-recording) launch measured them
+        w5, h5 = CONFIGS["K5"][:2]
+        k5_costs = pipe.band_costs(w5, h5, (0, 1, h5 // ROWS))
         segs5 = fixture_segments("K5", 64)
         out["k5"] = dict(k5, Mrays_per_s=round(3840 * 2160 * 64 / k5["us_per_step"], 1),
                          segments_per_s=(round(segs5 / (k5["us_per_step"] / 1e6), 1)
@@ -651,6 +655,31 @@ def driver_record_sides(device, stream, main_cfg):
         for k, v in k5rows.items():
             v["efficiency"] = round(k5["us_per_step"] / (int(k) * v["us_per_step"]), 4)
         shares["K5_fused_64"] = k5rows
+        # cost-balanced contiguous ranges: rt_partition_bands over the whole image's band
+        # costs, then two calibration rounds — each range's band costs rescaled by the time
+        # its share took over the cost it was given (a share's time is not its tiles' costs
+        # in the whole image: placement, tails), re-cut — and the final partition timed
+        # afresh like the round-robin shares
+        brows = {"1": k5rows["1"]}
+        for world in (2, 4, 8):
+            adj = np.array(k5_costs, np.float64)
+            hist = []
+            for it in range(3):
+                part = rt.partition_bands(adj, world)
+                if it == 2:
+                    break
+                t = [k5_run(world, rk, part)["us_per_step"] for rk in range(world)]
+                hist.append({"partition": [list(b) for b in part], "rank_us": t})
+                for (f, _, c), tr in zip(part, t):
+                    cs = adj[f:f + c].sum()
+                    if c and cs > 0:
+                        adj[f:f + c] *= tr / cs
+            brows[str(world)] = over_ranks(lambda rk: k5_run(world, rk, part), world)
+            brows[str(world)]["partition"] = [list(b) for b in part]
+            brows[str(world)]["calibration"] = hist
+        for k, v in brows.items():
+            v["efficiency"] = round(k5["us_per_step"] / (int(k) * v["us_per_step"]), 4)
+        shares["K5_balanced_64"] = brows
         shares["what"] = (
             "every rank's stripe share (8-row bands dealt round-robin) timed alone on this GPU "
             "in the main line's structure, each rank's step of bench.py --gpus N: us_per_step = "
@@ -660,7 +689,10 @@ def driver_record_sides(device, stream, main_cfg):
             "time / (N x that time) in the same structure and step count; K3 at the driver's 20 "
             "steps and at the default 200; K3_call_model: fixed_us + steps x per_step_us fitted "
             "to the two; runtime_floor_us: one 1-element kernel launched and synchronized on "
-            "the idle GPU (the floor of any call's fixed cost); K5: one 64-spp step per call")
+            "the idle GPU (the floor of any call's fixed cost); K5: one 64-spp step per call, "
+            "K5_balanced_64 with contiguous band ranges cut by rt_partition_bands from the "
+            "whole image's per-band costs (rt_band_costs), calibrated twice by the ranges' "
+            "measured times, instead of round-robin bands")
         out["rank_shares"] = shares
     finally:
         pipe.close()
@@ -767,6 +799,9 @@ def main(argv=None):
                         time.clock_gettime_ns(time.CLOCK_BOOTTIME))
 
     gate = StreamGate() if args.gate else None
+    # the roofline's repetition of the timed call (HIP events, never inside the timed
+    # region): its renderer allocated here, its reset frames issued right after the region
+    rep = StripeRenderer(pipe, w, h, rank, world, comm=None)
 
     def run():
         if gate:
@@ -784,6 +819,14 @@ def main(argv=None):
                      stamp=stamp if host_t is not None else None)
     dt = ts["dt"]
     info = pipe.last_launch_info()             # the last timed rt_update_frames call
+    # the roofline's kernel time: HIP events over an identical repetition of the timed call
+    # (the same reset and frames on the scratch renderer), issued at once while the GPU is
+    # as warm as in the region (a host-side check first would let its clock drop)
+    if dispatch:
+        step_block(rep, args.warmup, True)
+    rep_s = timed(stream, lambda: step_block(rep, args.steps, args.warmup == 0))
+    rep_info = pipe.last_launch_info()
+    del rep
     # the job's one gather of the finished tiles, timed on its own (barrier on both sides)
     e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t1 = time.perf_counter()
@@ -812,14 +855,6 @@ def main(argv=None):
         share_ok = None if 2 in vals else all(v == 1 for v in vals)
     cand_stats = pipe.candidate_stats()
 
-    # the roofline's kernel time: HIP events over an identical repetition of the timed call
-    # (a scratch renderer, the same reset and frames), never inside the timed region
-    rep = StripeRenderer(pipe, w, h, rank, world, comm=None)
-    if dispatch:
-        step_block(rep, args.warmup, True)
-    rep_s = timed(stream, lambda: step_block(rep, args.steps, args.warmup == 0))
-    rep_info = pipe.last_launch_info()
-    del rep
     total_launches = info["launches"] * (1 if dispatch else args.steps)
     launches_per_step = total_launches / args.steps
     queues = max(1, info.get("queues", 1))

@@ -85,6 +85,13 @@ struct rt_ctx {
     uint64_t order_gen = ~0ull;     // cand_gen tile_order was derived for
     uint32_t order_frames = 0;      // frames of the measurement it came from
     uint32_t cost_group = 1;        // tiles per tile_cost/tile_order unit (bounce workgroups, pairs)
+    // the share the last cost-recording launch ran (rt_band_costs): width, height, band
+    // first, step, count, unit group; valid when cost_key_ok
+    uint32_t cost_key[6] = {};
+    bool cost_key_ok = false;
+    // rt_deinterleave_bands' per-band source table on the device, and its host copy
+    uint32_t* d_band_src = nullptr;
+    std::vector<uint32_t> band_src;
     int tile_order_mode = RT_TILE_ORDER_AUTO;
     float* d_srgb = nullptr;  // rt_srgb_thresholds table on the device (256 floats)
     // hash(x*73) for x < hx_len (= rtk::hy_offset(width)), then hash(y*51) for y < hy_len
@@ -95,7 +102,7 @@ struct rt_ctx {
     // the source of TraceParams::hint_n (a hint only: the kernel verifies it per pixel).
     struct CountRecord {
         const void* image;
-        uint32_t w, h, rank, nranks, n;
+        uint32_t w, h, first, step, bands, n;   // the image's size and band set, its count
     };
     std::vector<CountRecord> counts;
     uint32_t frames_per_launch = 0;  // rt_update_frames fusion cap (0 = automatic)
@@ -872,6 +879,10 @@ void finish_tile_order(rt_ctx* ctx, const rtk::TraceParams& p) {
     if (!p.tile_cost) return;
     ctx->cost_gen = ctx->cand_gen;
     ctx->cost_frames = p.frames;
+    const uint32_t key[6] = {p.width, p.height, p.band_first, p.band_step, p.local_bands,
+                             ctx->cost_group};
+    std::copy(key, key + 6, ctx->cost_key);
+    ctx->cost_key_ok = true;
 }
 
 // Per-column / per-row halves of the pixel-invariant seed hash (wgsl:309-310), built on
@@ -905,8 +916,8 @@ rt_status ensure_hash_tables(rt_ctx* ctx, uint32_t w, uint32_t h, hipStream_t st
 bool lookup_count(const rt_ctx* ctx, const void* image, const rtk::TraceParams& p,
                   uint32_t& n) {
     for (const rt_ctx::CountRecord& r : ctx->counts)
-        if (r.image == image && r.w == p.width && r.h == p.height && r.rank == p.band_first &&
-            r.nranks == p.band_step) {
+        if (r.image == image && r.w == p.width && r.h == p.height && r.first == p.band_first &&
+            r.step == p.band_step && r.bands == p.local_bands) {
             n = r.n;
             return true;
         }
@@ -924,7 +935,7 @@ void forget_count(rt_ctx* ctx, const void* image) {
 void record_count(rt_ctx* ctx, const void* image, const rtk::TraceParams& p, uint32_t n) {
     forget_count(ctx, image);
     if (ctx->counts.size() >= 16) ctx->counts.erase(ctx->counts.begin());
-    ctx->counts.push_back({image, p.width, p.height, p.band_first, p.band_step, n});
+    ctx->counts.push_back({image, p.width, p.height, p.band_first, p.band_step, p.local_bands, n});
 }
 
 // The count a pixel holds after frame f of the kernel's loop, given the count before it
@@ -987,20 +998,38 @@ void fill_camera(rtk::TraceParams& p, const rt_scene_camera& c) {
     p.spp = host_f2u(c.samples_per_pixel);
 }
 
+// The round-robin stripes of rank / nranks as a band set (band b -> rank b mod nranks).
+rt_band_set stripe_set(uint32_t h, uint32_t rank, uint32_t nranks) {
+    const uint32_t bands = (h + RT_STRIPE_ROWS - 1) / RT_STRIPE_ROWS;
+    return {rank, nranks, bands > rank ? (bands - rank + nranks - 1) / nranks : 0u};
+}
+
+// A band set the kernels can run: inside the image, step >= 1, and (for two or more bands)
+// first and step within the packed stripe map's 16 / 15 bits (rtk::pack_bands).
+rt_status check_band_set(uint32_t h, const rt_band_set& bs) {
+    const uint32_t bands = (h + RT_STRIPE_ROWS - 1) / RT_STRIPE_ROWS;
+    if (bs.step == 0) return fail(RT_ERR_INVALID_ARGUMENT, "band set step is 0");
+    if (bs.count == 0) return RT_OK;
+    if (bs.first >= bands || (uint64_t)bs.first + (uint64_t)(bs.count - 1u) * bs.step >= bands)
+        return fail(RT_ERR_INVALID_ARGUMENT, "band set reaches past the image");
+    if (bs.first > 0xFFFFu || (bs.count >= 2u && bs.step >= 0x7FFFu))
+        return fail(RT_ERR_INVALID_ARGUMENT, "band set first / step out of range");
+    return RT_OK;
+}
+
 // Common setup of every trace launch: argument checks, scene upload, kernel parameters
 // (camera, stripe map, scan-mode data such as the candidate lists).
 rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint32_t h,
-                  uint32_t rank, uint32_t nranks, const rt_scene_camera* cam,
+                  const rt_band_set& bs, const rt_scene_camera* cam,
                   const rt_sphere* spheres, uint32_t count, const float* seeds,
                   hipStream_t stream, rtk::TraceParams& p) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     if (!in || !out || !cam) return fail(RT_ERR_INVALID_ARGUMENT, "NULL image or camera");
     if (rt_status s = check_image(w, h)) return s;
-    if (nranks == 0 || rank >= nranks) return fail(RT_ERR_INVALID_ARGUMENT, "bad rank/nranks");
+    if (rt_status s = check_band_set(h, bs)) return s;
     if (!seeds) return fail(RT_ERR_INVALID_ARGUMENT, "random_seeds is NULL");
     if (rt_status s = upload_spheres(ctx, spheres, count, stream)) return s;
 
-    const uint32_t bands = (h + RT_STRIPE_ROWS - 1) / RT_STRIPE_ROWS;
     std::memset(&p, 0, sizeof(p));
     p.geom = ctx->d_geom;
     p.sph = ctx->d_sph;
@@ -1008,9 +1037,9 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
     p.height = h;
     p.count = count;
     p.normal_rn = ctx->normal_rn ? 1u : 0u;
-    p.band_first = rank;
-    p.band_step = nranks;
-    p.local_bands = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
+    p.band_first = bs.first;
+    p.band_step = bs.step;
+    p.local_bands = bs.count;
     fill_camera(p, *cam);
     // bounce instance mode (rt_kernels.hip rt_bounce_kernel: 0 per wave, 1 compact, 2 pairs)
     p.compact = ctx->path_compaction == RT_PATHS_COMPACT ? 1u
@@ -1220,9 +1249,10 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
     hipStream_t stream = static_cast<hipStream_t>(stream_v);
+    if (nranks == 0 || rank >= nranks) return fail(RT_ERR_INVALID_ARGUMENT, "bad rank/nranks");
     rtk::TraceParams p;
-    if (rt_status s = prepare(ctx, in, out, w, h, rank, nranks, cam, spheres, count, seeds,
-                              stream, p))
+    if (rt_status s = prepare(ctx, in, out, w, h, stripe_set(h, rank, nranks), cam, spheres,
+                              count, seeds, stream, p))
         return s;
     const float4* src = reinterpret_cast<const float4*>(in);
     float4* dst = reinterpret_cast<float4*>(out);
@@ -1326,6 +1356,7 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->d_geom);
         (void)hipFree(ctx->d_sph);
         (void)hipFree(ctx->d_flag);
+        (void)hipFree(ctx->d_band_src);
         (void)hipFree(ctx->d_srgb);
         (void)hipFree(ctx->d_hx);
         (void)hipFree(ctx->tile_cost);
@@ -1500,11 +1531,14 @@ rt_status rt_render(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32
     return trace(ctx, in, out, w, h, 0, 1, cam, spheres, count, frames, seeds, stream);
 }
 
-rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t w, uint32_t h,
-                           uint32_t rank, uint32_t nranks, const rt_scene_camera* cam,
-                           const rt_sphere* spheres, uint32_t count, uint32_t frames,
-                           const float* seeds, void* stream_v, int* out_newest) {
-    CALL_STAMP(0);
+}  // extern "C"
+
+namespace {
+
+rt_status update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t w, uint32_t h,
+                        const rt_band_set& bands, const rt_scene_camera* cam,
+                        const rt_sphere* spheres, uint32_t count, uint32_t frames,
+                        const float* seeds, void* stream_v, int* out_newest) {
     if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
     if (image_a == image_b) return fail(RT_ERR_INVALID_ARGUMENT, "image_a and image_b alias");
     DeviceGuard guard(ctx->device);
@@ -1514,8 +1548,8 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
     if (rt_status s = chain_report(ctx)) return s;
     hipStream_t stream = static_cast<hipStream_t>(stream_v);
     rtk::TraceParams p;
-    if (rt_status s = prepare(ctx, image_a, image_b, w, h, rank, nranks, cam, spheres, count,
-                              seeds, stream, p))
+    if (rt_status s = prepare(ctx, image_a, image_b, w, h, bands, cam, spheres, count, seeds,
+                              stream, p))
         return s;
     CALL_STAMP(2);
     float4* img[2] = {reinterpret_cast<float4*>(image_a), reinterpret_cast<float4*>(image_b)};
@@ -1699,6 +1733,158 @@ rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t
                  g_call_stamp[5] - g_call_stamp[0], g_call_stamp[6] - g_call_stamp[0]);
 #endif
     return RT_OK;
+}
+
+// gathered row of every output band: band_src[b] = the row (in rows_per_rank-row rank
+// buffers back to back) where band b's first row lies; false if the sets do not cover every
+// band exactly once or a set exceeds rows_per_rank
+bool band_sources(uint32_t h, uint32_t nranks, const rt_band_set* sets, uint32_t rows_per_rank,
+                  std::vector<uint32_t>& out) {
+    const uint32_t bands = (h + RT_STRIPE_ROWS - 1) / RT_STRIPE_ROWS;
+    out.assign(bands, ~0u);
+    uint64_t seen = 0;
+    for (uint32_t r = 0; r < nranks; ++r) {
+        const rt_band_set& bs = sets[r];
+        if (check_band_set(h, bs) != RT_OK) return false;
+        if ((uint64_t)bs.count * RT_STRIPE_ROWS > rows_per_rank) return false;
+        for (uint32_t j = 0; j < bs.count; ++j) {
+            const uint32_t b = bs.first + j * bs.step;
+            if (out[b] != ~0u) return false;          // two owners
+            out[b] = (uint32_t)((uint64_t)r * rows_per_rank + (uint64_t)j * RT_STRIPE_ROWS);
+            ++seen;
+        }
+    }
+    return seen == bands;
+}
+
+}  // namespace
+
+extern "C" {
+
+rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t w, uint32_t h,
+                           uint32_t rank, uint32_t nranks, const rt_scene_camera* cam,
+                           const rt_sphere* spheres, uint32_t count, uint32_t frames,
+                           const float* seeds, void* stream_v, int* out_newest) {
+    CALL_STAMP(0);
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (nranks == 0 || rank >= nranks) return fail(RT_ERR_INVALID_ARGUMENT, "bad rank/nranks");
+    return update_frames(ctx, image_a, image_b, w, h, stripe_set(h, rank, nranks), cam, spheres,
+                         count, frames, seeds, stream_v, out_newest);
+}
+
+rt_status rt_update_frames_bands(rt_ctx* ctx, float* image_a, float* image_b, uint32_t w,
+                                 uint32_t h, const rt_band_set* bands,
+                                 const rt_scene_camera* cam, const rt_sphere* spheres,
+                                 uint32_t count, uint32_t frames, const float* seeds,
+                                 void* stream_v, int* out_newest) {
+    CALL_STAMP(0);
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!bands) return fail(RT_ERR_INVALID_ARGUMENT, "bands is NULL");
+    return update_frames(ctx, image_a, image_b, w, h, *bands, cam, spheres, count, frames,
+                         seeds, stream_v, out_newest);
+}
+
+rt_status rt_band_costs(rt_ctx* ctx, uint32_t w, uint32_t h, const rt_band_set* bands,
+                        double* out_cost) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!bands || !out_cost) return fail(RT_ERR_INVALID_ARGUMENT, "NULL bands or out_cost");
+    const uint32_t group = ctx->cost_key[5];
+    const uint32_t want[5] = {w, h, bands->first, bands->step, bands->count};
+    if (!ctx->cost_key_ok || !ctx->tile_cost || !std::equal(want, want + 5, ctx->cost_key))
+        return fail(RT_ERR_INVALID_ARGUMENT, "no tile costs recorded for this share");
+    const uint32_t tiles_x = (((w + 7u) >> 3) + group - 1u) / group;
+    const uint64_t units = (uint64_t)tiles_x * bands->count;
+    std::vector<uint32_t> c(units);
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    if (units) {
+        hipError_t e = hipMemcpy(c.data(), ctx->tile_cost, units * sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpy(tile costs)");
+    }
+    for (uint32_t j = 0; j < bands->count; ++j) {
+        double sum = 0.0;
+        for (uint32_t x = 0; x < tiles_x; ++x) sum += c[(uint64_t)j * tiles_x + x];
+        out_cost[j] = sum;
+    }
+    return RT_OK;
+}
+
+rt_status rt_partition_bands(const double* cost, uint32_t nbands, uint32_t nranks,
+                             rt_band_set* out) {
+    if (!cost || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL band_cost or out");
+    if (nranks == 0) return fail(RT_ERR_INVALID_ARGUMENT, "nranks is 0");
+    if (nbands > 65536u) return fail(RT_ERR_INVALID_SIZE, "more than 65536 bands");
+    for (uint32_t b = 0; b < nbands; ++b)
+        if (!(cost[b] >= 0.0) || !std::isfinite(cost[b]))
+            return fail(RT_ERR_INVALID_ARGUMENT, "band costs must be finite and >= 0");
+    // best[k][i]: the smallest largest-range cost of bands [0, i) in k ranges; cut[k][i] the
+    // start of the last range (the earliest among equals)
+    std::vector<double> pre(nbands + 1, 0.0);
+    for (uint32_t b = 0; b < nbands; ++b) pre[b + 1] = pre[b] + cost[b];
+    const uint32_t K = std::min(nranks, std::max(nbands, 1u));
+    std::vector<std::vector<double>> best(K + 1, std::vector<double>(nbands + 1, INFINITY));
+    std::vector<std::vector<uint32_t>> cut(K + 1, std::vector<uint32_t>(nbands + 1, 0));
+    best[0][0] = 0.0;
+    for (uint32_t k = 1; k <= K; ++k)
+        for (uint32_t i = 0; i <= nbands; ++i)
+            for (uint32_t j = 0; j <= i; ++j) {
+                const double v = std::max(best[k - 1][j], pre[i] - pre[j]);
+                if (v < best[k][i]) {
+                    best[k][i] = v;
+                    cut[k][i] = j;
+                }
+            }
+    std::vector<uint32_t> start(K + 1, 0);
+    start[K] = nbands;
+    for (uint32_t k = K, i = nbands; k >= 1; --k) {
+        start[k - 1] = cut[k][i];
+        i = cut[k][i];
+    }
+    for (uint32_t r = 0; r < nranks; ++r) {
+        if (r < K)
+            out[r] = {start[r], 1u, start[r + 1] - start[r]};
+        else
+            out[r] = {0u, 1u, 0u};   // more ranks than bands: the rest hold none
+    }
+    return RT_OK;
+}
+
+rt_status rt_deinterleave_bands(rt_ctx* ctx, const float* gathered, float* out, uint32_t w,
+                                uint32_t h, uint32_t nranks, const rt_band_set* sets,
+                                uint32_t rows_per_rank, void* stream_v) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!gathered || !out || !sets) return fail(RT_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (gathered == out) return fail(RT_ERR_INVALID_ARGUMENT, "gathered and out alias");
+    if (nranks == 0) return fail(RT_ERR_INVALID_ARGUMENT, "nranks is 0");
+    if (rt_status s = check_image(w, h)) return s;
+    std::vector<uint32_t> src;
+    if (!band_sources(h, nranks, sets, rows_per_rank, src))
+        return fail(RT_ERR_INVALID_ARGUMENT,
+                    "band sets must cover every band once, each within rows_per_rank rows");
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    hipStream_t stream = static_cast<hipStream_t>(stream_v);
+    if (src != ctx->band_src) {
+        // (the previous table may still be read by a queued de-interleave)
+        hipError_t e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+        if (src.size() > ctx->band_src.size() || !ctx->d_band_src) {
+            (void)hipFree(ctx->d_band_src);
+            ctx->d_band_src = nullptr;
+            ctx->band_src.clear();
+            e = hipMalloc(&ctx->d_band_src, src.size() * sizeof(uint32_t));
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc(band table)");
+        }
+        e = hipMemcpy(ctx->d_band_src, src.data(), src.size() * sizeof(uint32_t),
+                      hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpy(band table)");
+        ctx->band_src = src;
+    }
+    hipError_t e = rtk::launch_deinterleave_bands(
+        reinterpret_cast<const float4*>(gathered), reinterpret_cast<float4*>(out), w, h,
+        ctx->d_band_src, stream);
+    return e == hipSuccess ? RT_OK : hip_fail(e, "rt_deinterleave_bands_kernel launch");
 }
 
 uint32_t rt_stripe_local_rows(uint32_t height, uint32_t rank, uint32_t nranks) {

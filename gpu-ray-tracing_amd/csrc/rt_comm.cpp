@@ -11,6 +11,7 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <new>
 #include <string>
@@ -36,6 +37,22 @@ namespace {
 using rti::DeviceGuard;
 using rti::fail;
 using rti::hip_fail;
+
+// The root's gather buffer when the caller passes none: at least `bytes`, grown on demand.
+rt_status scratch_buffer(rt_comm* comm, size_t bytes, hipStream_t stream) {
+    if (bytes <= comm->scratch_bytes) return RT_OK;
+    if (comm->scratch) {
+        hipError_t e = hipStreamSynchronize(stream);   // the old one may be in use
+        if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+        (void)hipFree(comm->scratch);
+        comm->scratch = nullptr;
+        comm->scratch_bytes = 0;
+    }
+    hipError_t e = hipMalloc(&comm->scratch, bytes);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(gather buffer)");
+    comm->scratch_bytes = bytes;
+    return RT_OK;
+}
 
 rt_status nccl_fail(ncclResult_t r, const char* what) {
     return fail(RT_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
@@ -189,19 +206,8 @@ rt_status rt_gather_stripes(rt_ctx* ctx, rt_comm* comm, const float* local, floa
     if (is_root) {
         recv = gathered;
         if (!recv) {
-            const size_t bytes = count * comm->nranks * sizeof(float);
-            if (bytes > comm->scratch_bytes) {
-                if (comm->scratch) {
-                    hipError_t e = hipStreamSynchronize(stream);   // the old one may be in use
-                    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-                    (void)hipFree(comm->scratch);
-                    comm->scratch = nullptr;
-                    comm->scratch_bytes = 0;
-                }
-                hipError_t e = hipMalloc(&comm->scratch, bytes);
-                if (e != hipSuccess) return hip_fail(e, "hipMalloc(gather buffer)");
-                comm->scratch_bytes = bytes;
-            }
+            if (rt_status s = scratch_buffer(comm, count * comm->nranks * sizeof(float), stream))
+                return s;
             recv = comm->scratch;
         }
     }
@@ -213,6 +219,44 @@ rt_status rt_gather_stripes(rt_ctx* ctx, rt_comm* comm, const float* local, floa
                                             reinterpret_cast<float4*>(out_rgba), width, height,
                                             comm->nranks, rows0, stream);
     return e == hipSuccess ? RT_OK : hip_fail(e, "rt_deinterleave_kernel launch");
+}
+
+rt_status rt_gather_bands(rt_ctx* ctx, rt_comm* comm, const float* local, float* gathered,
+                          float* out_rgba, uint32_t width, uint32_t height,
+                          const rt_band_set* sets, uint32_t root, void* stream_v) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!comm) return fail(RT_ERR_INVALID_ARGUMENT, "comm is NULL");
+    if (!local || !sets) return fail(RT_ERR_INVALID_ARGUMENT, "local or sets is NULL");
+    if (rt_status s = rti::check_image(width, height)) return s;
+    if (root >= comm->nranks) return fail(RT_ERR_INVALID_ARGUMENT, "root >= nranks");
+    if (rti::ctx_device(ctx) != comm->device)
+        return fail(RT_ERR_INVALID_ARGUMENT, "ctx and comm are on different devices");
+    const bool is_root = comm->rank == root;
+    if (is_root && !out_rgba) return fail(RT_ERR_INVALID_ARGUMENT, "out_rgba is NULL on the root");
+    // every rank's send buffer has the largest share's row count
+    uint32_t rows = 0;
+    for (uint32_t r = 0; r < comm->nranks; ++r)
+        rows = std::max(rows, sets[r].count * (uint32_t)RT_STRIPE_ROWS);
+    if (rows == 0) return fail(RT_ERR_INVALID_ARGUMENT, "the band sets hold no band");
+    DeviceGuard guard(comm->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    hipStream_t stream = static_cast<hipStream_t>(stream_v);
+    const size_t count = (size_t)rows * width * 4u;   // floats per rank
+    float* recv = nullptr;
+    if (is_root) {
+        recv = gathered;
+        if (!recv) {
+            if (rt_status s = scratch_buffer(comm, count * comm->nranks * sizeof(float), stream))
+                return s;
+            recv = comm->scratch;
+        }
+    }
+    const ncclResult_t r =
+        ncclGather(local, recv, count, ncclFloat32, (int)root, comm->nccl, stream);
+    if (r != ncclSuccess) return nccl_fail(r, "ncclGather");
+    if (!is_root) return RT_OK;
+    return rt_deinterleave_bands(ctx, recv, out_rgba, width, height, comm->nranks, sets, rows,
+                                 stream);
 }
 
 }  // extern "C"

@@ -202,6 +202,10 @@ constexpr uint32_t pack_bands(uint32_t first, uint32_t step, bool ordered) {
     return first | ((step < 0x7FFFu ? step : 0x7FFFu) << 16) | (ordered ? 1u << 31 : 0u);
 }
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream);
+// out[y][x] = gathered[band_src[y / 8] + y % 8][x] (rt_deinterleave_bands)
+hipError_t launch_deinterleave_bands(const float4* gathered, float4* out, uint32_t width,
+                                     uint32_t height, const uint32_t* band_src,
+                                     hipStream_t stream);
 hipError_t launch_init(float4* out, uint64_t texels, hipStream_t stream);
 // Builds the per-tile candidate blocks for p's camera/scene/stripes (p.cand_k entries at
 // most per tile).

@@ -2897,6 +2897,20 @@ __global__ __launch_bounds__(256) void rt_deinterleave_kernel(const float4* __re
     }
 }
 
+// Band-set partitions (rt_deinterleave_bands): band_src[b] = the gathered row holding band
+// b's first row (rank * rows_per_rank + local band * 8), built and checked on the host.
+__global__ __launch_bounds__(256) void rt_deinterleave_bands_kernel(
+    const float4* __restrict__ g, float4* __restrict__ out, uint32_t width, uint32_t height,
+    const uint32_t* __restrict__ band_src) {
+    const uint64_t texels = (uint64_t)width * height;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < texels;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t y = (uint32_t)(i / width), x = (uint32_t)(i % width);
+        const uint32_t row = band_src[y / RT_STRIPE_ROWS] + y % RT_STRIPE_ROWS;
+        out[i] = g[(uint64_t)row * width + x];
+    }
+}
+
 // rt_present_rgba8: one texel per lane per step, 16 B in / 4 B out.  The sRGB boundary
 // table (1 KB) is staged in LDS; each channel is a branch-free 8-step binary search.
 template <bool kSrgb>
@@ -3450,6 +3464,18 @@ hipError_t launch_deinterleave(const float4* gathered, float4* out, uint32_t wid
     if (blocks > 8192u) blocks = 8192u;
     hipLaunchKernelGGL(rt_deinterleave_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream,
                        gathered, out, width, height, nranks, max_local_rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_deinterleave_bands(const float4* gathered, float4* out, uint32_t width,
+                                     uint32_t height, const uint32_t* band_src,
+                                     hipStream_t stream) {
+    const uint64_t texels = (uint64_t)width * height;
+    if (texels == 0) return hipSuccess;
+    uint64_t blocks = (texels + 255u) / 256u;
+    if (blocks > 8192u) blocks = 8192u;
+    hipLaunchKernelGGL(rt_deinterleave_bands_kernel, dim3((uint32_t)blocks), dim3(256), 0,
+                       stream, gathered, out, width, height, band_src);
     return hipGetLastError();
 }
 

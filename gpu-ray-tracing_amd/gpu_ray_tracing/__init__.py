@@ -9,7 +9,8 @@ from . import _lib
 from .camera import CameraSettings, SceneCamera
 from . import image_io
 from .compute_shader import (RT_STRIPE_ROWS, ComputeShaderImages, ComputeShaderNode,
-                             ComputeShaderPipeline, srgb_thresholds, stripe_local_rows)
+                             ComputeShaderPipeline, partition_bands, srgb_thresholds,
+                             stripe_band_set, stripe_local_rows)
 from .scene import (SCENE_DEFAULT, SCENE_N, SCENE_THREE, SphereCollection,
                     create_default_spheres, frame_seeds, synthetic_scene, three_spheres)
 
@@ -20,4 +21,5 @@ __all__ = [
     "ComputeShaderNode", "SphereCollection", "create_default_spheres", "synthetic_scene",
     "three_spheres", "frame_seeds", "stripe_local_rows", "RT_STRIPE_ROWS", "RtError",
     "SCENE_THREE", "SCENE_DEFAULT", "SCENE_N", "srgb_thresholds", "image_io",
+    "partition_bands", "stripe_band_set",
 ]

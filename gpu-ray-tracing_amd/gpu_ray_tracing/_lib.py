@@ -137,7 +137,26 @@ _SIGS = {
     "rt_comm_group_start": (ctypes.c_int, []),
     "rt_comm_group_end": (ctypes.c_int, []),
     "rt_gather_stripes": (ctypes.c_int, [P, P, P, P, P, U32, U32, U32, P]),
+    "rt_update_frames_bands": (ctypes.c_int, [P, P, P, U32, U32, P, P, P, U32, U32, P, P,
+                                              ctypes.POINTER(ctypes.c_int)]),
+    "rt_band_costs": (ctypes.c_int, [P, U32, U32, P, P]),
+    "rt_partition_bands": (ctypes.c_int, [P, U32, U32, P]),
+    "rt_deinterleave_bands": (ctypes.c_int, [P, P, P, U32, U32, U32, P, U32, P]),
+    "rt_gather_bands": (ctypes.c_int, [P, P, P, P, P, U32, U32, P, U32, P]),
 }
+
+
+class BandSetC(ctypes.Structure):
+    """rt_band_set (rt_abi.h, ABI 7): global bands first + j * step, j < count."""
+    _fields_ = [("first", U32), ("step", U32), ("count", U32)]
+
+
+def band_sets(sets) -> ctypes.Array:
+    """A ctypes array of rt_band_set from (first, step, count) triples."""
+    arr = (BandSetC * len(sets))()
+    for i, (f, st, c) in enumerate(sets):
+        arr[i].first, arr[i].step, arr[i].count = int(f), int(st), int(c)
+    return arr
 
 
 class LaunchInfoC(ctypes.Structure):

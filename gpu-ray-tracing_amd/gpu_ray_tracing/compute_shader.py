@@ -67,6 +67,21 @@ def stripe_local_rows(height: int, rank: int, nranks: int) -> int:
     return int(_lib.lib().rt_stripe_local_rows(height, rank, nranks))
 
 
+def stripe_band_set(height: int, rank: int, nranks: int) -> tuple[int, int, int]:
+    """The round-robin stripes of rank / nranks as a band set (first, step, count)."""
+    bands = (height + RT_STRIPE_ROWS - 1) // RT_STRIPE_ROWS
+    return (rank, nranks, (bands - rank + nranks - 1) // nranks if bands > rank else 0)
+
+
+def partition_bands(band_cost, nranks: int) -> list[tuple[int, int, int]]:
+    """rt_partition_bands: the bands cut into nranks contiguous ranges (first, 1, count)
+    whose largest cost is the smallest possible (host-only, exact)."""
+    c = np.ascontiguousarray(band_cost, np.float64)
+    out = (_lib.BandSetC * nranks)()
+    _lib.call("rt_partition_bands", _np_ptr(c), c.size, nranks, out)
+    return [(b.first, b.step, b.count) for b in out]
+
+
 class ComputeShaderPipeline:
     """One librt_hip.so context on one HIP device (lib.rs:231-324)."""
 
@@ -351,6 +366,42 @@ class ComputeShaderPipeline:
 
         run.images = (image_a, image_b)
         return run
+
+    def update_frames_bands(self, image_a: torch.Tensor, image_b: torch.Tensor, width: int,
+                            height: int, bands, camera: SceneCamera,
+                            spheres: SphereCollection, seeds) -> int:
+        """rt_update_frames_bands: update_frames over the band set bands = (first, step,
+        count) — local band j is global band first + j * step; the images hold count * 8
+        rows.  Returns 0 if image_a holds the result, 1 for image_b."""
+        rows = int(bands[2]) * RT_STRIPE_ROWS
+        _check_image(image_a, width, rows, "image_a")
+        _check_image(image_b, width, rows, "image_b")
+        bs = _lib.band_sets([bands])
+        cam = camera.to_c()
+        p, n = self._spheres(spheres)
+        sd = np.ascontiguousarray(seeds, np.float32)
+        newest = ctypes.c_int(-1)
+        _lib.call("rt_update_frames_bands", self._ctx, _ptr(image_a), _ptr(image_b), width,
+                  height, bs, ctypes.byref(cam), p, n, sd.size, _np_ptr(sd), self._stream(),
+                  ctypes.byref(newest))
+        return newest.value
+
+    def band_costs(self, width: int, height: int, bands) -> np.ndarray:
+        """rt_band_costs: per local band of `bands` the tile costs (device clock ticks) the
+        context's last cost-recording launch measured for that share."""
+        out = np.zeros(int(bands[2]), np.float64)
+        _lib.call("rt_band_costs", self._ctx, width, height, _lib.band_sets([bands]),
+                  _np_ptr(out))
+        return out
+
+    def deinterleave_bands(self, gathered: torch.Tensor, out: torch.Tensor, width: int,
+                           height: int, sets, rows_per_rank: int) -> None:
+        """rt_deinterleave_bands: nranks = len(sets) compact buffers of rows_per_rank rows
+        each (rank order) scattered into the width x height image."""
+        _check_image(gathered, width, rows_per_rank * len(sets), "gathered")
+        _check_image(out, width, height, "out")
+        _lib.call("rt_deinterleave_bands", self._ctx, _ptr(gathered), _ptr(out), width,
+                  height, len(sets), _lib.band_sets(sets), rows_per_rank, self._stream())
 
     def deinterleave(self, gathered: torch.Tensor, out: torch.Tensor, width: int, height: int,
                      nranks: int) -> None:

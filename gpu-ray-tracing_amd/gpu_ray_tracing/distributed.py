@@ -3,11 +3,13 @@
 SURVEY §8e: pixels are independent and every RNG seed is a pure function of the global
 pixel coordinate, so the image shards with no data-path exchange.  Bands of
 RT_STRIPE_ROWS rows are dealt round-robin (band b -> rank b % world), which balances the
-sky/ground cost between ranks.  Each rank renders its bands into a compact local buffer
-(rt_render_stripes); the only collective is ONE gather of the finished tiles to rank 0
-(RCCL over xGMI), followed by the de-interleave kernel on the root.  The gather runs either
-behind the C ABI (StripeComm: rt_comm_* + rt_gather_stripes, ncclGather inside
-librt_hip.so — what a non-Python host binds) or through torch.distributed (gather_stripes).
+sky/ground cost between ranks — or, given a partition (one band set per rank, e.g.
+rt_partition_bands' cost-balanced contiguous ranges), by that.  Each rank renders its bands
+into a compact local buffer (rt_update_frames / rt_update_frames_bands); the only collective
+is ONE gather of the finished tiles to rank 0 (RCCL over xGMI), followed by the
+de-interleave kernel on the root.  The gather runs either behind the C ABI (StripeComm:
+rt_comm_* + rt_gather_stripes / rt_gather_bands, ncclGather inside librt_hip.so — what a
+non-Python host binds) or through torch.distributed (gather_stripes).
 """
 from __future__ import annotations
 
@@ -17,7 +19,8 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .compute_shader import ComputeShaderPipeline, _check_image, stripe_local_rows
+from .compute_shader import (RT_STRIPE_ROWS, ComputeShaderPipeline, _check_image,
+                             stripe_local_rows)
 
 
 class StripeComm:
@@ -78,6 +81,27 @@ class StripeComm:
                   self.pipe._stream())
         return out if self.rank == root else None
 
+    def gather_bands(self, local: torch.Tensor, width: int, height: int, sets, root: int = 0,
+                     gathered: torch.Tensor | None = None,
+                     out: torch.Tensor | None = None) -> torch.Tensor | None:
+        """rt_gather_bands for a partition (sets[r] = rank r's band set): the full image on
+        `root`, None elsewhere; every rank's `local` padded to the largest share's rows."""
+        rows = max(int(c) for _, _, c in sets) * RT_STRIPE_ROWS
+        _check_image(local, width, rows, "local")
+        gptr = outp = None
+        if self.rank == root:
+            if out is None:
+                out = torch.empty((height, width, 4), dtype=torch.float32, device=local.device)
+            _check_image(out, width, height, "out")
+            outp = ctypes.c_void_p(out.data_ptr())
+            if gathered is not None:
+                _check_image(gathered, width, rows * self.nranks, "gathered")
+                gptr = ctypes.c_void_p(gathered.data_ptr())
+        _lib.call("rt_gather_bands", self.pipe._ctx, self._comm,
+                  ctypes.c_void_p(local.data_ptr()), gptr, outp, width, height,
+                  _lib.band_sets(sets), root, self.pipe._stream())
+        return out if self.rank == root else None
+
     def close(self) -> None:
         if getattr(self, "_comm", None) and self._comm.value:
             _lib.call("rt_comm_destroy", self._comm)
@@ -126,16 +150,29 @@ class StripeRenderer:
     """One rank's share of a width x height progressive render."""
 
     def __init__(self, pipeline: ComputeShaderPipeline, width: int, height: int, rank: int,
-                 world: int, comm: StripeComm | None = None):
-        """comm: gather through the C ABI's RCCL communicator (rt_gather_stripes) instead
-        of torch.distributed."""
+                 world: int, comm: StripeComm | None = None, partition=None):
+        """comm: gather through the C ABI's RCCL communicator (rt_gather_stripes /
+        rt_gather_bands) instead of torch.distributed.  partition: one band set (first, step,
+        count) per rank, identical on every rank and covering every band once (e.g.
+        partition_bands' cost-balanced ranges); None = round-robin stripes."""
         if comm is not None and (comm.rank, comm.nranks) != (rank, world):
             raise ValueError("the communicator's rank/size differ from the renderer's")
         self.pipe, self.width, self.height = pipeline, width, height
         self.rank, self.world = rank, world
         self.comm = comm
-        self.rows = stripe_local_rows(height, rank, world)
-        self.rows0 = padded_rows(height, world)
+        self.partition = None
+        if partition is not None:
+            self.partition = [tuple(int(v) for v in bs) for bs in partition]
+            if len(self.partition) != world:
+                raise ValueError("a partition holds one band set per rank")
+            self.bands = self.partition[rank]
+            self.rows = self.bands[2] * RT_STRIPE_ROWS
+            self.rows0 = max(bs[2] for bs in self.partition) * RT_STRIPE_ROWS
+        else:
+            nb = (height + RT_STRIPE_ROWS - 1) // RT_STRIPE_ROWS
+            self.bands = (rank, world, (nb - rank + world - 1) // world if nb > rank else 0)
+            self.rows = stripe_local_rows(height, rank, world)
+            self.rows0 = padded_rows(height, world)
         # ping-pong local accumulators, padded to rows0 so the gather is uniform
         self.buf = [pipeline.new_image(width, self.rows0), pipeline.new_image(width, self.rows0)]
         self.cur = 0
@@ -149,8 +186,15 @@ class StripeRenderer:
                                          device=dev)
             self._image = torch.empty((height, width, 4), dtype=torch.float32, device=dev)
 
+    def band_list(self) -> list[int]:
+        """This rank's global bands in local order."""
+        f, st, c = self.bands
+        return [f + j * st for j in range(c)]
+
     def frame(self, camera, spheres, seeds) -> None:
         """One progressive `update` (or len(seeds) fused frames) over this rank's bands."""
+        if self.partition is not None:
+            raise ValueError("a partitioned renderer runs frames() (rt_update_frames_bands)")
         src, dst = self.buf[self.cur], self.buf[1 - self.cur]
         if self.rows:
             self.pipe.render_stripes(src, dst, self.width, self.height, self.rank, self.world,
@@ -159,7 +203,13 @@ class StripeRenderer:
 
     def frames(self, camera, spheres, seeds) -> None:
         """len(seeds) progressive frames, one `update` dispatch each, from a single call."""
-        if self.rows:
+        if self.rows and self.partition is not None:
+            newest = self.pipe.update_frames_bands(self.buf[self.cur], self.buf[1 - self.cur],
+                                                   self.width, self.height, self.bands, camera,
+                                                   spheres, seeds)
+            if newest == 1:
+                self.cur = 1 - self.cur
+        elif self.rows:
             bind = getattr(self.pipe, "bind_update_frames", None)
             if self._runs is None and bind is not None:
                 # both ping-pong directions bound at the first call (the buffers are this
@@ -192,10 +242,14 @@ class StripeRenderer:
             if group is not None:
                 raise ValueError("a renderer with a communicator gathers over it, not a group")
             pre = dst == 0 and self._gathered is not None
-            return self.comm.gather(self.local, self.width, self.height, dst,
-                                    gathered=self._gathered.reshape(-1, self.width, 4) if pre else None,
+            g = self._gathered.reshape(-1, self.width, 4) if pre else None
+            if self.partition is not None:
+                return self.comm.gather_bands(self.local, self.width, self.height,
+                                              self.partition, dst, gathered=g,
+                                              out=self._image if pre else None)
+            return self.comm.gather(self.local, self.width, self.height, dst, gathered=g,
                                     out=self._image if pre else None)
-        if self.world == 1:
+        if self.world == 1 and self.partition is None:
             return self.local[: self.height]
         pre = dst == 0 and self._gathered is not None
         gathered = gather_stripes(self.local, self.world, self.rank, dst, group,
@@ -205,5 +259,9 @@ class StripeRenderer:
         # (the de-interleave writes every pixel: no zero fill needed)
         out = self._image if pre else torch.empty((self.height, self.width, 4),
                                                   dtype=torch.float32, device=gathered.device)
-        self.pipe.deinterleave(gathered, out, self.width, self.height, self.world)
+        if self.partition is not None:
+            self.pipe.deinterleave_bands(gathered, out, self.width, self.height,
+                                         self.partition, self.rows0)
+        else:
+            self.pipe.deinterleave(gathered, out, self.width, self.height, self.world)
         return out

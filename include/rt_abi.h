@@ -136,6 +136,18 @@ typedef struct rt_camera_settings {
  * Pixel coordinates (and therefore every RNG seed) stay global. */
 #define RT_STRIPE_ROWS 8u
 
+/* A rank's share as an arithmetic set of bands (ABI 7): global bands first, first + step,
+ * ..., first + (count - 1) * step, held at local rows RT_STRIPE_ROWS * j ... of the rank's
+ * compact images (local band j = global band first + j * step).  The round-robin stripes of
+ * rank r of n are {r, n, ceil((bands - r) / n)}; a contiguous range of bands is {first, 1,
+ * count} — what rt_partition_bands gives for a cost-balanced partition.  first < 65536 and
+ * step < 32768 (the kernels' packed stripe map). */
+typedef struct rt_band_set {
+    uint32_t first;
+    uint32_t step;
+    uint32_t count;
+} rt_band_set;
+
 /* ------------------------------------------------------------------------------------ */
 /* Status codes (the reference panics / unwraps instead: lib.rs:216-217, 356-358, 399-411) */
 /* ------------------------------------------------------------------------------------ */
@@ -158,7 +170,7 @@ typedef struct rt_ctx rt_ctx;
 
 /* Version / introspection ------------------------------------------------------------ */
 RT_API uint32_t rt_abi_version(void); /* RT_ABI_VERSION */
-#define RT_ABI_VERSION 6u
+#define RT_ABI_VERSION 7u
 /* Text of the last error on this thread (never NULL). */
 RT_API const char* rt_last_error(void);
 /* Trace-kernel instances (rt_launch_info.kernel) and their names as rocprofv3 lists them
@@ -431,6 +443,40 @@ RT_API rt_status rt_render_stripes(rt_ctx* ctx, const float* in_local, float* ou
                             uint32_t frames, const float* random_seeds, void* stream);
 RT_API uint32_t rt_stripe_local_rows(uint32_t height, uint32_t rank, uint32_t nranks);
 
+/* rt_update_frames over an explicit band set instead of the round-robin stripes of
+ * rank / nranks: image_a and image_b are compact local images of width x (bands->count *
+ * RT_STRIPE_ROWS) rows; every other argument, and the result, as rt_update_frames (the
+ * round-robin call equals this one with {rank, nranks, ceil((bands - rank) / nranks)}). */
+RT_API rt_status rt_update_frames_bands(rt_ctx* ctx, float* image_a, float* image_b,
+                                        uint32_t width, uint32_t height,
+                                        const rt_band_set* bands, const rt_scene_camera* camera,
+                                        const rt_sphere* spheres, uint32_t sphere_count,
+                                        uint32_t frames, const float* random_seeds,
+                                        void* stream, int* out_newest);
+/* The per-band costs the context's last cost-recording launch measured (the fused
+ * launches' per-tile durations in device clock ticks, summed over each local band's tiles;
+ * rt_set_tile_order), for that launch's share: out_cost[j] for local band j of `bands`,
+ * which must be the band set (and width, height) that launch ran — RT_ERR_INVALID_ARGUMENT
+ * when it is not or no launch has recorded costs.  Synchronous (reads the costs back on the
+ * context's device with a blocking copy). */
+RT_API rt_status rt_band_costs(rt_ctx* ctx, uint32_t width, uint32_t height,
+                               const rt_band_set* bands, double* out_cost);
+/* Cost-balanced partition (host only): the nbands bands, band b costing band_cost[b] >= 0,
+ * cut into nranks contiguous ranges (out[r] = {first_r, 1, count_r}, in band order, a range
+ * may be empty) that minimise the largest range cost (exact, by dynamic programming; ties
+ * to the earliest cut).  Any partition gives bit-identical pixels: every seed is a function
+ * of the global pixel (wgsl:309-311, 353). */
+RT_API rt_status rt_partition_bands(const double* band_cost, uint32_t nbands, uint32_t nranks,
+                                    rt_band_set* out);
+/* Root side of a band-set gather: `gathered` holds nranks compact buffers back to back in
+ * rank order, each padded to rows_per_rank rows (>= every sets[r].count * RT_STRIPE_ROWS);
+ * scatter them into the width x height image out_rgba.  The sets must cover every band of
+ * the image exactly once. */
+RT_API rt_status rt_deinterleave_bands(rt_ctx* ctx, const float* gathered, float* out_rgba,
+                                       uint32_t width, uint32_t height, uint32_t nranks,
+                                       const rt_band_set* sets, uint32_t rows_per_rank,
+                                       void* stream);
+
 /* Root side of the gather: `gathered` holds nranks compact buffers back to back, each
  * padded to max-local-rows (rt_stripe_local_rows(height,0,nranks)) rows; scatter them
  * into the full width x height image `out_rgba` (device pointers). */
@@ -472,6 +518,14 @@ RT_API rt_status rt_comm_group_end(void);
 RT_API rt_status rt_gather_stripes(rt_ctx* ctx, rt_comm* comm, const float* local,
                                    float* gathered, float* out_rgba, uint32_t width,
                                    uint32_t height, uint32_t root, void* stream);
+/* The same gather for a band-set partition (sets[r] = rank r's band set, identical on every
+ * rank): each rank's `local` is padded to max_r sets[r].count * RT_STRIPE_ROWS rows (the
+ * ncclGather's equal send count); `gathered` (root, NULL = the communicator's buffer) holds
+ * nranks such buffers; the root de-interleaves with rt_deinterleave_bands. */
+RT_API rt_status rt_gather_bands(rt_ctx* ctx, rt_comm* comm, const float* local,
+                                 float* gathered, float* out_rgba, uint32_t width,
+                                 uint32_t height, const rt_band_set* sets, uint32_t root,
+                                 void* stream);
 
 /* Presentation (replaces the sprite of lib.rs:79-102, which shows the newest
  * Rgba32Float image on the window): quantizes the accumulator's mean colour to 8-bit RGBA

@@ -93,9 +93,10 @@ class _OraclePipeline:
     def new_image(self, width, height):
         return torch.zeros((height, width, 4), dtype=torch.float32)
 
-    def _bands(self, width, height, rank, world, src, dst, camera, spheres, seeds):
-        ys = [b * 8 + r for b in range(rank, (height + 7) // 8, world) for r in range(8)
-              if b * 8 + r < height]
+    def _bands(self, width, height, rank, world, src, dst, camera, spheres, seeds, bands=None):
+        if bands is None:
+            bands = range(rank, (height + 7) // 8, world)
+        ys = [b * 8 + r for b in bands for r in range(8) if b * 8 + r < height]
         yy = np.repeat(np.array(ys, np.uint32), width)
         xx = np.tile(np.arange(width, dtype=np.uint32), len(ys))
         st0 = src[: len(ys)].numpy().reshape(-1, 4)
@@ -111,6 +112,21 @@ class _OraclePipeline:
                     seeds)
         return newest
 
+    def update_frames_bands(self, a, b, width, height, bands, camera, spheres, seeds):
+        f, st, c = bands
+        newest = len(seeds) % 2
+        self._bands(width, height, None, None, a, (b if newest else a), camera, spheres, seeds,
+                    bands=[f + j * st for j in range(c)])
+        return newest
+
+    def deinterleave_bands(self, gathered, out, width, height, sets, rows_per_rank):
+        g = gathered.reshape(len(sets), rows_per_rank, width, 4)
+        for r, (f, st, c) in enumerate(sets):
+            for j in range(c):
+                b = f + j * st
+                for y in range(b * 8, min(height, b * 8 + 8)):
+                    out[y] = g[r, j * 8 + y % 8]
+
     def deinterleave(self, gathered, out, width, height, nranks):
         rows0 = gathered.shape[0] // nranks
         g = gathered.reshape(nranks, rows0, width, 4)
@@ -119,7 +135,7 @@ class _OraclePipeline:
             out[y] = g[band % nranks, (band // nranks) * 8 + y % 8]
 
 
-def _renderer_worker(rank, world, port, w, h, dst, q):
+def _renderer_worker(rank, world, port, w, h, dst, q, partition=None):
     sys.path[:0] = [str(PKG_DIR), str(ROOT)]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -132,9 +148,12 @@ def _renderer_worker(rank, world, port, w, h, dst, q):
         moved = H.scene_camera_from(max_depth=4, width=w, height=h, random_seed=float(seeds[0]))
         still = H.scene_camera_from(max_depth=4, width=w, height=h, moved=False,
                                     random_seed=float(seeds[2]))
-        r = StripeRenderer(_OraclePipeline(O), w, h, rank, world)
+        r = StripeRenderer(_OraclePipeline(O), w, h, rank, world, partition=partition)
         # bench.py's step shape: a fused first call, then per-dispatch frames, then ONE gather
-        r.frame(moved, spheres, seeds[:2])
+        if partition is None:
+            r.frame(moved, spheres, seeds[:2])
+        else:
+            r.frames(moved, spheres, seeds[:2])
         r.frames(still, spheres, seeds[2:5])
         r.frames(still, spheres, seeds[5:6])
         img = r.finish(dst=dst)
@@ -172,6 +191,75 @@ def test_stripe_renderer_finish_gloo(world, w, h, dst):
             if p.is_alive():
                 p.terminate()
                 p.join(timeout=10)
+
+
+def _partition(costs, world):
+    from gpu_ray_tracing import partition_bands
+    return partition_bands(costs, world)
+
+
+@pytest.mark.parametrize("world,w,h,dst,costs", [
+    (2, 16, 40, 0, [1.0, 5.0, 1.0, 1.0, 3.0]),           # ranges {0-1}, {2-4}
+    (3, 12, 44, 1, [0.0, 0.0, 9.0, 1.0, 1.0, 1.0]),      # ragged last band, a heavy band
+    (3, 9, 8, 0, [1.0])])                                 # ranks without bands
+def test_partitioned_renderer_finish_gloo(world, w, h, dst, costs):
+    """A non-round-robin partition end to end over gloo (verdict r05 item 2): the bands cut
+    into cost-balanced contiguous ranges by rt_partition_bands, each rank rendering its range
+    through update_frames_bands, ONE gather (equal buffers padded to the largest range) and
+    the band-set de-interleave — bit-identical to the single-process render."""
+    part = _partition(costs, world)
+    assert sorted(b for f, st, c in part for b in range(f, f + st * c, st)) == \
+        list(range(len(costs)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_renderer_worker, args=(r, world, port, w, h, dst, q, part))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        assert q.get(timeout=5) is True
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+
+
+def test_partition_bands_is_optimal():
+    """rt_partition_bands against brute force over every contiguous cut: the largest range
+    cost is the minimum, the ranges are contiguous, in order and cover every band once."""
+    import itertools
+    from gpu_ray_tracing import partition_bands
+    rng = np.random.default_rng(4)
+    for trial in range(40):
+        nb = int(rng.integers(1, 9))
+        world = int(rng.integers(1, 5))
+        costs = rng.choice([0.0, 1.0, 2.0, 3.5, 10.0], nb)
+        part = partition_bands(costs, world)
+        assert len(part) == world
+        pos = 0
+        for f, st, c in part:
+            assert st == 1 and (c == 0 or f == pos)
+            pos += c
+        assert pos == nb
+        got = max(costs[f:f + c].sum() for f, _, c in part)
+        best = min(max(costs[a:b].sum() for a, b in zip((0,) + cut, cut + (nb,)))
+                   for cut in itertools.combinations_with_replacement(range(nb + 1), world - 1)
+                   if list(cut) == sorted(cut))
+        assert got == best, (costs, world, part)
+
+
+def test_band_set_errors(rt):
+    from gpu_ray_tracing import partition_bands
+    with pytest.raises(rt.RtError):
+        partition_bands([1.0, -1.0], 2)
+    with pytest.raises(rt.RtError):
+        partition_bands([1.0, float("nan")], 2)
+    assert partition_bands([], 3) == [(0, 1, 0)] * 3
 
 
 def _hip_renderer_worker(rank, world, port, w, h, dst, q):

@@ -1146,3 +1146,88 @@ def test_tile_order_does_not_change_pixels(rt, pipe):
         assert na == nb
         assert_same(a1, a0)
         assert_same(b1, b0)
+
+
+def _k5_partition(rt, p, g, world):
+    """rt_partition_bands over the band costs a whole-image 64-frame K5 launch records."""
+    w, h = int(g["width"]), int(g["height"])
+    cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
+    a, b = p.new_image(w, h), p.new_image(w, h)
+    p.update_frames(a, b, w, h, cam, sc, g["seeds"])          # records the tile costs
+    costs = p.band_costs(w, h, (0, 1, h // 8))
+    assert costs.shape == (h // 8,) and np.all(costs > 0) and np.all(np.isfinite(costs))
+    with pytest.raises(rt.RtError):                            # not the share that ran
+        p.band_costs(w, h, (0, 2, h // 16))
+    return rt.partition_bands(costs, world), costs
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_k5_cost_balanced_partition_matches_golden(rt, world):
+    """The cost-balanced partition (verdict r05 item 2): the band costs of a whole-image K5
+    launch (rt_band_costs), cut into `world` contiguous ranges (rt_partition_bands); every
+    rank renders its range with rt_update_frames_bands (two steps: per wave, then the cost
+    order / split schedule), every band of every rank equal to the oracle's (per-band
+    digests); the ranks' buffers, padded to the largest range, de-interleaved by
+    rt_deinterleave_bands into the image whose digest is the oracle's whole image."""
+    g = load_golden("k5.npz")
+    w, h = int(g["width"]), int(g["height"])
+    cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
+    p = rt.ComputeShaderPipeline(0)
+    try:
+        part, costs = _k5_partition(rt, p, g, world)
+        loads = [costs[f:f + c].sum() for f, _, c in part]
+        assert max(loads) <= costs.sum() / world + costs.max()
+        rows0 = max(c for _, _, c in part) * 8
+        gathered = torch.zeros((world * rows0, w, 4), dtype=torch.float32, device="cuda")
+        for rank, bs in enumerate(part):
+            f, st, c = bs
+            a = gathered[rank * rows0:rank * rows0 + rows0]
+            b = p.new_image(w, rows0)
+            for step in range(2):
+                newest = p.update_frames_bands(a, b, w, h, bs, cam, sc, g["seeds"])
+                img = host(b if newest == 1 else a)
+                assert bands_match(img, range(f, f + c), g["band_sha"]) == [], (rank, step)
+            if newest == 1:
+                a.copy_(b)
+        out = p.new_image(w, h)
+        p.deinterleave_bands(gathered, out, w, h, part, rows0)
+        assert canon_sha(host(out)) == str(g["sha256"])
+    finally:
+        p.close()
+
+
+def test_band_set_equals_stripes(rt):
+    """rt_update_frames_bands with the round-robin set of rank r of n is rt_update_frames
+    (r, n): the same bits (K3 bench fixture, 5 + 20 frames, frame chains and one launch per
+    frame); a contiguous range of the K3 image against the fixture's band digests."""
+    g = load_golden("bench_k3.npz")
+    w, h = int(g["width"]), int(g["height"])
+    cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
+    still = cam.with_fields(camera_has_moved=0.0)
+    k = list(g["frame_counts"]).index(25)
+    for fpl, bs in ((0, rt.stripe_band_set(h, 3, 8)), (1, rt.stripe_band_set(h, 1, 4)),
+                    (0, (40, 1, 57)), (1, (7, 1, 30)), (0, (0, 3, 45))):
+        p = rt.ComputeShaderPipeline(0)
+        p.set_frames_per_launch(fpl)
+        p.set_frame_images("every")
+        try:
+            rows = bs[2] * 8
+            a, b = p.new_image(w, rows), p.new_image(w, rows)
+            if p.update_frames_bands(a, b, w, h, bs, cam, sc, g["seeds"][:5]) == 1:
+                a, b = b, a
+            newest = p.update_frames_bands(a, b, w, h, bs, still, sc, g["seeds"][5:25])
+            img = host(b if newest == 1 else a)
+            bands = [bs[0] + j * bs[1] for j in range(bs[2])]
+            assert bands_match(img, bands, g["band_sha"][k]) == [], (fpl, bs)
+        finally:
+            p.close()
+    p = rt.ComputeShaderPipeline(0)
+    try:
+        with pytest.raises(rt.RtError):
+            p.update_frames_bands(p.new_image(w, 8), p.new_image(w, 8), w, h, (135, 1, 1),
+                                  cam, sc, g["seeds"][:1])        # past the image
+        with pytest.raises(rt.RtError):
+            p.update_frames_bands(p.new_image(w, 16), p.new_image(w, 16), w, h, (0, 0, 2),
+                                  cam, sc, g["seeds"][:1])        # step 0
+    finally:
+        p.close()

@@ -21,14 +21,14 @@ def header_functions():
 
 def test_library_exports_every_declared_symbol(rt):
     declared = header_functions()
-    assert len(declared) == 45
+    assert len(declared) == 50
     nm = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True,
                         text=True, check=True).stdout
     exported = set(re.findall(r" T (rt_\w+)$", nm, flags=re.M))
     assert set(declared) <= exported, set(declared) - exported
     # the ctypes binding covers exactly the header
     assert set(rt._lib.exported_symbols()) == set(declared)
-    assert rt._lib.lib().rt_abi_version() == 6
+    assert rt._lib.lib().rt_abi_version() == 7
 
 
 def test_scene_camera_layout_matches_reference(rt):

@@ -7,14 +7,17 @@
 # QUEUES (default 0 = the library's choice, what bench.py times: two concurrent half-image
 # parts per K3 update) is passed as --queues; the summary records it, and bench.py scales the
 # per-launch counts by it (one update = QUEUES launches of equal halves).
-# Usage: [PMC_ROUND=r05] [QUEUES=0] bash tools/pmc_bench.sh TAG "K3 K2 K4 K5"
+# K2/K3 run the driver's --steps 20 --warmup 5 (the timed chain is one 20-frame launch: the
+# summary's frames_per_launch must match the line's).
+# Usage: [PMC_ROUND=r06] [QUEUES=0] bash tools/pmc_bench.sh TAG "K3 K2 K4 K5"
 set -o pipefail
-TAG=$1; CFGS=$2; PMC_ROUND=${PMC_ROUND:-r05}; QUEUES=${QUEUES:-0}
+TAG=$1; CFGS=$2; PMC_ROUND=${PMC_ROUND:-r06}; QUEUES=${QUEUES:-0}
 cd $GRAFT_REPO_ROOT; O=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
 for c in $CFGS; do
   ARGS="--config $c --side 0 --cpu-seconds 0 --queues $QUEUES"
   [ "$c" = "K5" ] && ARGS="$ARGS --steps 1 --warmup 1"
+  { [ "$c" = "K3" ] || [ "$c" = "K2" ]; } && ARGS="$ARGS --steps 20 --warmup 5"
   timeout -k 10 300 python3 bench.py $ARGS > $O/pmc_bench_$c.json 2> $O/pmc_bench_$c.err \
     || { echo "bench $c failed"; tail -3 $O/pmc_bench_$c.err; exit 1; }
   K=$(python3 -c "import json; print(json.loads(open('$O/pmc_bench_$c.json').read())['roofline']['kernel'])")
