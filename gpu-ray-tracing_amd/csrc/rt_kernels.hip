@@ -1333,12 +1333,9 @@ static_assert(kSinglePix >= 1 && kSinglePix <= 4, "1 to 4 tiles per wave");
 #ifndef RT_SINGLE_MIN_WAVES
 #define RT_SINGLE_MIN_WAVES 7
 #endif
-// Knock-out builds of the one-frame kernel (cost attribution only, never the product):
-// bit 1 no accumulator load, 2 no sphere scan, 4 no random camera ray, 8 no hit shading,
-// 16 no image store.
-#ifndef RT_SKO
-#define RT_SKO 0
-#endif
+// (Knock-out builds of the one-frame kernel — no accumulator load, sphere scan, random
+// camera ray, hit shading or image store, for cost attribution — are an experiment-only
+// patch: tools/patches/single_knockouts.patch, DESIGN_HISTORY.md §5.)
 // waves per workgroup of the one-frame kernel: 2 since round 4 (profiles/r04/r04a2_single_shape.txt,
 // r04b2_driver_wg2.txt: 0.2 us per update faster than 4 at K3, same bits)
 #ifndef RT_SINGLE_WG
@@ -1481,14 +1478,8 @@ __device__ __forceinline__ void single_sample(const P& p, const Cam& cam,
     v3 o[S], d[S];
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {                            // wgsl:311, 305-325
-#if RT_SKO & 4
-        o[s] = cam.center;
-        d[s] = sub(fmas((float)tc[s].y + (float)(hxy[s] & 1u), cam.pdv,
-                        fmas((float)tc[s].x, cam.pdu, cam.vul)), o[s]);
-#else
         get_ray<kSingleDisk>(cam, tc[s].x, tc[s].y, hxy[s], seed[s] * 25u + p.seed_b, o[s],
                              d[s]);
-#endif
     }
     SST_V(3, d[S - 1].x);
     const uint32_t lane = threadIdx.x & 63u;
@@ -1508,7 +1499,7 @@ __device__ __forceinline__ void single_sample(const P& p, const Cam& cam,
         black[s] = false;
         any_other[s] = false;
     }
-    if (p.depth != 0u && !(RT_SKO & 2)) {                         // wgsl:264
+    if (p.depth != 0u) {                                          // wgsl:264
         // sphere_list_hit over each tile's list, the tiles' chunks interleaved
         float tmax[S], a[S];
         int idx[S];
@@ -1579,11 +1570,7 @@ __device__ __forceinline__ void single_sample(const P& p, const Cam& cam,
             hm[s] = mask_sge(idx[s], 0) & live_m[s];
             any_m |= hm[s];
         }
-        if (RT_SKO & 8) {
-#pragma unroll
-            for (uint32_t s = 0; s < S; ++s)
-                if (hit[s]) cf[s] = mk(tmax[s], 0.5f, 0.5f);
-        } else if (any_m != 0ull) {
+        if (any_m != 0ull) {
             float4 pr[S], mat[S];
 #pragma unroll
             for (uint32_t s = 0; s < S; ++s) {
@@ -1655,8 +1642,6 @@ __device__ __forceinline__ void single_body(
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const uint32_t* __restrict__ a_order, const SingleParams& p) {
     static_assert(kPix >= 1 && kPix <= 4, "1 to 4 tiles per wave");
-    static_assert(!kChain || !(RT_SKO & 16),
-                  "frame chains hand the image over through write-through stores");
     constexpr uint32_t S = kPix;
     WAVE_TRACE(0);
 #if RT_SSTAMPS
@@ -1746,9 +1731,8 @@ __device__ __forceinline__ void single_body(
     } else {
 #pragma unroll
         for (uint32_t s = 0; s < S; ++s)
-            acc[s] = (RT_SKO & 1) ? make_float4(0.0f, 0.0f, 0.0f, (float)p.n_hint)
-                     : kReset     ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)   // (discarded: no load)
-                                  : a_in[tc[s].valid ? tc[s].idx : 0];            // wgsl:339
+            acc[s] = kReset ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)   // (discarded: no load)
+                            : a_in[tc[s].valid ? tc[s].idx : 0];            // wgsl:339
     }
     if (tx0 >= tiles_x) return;
     SST_V(2, hxy[S - 1]);
@@ -1842,14 +1826,6 @@ __device__ __forceinline__ void single_body(
             }
     }
     SST_V(6, c[S - 1].x);
-#if RT_SKO & 16
-    // every result stays live; the per-lane store happens only if a never-true runtime
-    // condition holds (no image traffic, all compute kept)
-#pragma unroll
-    for (uint32_t s = 0; s < S; ++s)
-        if (__float_as_uint(c[s].x + c[s].y + c[s].z) == p.hy_off + 0x7F7FFFFFu + n[s])
-            p.out[tc[s].idx] = make_float4(c[s].x, c[s].y, c[s].z, (float)n[s]);
-#else
     // write-through (sc1) stores: the lines leave the XCD's L2 as they are written, so the
     // launch ends with no dirty image lines to write back at the kernel boundary
     float4* band = p.out + (size_t)lband * RT_STRIPE_ROWS * a_width;
@@ -1868,7 +1844,6 @@ __device__ __forceinline__ void single_body(
             __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, (int)(drop ? 0x7FFFFFF0u : off), 0,
                                                    16);
         }
-#endif
 #if RT_SSTAMPS
     sst_put(7, __builtin_amdgcn_s_memtime());
     sst_put(9, __builtin_amdgcn_s_memrealtime());

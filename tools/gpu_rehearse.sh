@@ -18,5 +18,5 @@ run 2 29513 --config K2 --side 0 > $O/k2_n2.json 2> $O/k2_n2.err || { tail $O/k2
 run 4 29514 --config K4 --steps 2 --warmup 1 > $O/k4_n4.json 2> $O/k4_n4.err || { tail $O/k4_n4.err; exit 1; }
 run 2 29515 --config K5 --steps 1 --warmup 1 > $O/k5_n2.json 2> $O/k5_n2.err || { tail $O/k5_n2.err; exit 1; }
 for f in k3_n2_driver k3_n3 k2_n2 k4_n4 k5_n2; do
-  python -c "import json; d=json.loads([l for l in open('$O/$f.json') if l.startswith('{')][-1]); print('$f', d['n_gpus'], d['value'], d['image_ok'], d['image_check'], d['timed_breakdown_ms'], d['data'][-40:])"
+  python -c "import json; d=json.loads([l for l in open('$O/$f.json') if l.startswith('{')][-1]); print('$f', d['n_gpus'], d['value'], d['image_ok'], d.get('share_ok'), d['image_check'], d['timed_breakdown_ms'], d['data'][-40:])"
 done

@@ -2,7 +2,13 @@
 output): per kernel name the calls, total / average / min / max duration (us), and for
 kernels that run as concurrent parts (rt_set_update_queues) the union of their intervals —
 the time the GPU had at least one of them running — per `units` (e.g. updates).
-usage: python tools/rocpd_stats.py DB.db [KERNEL_SUBSTRING UNITS] > stats.csv"""
+With RT_WINDOW=LINE.json (a bench.py line run with RT_TIMELINE=1: its `timeline_host` holds
+CLOCK_MONOTONIC / CLOCK_BOOTTIME ns at the timed region's start and after its closing
+synchronize) only the dispatches that start inside the timed region are counted — the
+profile of the timed steps alone, not the warm-up or the side lines.
+usage: [RT_WINDOW=LINE.json] python tools/rocpd_stats.py DB.db [KERNEL_SUBSTRING UNITS] > stats.csv"""
+import json
+import os
 import csv
 import sqlite3
 import sys
@@ -11,6 +17,15 @@ import sys
 def main(db, sub=None, units=None):
     c = sqlite3.connect(db)
     rows = list(c.execute("select name, start, end from kernels"))
+    win = os.environ.get("RT_WINDOW")
+    if win:
+        host = json.loads(open(win).read().strip().splitlines()[-1])["timeline_host"]
+        # the clock whose [t0, synced] window holds dispatches
+        best = max(((k, [r for r in rows if host["t0"][k] <= r[1] <= host["synced"][k]])
+                    for k in (0, 1)), key=lambda kr: len(kr[1]))
+        rows = best[1]
+        print(f"# dispatches starting inside the timed region ({('monotonic', 'boottime')[best[0]]} "
+              f"clock): {len(rows)}")
     by = {}
     for name, s, e in rows:
         by.setdefault(name, []).append((s, e))
