@@ -654,6 +654,9 @@ def driver_record_sides(device, stream, main_cfg):
             k5rows[str(world)] = over_ranks(lambda rk: k5_run(world, rk), world)
         for k, v in k5rows.items():
             v["efficiency"] = round(k5["us_per_step"] / (int(k) * v["us_per_step"]), 4)
+        # the 8-rank shares once more: how far a rank's own time moves between two timings
+        # of the same share (run-to-run noise against the spread between ranks)
+        k5rows["8"]["rank_us_repeat"] = [k5_run(8, rk)["us_per_step"] for rk in range(8)]
         shares["K5_fused_64"] = k5rows
         # cost-balanced contiguous ranges: rt_partition_bands over the whole image's band
         # costs, then two calibration rounds — each range's band costs rescaled by the time
