@@ -34,8 +34,10 @@ count for the rendered frames (the oracle counts them over the whole image).
 image_ok: the timed image's SHA-256 (NaN canonical) against the fixture's whole-image digest
 (tests/golden/*.npz `sha256`, oracle-generated), else its sampled pixels; rank shares are
 checked band by band against the fixture's per-band digests (`band_sha`).
-roofline: the timed kernel's launch duration by HIP events over an identical repetition after
-the timed region (same renderer state, same frames); `bound: "valu"` when a committed PMC
+roofline: the timed kernel's launch duration over an identical repetition of the timed call
+right after the region (the GPU still warm), from timing events its launches' own dispatch
+packets carry (rt_set_launch_timing; one launch per frame: HIP events around the
+repetition); `bound: "valu"` when a committed PMC
 summary of that kernel instance exists (profiles/pmc_<round>_<config>.json): achieved = the
 VALU lane-operations per second it issues (SQ_INSTS_VALU x 64 / launch time) against 1024
 SIMDs x 32 lanes x 2.4 GHz (a wave64 VALU op holds a SIMD-32 two cycles); `hbm` = the
@@ -554,9 +556,18 @@ def driver_record_sides(device, stream, main_cfg):
                 r.frames(cam, sc, seeds[:lead])
                 walls.append(wall(lambda: r.frames(cam_t, sc, seeds[lead:lead + steps])) / steps)
             ok = share_check(cfg, r.local, lead + steps, stripe_bands(h, rank, world))
+            # the kernel time of three more such calls: frame chains from the timing events
+            # their launches carry (rt_set_launch_timing — ≈ 9 µs slower per call, so never in
+            # the wall-clock calls), one-frame launches (which carry none) by HIP events
+            pipe.set_launch_timing(mode == "chain")
             for k in range(3):
                 r.frames(cam, sc, seeds[:lead])
-                evs.append(timed(stream, lambda: r.frames(cam_t, sc, seeds[lead:lead + steps])) / steps)
+                if mode == "chain":
+                    wall(lambda: r.frames(cam_t, sc, seeds[lead:lead + steps]))
+                    evs.append(pipe.last_call_kernel_time()[0] / steps)
+                else:
+                    evs.append(timed(stream, lambda: r.frames(cam_t, sc, seeds[lead:lead + steps])) / steps)
+            pipe.set_launch_timing(False)
             info = pipe.last_launch_info()
             t = statistics.median(walls)
             return {"us_per_step": round(t * 1e6, 3),
@@ -688,7 +699,8 @@ def driver_record_sides(device, stream, main_cfg):
             "in the main line's structure, each rank's step of bench.py --gpus N: us_per_step = "
             "the slowest rank's (max_over_ranks; rank_us lists them all) wall-clock per step "
             "(host clock around one call of the steps and a synchronize, the median of five "
-            "calls; events_us_per_step: HIP events, three more calls); efficiency = the 1-rank "
+            "calls; events_us_per_step: the kernel time of three more calls, from the timing "
+            "events their launches carry, rt_set_launch_timing); efficiency = the 1-rank "
             "time / (N x that time) in the same structure and step count; K3 at the driver's 20 "
             "steps and at the default 200; K3_call_model: fixed_us + steps x per_step_us fitted "
             "to the two; runtime_floor_us: one 1-element kernel launched and synchronized on "
@@ -802,8 +814,12 @@ def main(argv=None):
                         time.clock_gettime_ns(time.CLOCK_BOOTTIME))
 
     gate = StreamGate() if args.gate else None
-    # the roofline's repetition of the timed call (HIP events, never inside the timed
-    # region): its renderer allocated here, its reset frames issued right after the region
+    # the roofline's kernel time: an identical repetition of the timed call right after the
+    # region (the GPU still warm) on a scratch renderer allocated here — its fused launches
+    # carrying timing events in their own dispatch packets (rt_set_launch_timing; that launch
+    # path costs ≈ 9 µs more per call, so it never runs inside the region), one-launch-per-
+    # frame steps (which carry none) between HIP events
+    launch_timing = launch_mode != "dispatch"
     rep = StripeRenderer(pipe, w, h, rank, world, comm=None)
 
     def run():
@@ -822,14 +838,33 @@ def main(argv=None):
                      stamp=stamp if host_t is not None else None)
     dt = ts["dt"]
     info = pipe.last_launch_info()             # the last timed rt_update_frames call
-    # the roofline's kernel time: HIP events over an identical repetition of the timed call
-    # (the same reset and frames on the scratch renderer), issued at once while the GPU is
-    # as warm as in the region (a host-side check first would let its clock drop)
-    if dispatch:
-        step_block(rep, args.warmup, True)
-    rep_s = timed(stream, lambda: step_block(rep, args.steps, args.warmup == 0))
-    rep_info = pipe.last_launch_info()
-    del rep
+    if launch_timing:
+        # the repetition's last call: all K steps (K2/K3 chains) or one 64-spp step
+        if dispatch:
+            step_block(rep, args.warmup, True)
+            pipe.set_launch_timing(True)
+            step_block(rep, args.steps, args.warmup == 0)
+        else:
+            pipe.set_launch_timing(True)
+            step_block(rep, 1, False)
+        k_s, k_launches = pipe.last_call_kernel_time()
+        pipe.set_launch_timing(False)
+        torch.cuda.synchronize()
+        del rep
+        kernel_how = {"how": "an identical repetition of the timed call right after the "
+                             "region, timing events carried by its launches' dispatch "
+                             "packets (rt_set_launch_timing)", "launches": k_launches,
+                      "us": round(k_s * 1e6, 3)}
+    else:
+        # HIP events over an identical repetition of the timed call (the same reset and
+        # frames on the scratch renderer), issued at once while the GPU is as warm as in the
+        # region (a host-side check first would let its clock drop)
+        if dispatch:
+            step_block(rep, args.warmup, True)
+        rep_s = timed(stream, lambda: step_block(rep, args.steps, args.warmup == 0))
+        del rep
+        kernel_how = {"how": "HIP events over an identical repetition of the timed call",
+                      "us_per_step": round(rep_s / args.steps * 1e6, 3)}
     # the job's one gather of the finished tiles, timed on its own (barrier on both sides)
     e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t1 = time.perf_counter()
@@ -861,7 +896,10 @@ def main(argv=None):
     total_launches = info["launches"] * (1 if dispatch else args.steps)
     launches_per_step = total_launches / args.steps
     queues = max(1, info.get("queues", 1))
-    launch_s = rep_s / max(1, total_launches // queues)
+    if launch_timing:
+        launch_s = k_s / max(1, k_launches)
+    else:
+        launch_s = rep_s / max(1, total_launches // queues)
     value = w * h * spf * args.steps / dt / 1e6
 
     kernel = info["kernel_name"]
@@ -881,8 +919,7 @@ def main(argv=None):
     roof = roofline(kernel, launch_s, bytes_launch, pmc, pmc_path, pq,
                     {"frames_per_launch": fpl, "launches_per_step": launches_per_step,
                      "queues": queues, "submit": info.get("submit"),
-                     "events_repetition": {"us_per_step": round(rep_s / args.steps * 1e6, 3),
-                                           "kernel": rep_info["kernel_name"]}})
+                     "kernel_time": kernel_how})
 
     segs = fixture_segments(cfg, frames_total)
     if dispatch and depth == 1:

@@ -134,6 +134,11 @@ struct rt_ctx {
     uint64_t unit_cap = 0;
     uint64_t unit_key[5] = {~0ull, 0, 0, 0, 0};
     int cus = 0;                        // compute units of `device` (0: not queried yet)
+    // rt_set_launch_timing: events the fused launches of each call carry, and how many
+    // launches the last call timed
+    hipEvent_t time_ev[2] = {};
+    bool timing = false;
+    uint32_t timed_launches = 0;
 };
 
 namespace {
@@ -1357,6 +1362,8 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->d_sph);
         (void)hipFree(ctx->d_flag);
         (void)hipFree(ctx->d_band_src);
+        for (hipEvent_t ev : ctx->time_ev)
+            if (ev) (void)hipEventDestroy(ev);
         (void)hipFree(ctx->d_srgb);
         (void)hipFree(ctx->d_hx);
         (void)hipFree(ctx->tile_cost);
@@ -1586,6 +1593,17 @@ rt_status update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t w,
         if (rt_status s = usable_chain(ctx, p, &fl.chain)) return s;
     rtc::Chain* const chain = fl.chain;
     uint32_t seg_parts = 0, seg_packets = 0;
+    // launch timing (rt_set_launch_timing): armed for this call's fused launches, disarmed on
+    // every exit path
+    struct Timing {
+        rt_ctx* ctx;
+        explicit Timing(rt_ctx* c) : ctx(c) {
+            if (ctx->timing) rtk::arm_launch_events(ctx->time_ev[0], ctx->time_ev[1]);
+        }
+        ~Timing() {
+            if (ctx->timing) ctx->timed_launches = rtk::disarm_launch_events();
+        }
+    } timing_scope{ctx};
     for (uint32_t f0 = 0; f0 < frames; f0 += per) {
         const uint32_t nf = std::min<uint32_t>(per, frames - f0);
         p.in = img[cur];
@@ -1782,6 +1800,35 @@ rt_status rt_update_frames_bands(rt_ctx* ctx, float* image_a, float* image_b, ui
     if (!bands) return fail(RT_ERR_INVALID_ARGUMENT, "bands is NULL");
     return update_frames(ctx, image_a, image_b, w, h, *bands, cam, spheres, count, frames,
                          seeds, stream_v, out_newest);
+}
+
+rt_status rt_set_launch_timing(rt_ctx* ctx, int enable) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    if (enable && !ctx->time_ev[0]) {
+        for (int i = 0; i < 2; ++i) {
+            hipError_t e = hipEventCreate(&ctx->time_ev[i]);
+            if (e != hipSuccess) return hip_fail(e, "hipEventCreate(launch timing)");
+        }
+    }
+    ctx->timing = enable != 0;
+    ctx->timed_launches = 0;
+    return RT_OK;
+}
+
+rt_status rt_last_call_kernel_time(rt_ctx* ctx, float* out_ms, uint32_t* out_launches) {
+    if (!ctx) return fail(RT_ERR_INVALID_CONTEXT, "ctx is NULL");
+    if (!out_ms) return fail(RT_ERR_INVALID_ARGUMENT, "out_ms is NULL");
+    if (!ctx->timing || ctx->timed_launches == 0)
+        return fail(RT_ERR_INVALID_ARGUMENT, "the last call carried no timed launch");
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
+    hipError_t e = hipEventSynchronize(ctx->time_ev[1]);
+    if (e == hipSuccess) e = hipEventElapsedTime(out_ms, ctx->time_ev[0], ctx->time_ev[1]);
+    if (e != hipSuccess) return hip_fail(e, "hipEventElapsedTime(launch timing)");
+    if (out_launches) *out_launches = ctx->timed_launches;
+    return RT_OK;
 }
 
 rt_status rt_band_costs(rt_ctx* ctx, uint32_t w, uint32_t h, const rt_band_set* bands,

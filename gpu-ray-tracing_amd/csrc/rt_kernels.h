@@ -202,6 +202,11 @@ constexpr uint32_t pack_bands(uint32_t first, uint32_t step, bool ordered) {
     return first | ((step < 0x7FFFu ? step : 0x7FFFu) << 16) | (ordered ? 1u << 31 : 0u);
 }
 hipError_t launch_trace(const TraceParams& p, int kernel, hipStream_t stream);
+// Launch timing (rt_set_launch_timing): arm two timing events for this host thread's next
+// fused launches (rt_trace_kernel / rt_tpair_kernel / rt_bounce_kernel: start on the first,
+// stop on every one); disarm returns how many launches carried them.
+void arm_launch_events(hipEvent_t start, hipEvent_t stop);
+uint32_t disarm_launch_events();
 // out[y][x] = gathered[band_src[y / 8] + y % 8][x] (rt_deinterleave_bands)
 hipError_t launch_deinterleave_bands(const float4* gathered, float4* out, uint32_t width,
                                      uint32_t height, const uint32_t* band_src,

@@ -12,6 +12,7 @@
 // The 32-byte material record is fetched only for the winning hit.  Each lane keeps its
 // pixel's accumulator in registers across fused frames and writes it back with one
 // coalesced 16-byte store (one HBM read + one write per pixel per launch).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "rt_device.h"
@@ -3112,6 +3113,22 @@ static dim3 tile_grid(const TraceParams& p, uint32_t waves = 4) {
 // per-launch symbol lookup or per-argument marshalling of the 2.6-KB TraceParams block.
 // Slots: 0-4 rt_trace_kernel<k>, 5-8 rt_bounce_kernel<m>, 9-10 rt_tpair_kernel<4 / 2>.
 constexpr int kLaunchSlots = 12;
+// Launch timing (rt_set_launch_timing): while armed, launch_packed goes through
+// hipExtModuleLaunchKernel with the armed events — the start event on the first launch
+// after arming, the stop event on every launch — so the dispatch packets themselves carry
+// the timestamps (no marker packets on the stream, which cost an idle GPU's short region
+// ≈ 2.5 µs).  Per host thread, like the calls that arm it.
+static thread_local hipEvent_t g_ev_start = nullptr, g_ev_stop = nullptr;
+static thread_local uint32_t g_ev_launches = 0;
+void arm_launch_events(hipEvent_t start, hipEvent_t stop) {
+    g_ev_start = start;
+    g_ev_stop = stop;
+    g_ev_launches = 0;
+}
+uint32_t disarm_launch_events() {
+    g_ev_start = g_ev_stop = nullptr;
+    return g_ev_launches;
+}
 static hipError_t launch_packed(int slot, const void* sym, dim3 grid, dim3 block, size_t lds,
                                 hipStream_t stream, void* args, size_t bytes) {
     constexpr int kMaxDevices = 64;
@@ -3130,6 +3147,17 @@ static hipError_t launch_packed(int slot, const void* sym, dim3 grid, dim3 block
     }
     void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes,
                      HIP_LAUNCH_PARAM_END};
+    if (g_ev_stop) {
+        // (global work sizes in work-items)
+        e = hipExtModuleLaunchKernel(fn[dev][slot], grid.x * block.x, grid.y * block.y,
+                                     grid.z * block.z, block.x, block.y, block.z, lds, stream,
+                                     nullptr, extra, g_ev_start, g_ev_stop, 0);
+        if (e == hipSuccess) {
+            g_ev_start = nullptr;
+            ++g_ev_launches;
+        }
+        return e;
+    }
     return hipModuleLaunchKernel(fn[dev][slot], grid.x, grid.y, grid.z, block.x, block.y,
                                  block.z, (unsigned)lds, stream, nullptr, extra);
 }

@@ -143,6 +143,8 @@ _SIGS = {
     "rt_partition_bands": (ctypes.c_int, [P, U32, U32, P]),
     "rt_deinterleave_bands": (ctypes.c_int, [P, P, P, U32, U32, U32, P, U32, P]),
     "rt_gather_bands": (ctypes.c_int, [P, P, P, P, P, U32, U32, P, U32, P]),
+    "rt_set_launch_timing": (ctypes.c_int, [P, ctypes.c_int]),
+    "rt_last_call_kernel_time": (ctypes.c_int, [P, ctypes.POINTER(F), ctypes.POINTER(U32)]),
 }
 
 

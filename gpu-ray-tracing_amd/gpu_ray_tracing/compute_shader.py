@@ -186,6 +186,18 @@ class ComputeShaderPipeline:
             d["kernel_name"] = d["kernel_name"].replace("rt_single_kernel", "rt_chain_kernel")
         return d
 
+    def set_launch_timing(self, enable: bool) -> None:
+        """rt_set_launch_timing: the fused launches of each update_frames call carry timing
+        events in their own dispatch packets (no marker packets on the stream)."""
+        _lib.call("rt_set_launch_timing", self._ctx, 1 if enable else 0)
+
+    def last_call_kernel_time(self) -> tuple[float, int]:
+        """rt_last_call_kernel_time: (seconds from the start of the last call's first timed
+        launch to the end of its last, launches timed); waits for that launch."""
+        ms, n = ctypes.c_float(0.0), _lib.U32(0)
+        _lib.call("rt_last_call_kernel_time", self._ctx, ctypes.byref(ms), ctypes.byref(n))
+        return ms.value / 1e3, int(n.value)
+
     def candidate_stats(self) -> dict:
         """rt_candidate_stats: the camera rays' per-tile candidate lists built last."""
         out = (ctypes.c_uint64 * 5)()

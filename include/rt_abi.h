@@ -385,6 +385,17 @@ RT_API rt_status rt_set_update_queues(rt_ctx* ctx, uint32_t queues);
 #define RT_SUBMIT_HIP 1
 #define RT_SUBMIT_AQL 2
 RT_API rt_status rt_set_update_submit(rt_ctx* ctx, int mode);
+/* Launch timing (ABI 7, diagnostic): while enabled, the fused launches of each
+ * rt_update_frames / rt_update_frames_bands call (the frame-chain, fused camera-ray and bounce
+ * instances) carry the context's two timing events in their own dispatch packets
+ * (hipExtModuleLaunchKernel: no marker packets on the stream); rt_last_call_kernel_time then
+ * gives the time from the start of the call's first such launch to the end of its last
+ * (milliseconds; synchronous: waits for that launch) and how many launches carried them.
+ * RT_ERR_INVALID_ARGUMENT when the last call had none (one-frame launches, AQL packets).
+ * Pixel results are identical; the ext launch path costs a call on an idle GPU ≈ 9 µs more
+ * (profiles/r06/r06i/), so time what it measures apart from wall-clock regions. */
+RT_API rt_status rt_set_launch_timing(rt_ctx* ctx, int enable);
+RT_API rt_status rt_last_call_kernel_time(rt_ctx* ctx, float* out_ms, uint32_t* out_launches);
 /* Whether AQL submission is available on the context's device (*aql_available; if not,
  * rt_last_error() says why), whether a go wait gave up (*go_give_ups, 0 or 1: a segment
  * whose caller's stream had not reached it within the bound; its frames were dropped; 0 in

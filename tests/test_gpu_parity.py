@@ -1231,3 +1231,32 @@ def test_band_set_equals_stripes(rt):
                                   cam, sc, g["seeds"][:1])        # step 0
     finally:
         p.close()
+
+
+def test_launch_timing_keeps_bits(rt):
+    """rt_set_launch_timing: the fused launches carry the timing events in their own dispatch
+    packets (hipExtModuleLaunchKernel); the image is the same bits (bench fixture's 25-frame
+    digest), the time is positive and covers the call's launches, and a call of one-frame
+    launches reports no timed launch."""
+    g = load_golden("bench_k3.npz")
+    w, h = int(g["width"]), int(g["height"])
+    cam, sc = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"])
+    k = list(g["frame_counts"]).index(25)
+    p = rt.ComputeShaderPipeline(0)
+    try:
+        p.set_frame_images("every")
+        p.set_launch_timing(True)
+        a, b = p.new_image(w, h), p.new_image(w, h)
+        if p.update_frames(a, b, w, h, cam, sc, g["seeds"][:5]) == 1:
+            a, b = b, a
+        newest = p.update_frames(a, b, w, h, cam.with_fields(camera_has_moved=0.0), sc,
+                                 g["seeds"][5:25])
+        t, n = p.last_call_kernel_time()
+        assert n == p.last_launch_info()["launches"] == 1 and 1e-6 < t < 0.1
+        assert canon_sha(host(b if newest == 1 else a)) == str(g["sha256"][k])
+        p.set_frames_per_launch(1)
+        p.update_frames(a, b, w, h, cam, sc, g["seeds"][:2])
+        with pytest.raises(rt.RtError):
+            p.last_call_kernel_time()
+    finally:
+        p.close()

@@ -6,6 +6,8 @@ frames.  Variants of the region:
   ev     HIP events recorded around the call (bench.py's region before round 6)
   noev   no events: synchronize, clock, call, synchronize, clock
   stream the closing wait is the stream's synchronize instead of the device's
+  ext    no events on the stream; the launch itself carries the timing events
+         (rt_set_launch_timing: hipExtModuleLaunchKernel), read after the region
 Also times an empty region (synchronize, clock, synchronize) and a 1-block kernel launch +
 synchronize (torch's fill on a 4-byte tensor) for the host/runtime floor.
 usage: python tools/call_latency.py [N] [rank] [reps]"""
@@ -60,17 +62,24 @@ def region(F, variant):
         e1.record(stream)
         torch.cuda.synchronize()
         return time.perf_counter() - t0, e0.elapsed_time(e1) / 1e3
+    pipe.set_launch_timing(variant == "ext")
     t0 = time.perf_counter()
     r.frames(cam_t, sc, seeds[5:5 + F])
     if variant == "stream":
         stream.synchronize()
     else:
         torch.cuda.synchronize()
-    return time.perf_counter() - t0, None
+    t = time.perf_counter() - t0
+    if variant == "ext":
+        try:
+            return t, pipe.last_call_kernel_time()[0]
+        except Exception:          # noqa: BLE001  (a one-frame call carries none)
+            return t, None
+    return t, None
 
 
 out = {"share": f"rank {RANK} of {N}", "reps": R, "kernel": None, "frames": list(FS)}
-for variant in ("ev", "noev", "stream"):
+for variant in ("ev", "noev", "stream", "ext", "noev"):
     rows = {}
     for F in FS:
         wall, ev = [], []
@@ -89,7 +98,7 @@ for variant in ("ev", "noev", "stream"):
     mx, my = st.mean(xs), st.mean(ys)
     b = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sum((x - mx) ** 2 for x in xs)
     rows["fit"] = {"fixed_us": round(my - b * mx, 2), "per_frame_us": round(b, 3)}
-    out[variant] = rows
+    out[variant if variant not in out else variant + "_again"] = rows
 out["kernel"] = pipe.last_launch_info()["kernel_name"]
 
 # host/runtime floor: an empty region, and one tiny kernel + synchronize
