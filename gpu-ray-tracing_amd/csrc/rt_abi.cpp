@@ -1777,6 +1777,14 @@ bool band_sources(uint32_t h, uint32_t nranks, const rt_band_set* sets, uint32_t
 
 }  // namespace
 
+namespace rti {
+bool band_sets_cover(uint32_t h, uint32_t nranks, const rt_band_set* sets,
+                     uint32_t rows_per_rank) {
+    std::vector<uint32_t> src;
+    return band_sources(h, nranks, sets, rows_per_rank, src);
+}
+}  // namespace rti
+
 extern "C" {
 
 rt_status rt_update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t w, uint32_t h,

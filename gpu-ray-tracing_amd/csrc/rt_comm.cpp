@@ -238,6 +238,9 @@ rt_status rt_gather_bands(rt_ctx* ctx, rt_comm* comm, const float* local, float*
     for (uint32_t r = 0; r < comm->nranks; ++r)
         rows = std::max(rows, sets[r].count * (uint32_t)RT_STRIPE_ROWS);
     if (rows == 0) return fail(RT_ERR_INVALID_ARGUMENT, "the band sets hold no band");
+    // (checked before the collective, on every rank: the root would refuse them after it)
+    if (!rti::band_sets_cover(height, comm->nranks, sets, rows))
+        return fail(RT_ERR_INVALID_ARGUMENT, "band sets must cover every band once");
     DeviceGuard guard(comm->device);
     if (!guard.ok) return fail(RT_ERR_INVALID_DEVICE, "hipSetDevice failed");
     hipStream_t stream = static_cast<hipStream_t>(stream_v);

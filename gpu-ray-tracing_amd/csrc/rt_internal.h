@@ -17,6 +17,10 @@ rt_status hip_fail(hipError_t e, const char* what);
 rt_status check_image(uint32_t w, uint32_t h);
 // The HIP device of a context (rt_create's argument).
 int ctx_device(const rt_ctx* ctx);
+// Whether nranks band sets cover every band of a height-row image exactly once, each within
+// rows_per_rank rows (rt_deinterleave_bands' precondition).
+bool band_sets_cover(uint32_t height, uint32_t nranks, const rt_band_set* sets,
+                     uint32_t rows_per_rank);
 
 // Switches to a device for the duration of a call.
 struct DeviceGuard {

@@ -475,3 +475,107 @@ def test_timed_region_excludes_closing_barrier():
         assert ts["dt"] <= max(ts["per_rank"]) + ts["start_skew_s"] + 1e-6
         assert 0.02 <= ts["per_rank"][1] < 0.02 + 0.2, ts
         assert ts["barrier_s"] >= 0.4, ts
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h", [(40, 32), (24, 44)])
+def test_gather_bands_abi_single_rank(rt, w, h):
+    """rt_gather_bands behind the C ABI on one GPU (one-rank communicator): a one-rank
+    "partition" whose band set is a contiguous range covering the image, rendered with
+    rt_update_frames_bands and gathered by ncclGather + the band-set de-interleave; equal
+    to the oracle's render bit for bit; a partition that does not cover the image is
+    refused."""
+    import ctypes
+    import gpu_ray_tracing as rt_
+    from gpu_ray_tracing.distributed import StripeComm, StripeRenderer
+    from oracle import oracle as O
+    pipe = rt.ComputeShaderPipeline(0)
+    comm = StripeComm(pipe, StripeComm.unique_id(), 1, 0)
+    try:
+        sc = rt.create_default_spheres(seed=9)
+        seeds = rt.frame_seeds(33, 3)
+        cam = rt.SceneCamera.from_settings(
+            rt.CameraSettings(max_depth=3, samples_per_pixel=500), w, h, float(seeds[0]))
+        nb = (h + 7) // 8
+        r = StripeRenderer(pipe, w, h, 0, 1, comm=comm, partition=[(0, 1, nb)])
+        r.frames(cam, sc, seeds)
+        img = r.finish()
+        full, _ = O.render(np.zeros((h, w, 4), np.float32), cam.blob, sc.spheres, seeds)
+        got = img.cpu().numpy()
+        assert got.shape == (h, w, 4)
+        assert np.array_equal(got.view(np.uint32), full.view(np.uint32))
+        bad = rt_._lib.band_sets([(0, 1, nb - 1)])               # misses the last band
+        out = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+        rc = rt_._lib.lib().rt_gather_bands(pipe._ctx, comm._comm, ctypes.c_void_p(r.local.data_ptr()),
+                                            None, ctypes.c_void_p(out.data_ptr()), w, h, bad, 0,
+                                            pipe._stream())
+        assert rc == 1
+        torch.cuda.synchronize()
+    finally:
+        comm.close()
+        pipe.close()
+
+
+def _hip_partition_worker(rank, world, port, w, h, dst, part, q):
+    """One rank of a partitioned StripeRenderer job on the HIP pipeline (GPU 0, gloo)."""
+    sys.path[:0] = [str(PKG_DIR), str(ROOT)]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        import gpu_ray_tracing as rt
+        from gpu_ray_tracing.distributed import StripeRenderer
+        from oracle import oracle as O
+        sc = rt.create_default_spheres(seed=6)
+        seeds = rt.frame_seeds(14, 5)
+        moved = rt.SceneCamera.from_settings(
+            rt.CameraSettings(max_depth=4, samples_per_pixel=500), w, h, float(seeds[0]))
+        still = moved.with_fields(camera_has_moved=0.0)
+        pipe = rt.ComputeShaderPipeline(0)
+        r = StripeRenderer(pipe, w, h, rank, world, partition=part)
+        r.frames(moved, sc, seeds[:2])
+        pipe.set_frames_per_launch(1)
+        r.frames(still, sc, seeds[2:5])
+        img = r.finish(dst=dst)
+        if rank == dst:
+            full, _ = O.render(np.zeros((h, w, 4), np.float32), moved.blob, sc.spheres, seeds[:2])
+            full, _ = O.render(full, still.blob, sc.spheres, seeds[2:5])
+            got = img.cpu().numpy()
+            q.put(bool(got.shape == (h, w, 4)
+                       and np.array_equal(got.view(np.uint32), full.view(np.uint32))))
+        else:
+            assert img is None
+        torch.cuda.synchronize()
+        pipe.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,w,h,dst,part", [
+    (2, 40, 40, 0, [(0, 1, 2), (2, 1, 3)]),              # contiguous ranges
+    (3, 33, 44, 1, [(0, 3, 2), (1, 4, 2), (2, 2, 2)]),    # mixed steps, a ragged last band
+])
+def test_partitioned_renderer_hip_multiprocess(world, w, h, dst, part):
+    """A non-round-robin partition on the GPU: `world` processes render their band sets with
+    rt_update_frames_bands (fused and one launch per frame), the tiles gathered to `dst` and
+    scattered by rt_deinterleave_bands — bit-identical to the oracle's render."""
+    covered = sorted(f + j * st for f, st, c in part for j in range(c))
+    assert covered == list(range((h + 7) // 8))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hip_partition_worker, args=(r, world, port, w, h, dst, part, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        for p in procs:
+            p.join(timeout=240)
+            assert p.exitcode == 0
+        assert q.get(timeout=5) is True
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
