@@ -1873,34 +1873,51 @@ rt_status rt_partition_bands(const double* cost, uint32_t nbands, uint32_t nrank
     for (uint32_t b = 0; b < nbands; ++b)
         if (!(cost[b] >= 0.0) || !std::isfinite(cost[b]))
             return fail(RT_ERR_INVALID_ARGUMENT, "band costs must be finite and >= 0");
-    // best[k][i]: the smallest largest-range cost of bands [0, i) in k ranges; cut[k][i] the
-    // start of the last range (the earliest among equals)
+    // The smallest largest-range cost B* over all cuts into at most nranks contiguous ranges
+    // (a range's cost: the difference of prefix sums), by bisection over B with the greedy
+    // test "ranges as long as they fit under B" (O(bands) per step, memory O(bands)).  The
+    // test is monotone in B and changes only at range costs, so once lo < hi are adjacent
+    // doubles with hi feasible and lo not, B* = hi exactly.  The cut under hi then takes
+    // ranges as long as fit but always leaves one band for each rank still to come, so it
+    // uses min(nranks, nbands) ranges: once that bound binds, every later range is one band,
+    // which fits (B* >= every band's cost).
     std::vector<double> pre(nbands + 1, 0.0);
     for (uint32_t b = 0; b < nbands; ++b) pre[b + 1] = pre[b] + cost[b];
-    const uint32_t K = std::min(nranks, std::max(nbands, 1u));
-    std::vector<std::vector<double>> best(K + 1, std::vector<double>(nbands + 1, INFINITY));
-    std::vector<std::vector<uint32_t>> cut(K + 1, std::vector<uint32_t>(nbands + 1, 0));
-    best[0][0] = 0.0;
-    for (uint32_t k = 1; k <= K; ++k)
-        for (uint32_t i = 0; i <= nbands; ++i)
-            for (uint32_t j = 0; j <= i; ++j) {
-                const double v = std::max(best[k - 1][j], pre[i] - pre[j]);
-                if (v < best[k][i]) {
-                    best[k][i] = v;
-                    cut[k][i] = j;
-                }
-            }
-    std::vector<uint32_t> start(K + 1, 0);
-    start[K] = nbands;
-    for (uint32_t k = K, i = nbands; k >= 1; --k) {
-        start[k - 1] = cut[k][i];
-        i = cut[k][i];
+    auto cuts = [&](double B, std::vector<uint32_t>* starts) -> uint64_t {
+        uint64_t n = 0;
+        for (uint32_t i = 0; i < nbands;) {
+            uint32_t j = i + 1;                      // a range holds at least one band
+            if (pre[j] - pre[i] > B) return UINT64_MAX;
+            // (the final cut: leave a band for each of the ranks after this one)
+            const uint64_t left = starts && nranks > n + 1 ? nranks - n - 1 : 0;
+            const uint32_t jmax = left >= nbands ? i + 1
+                                                 : std::max<uint32_t>(i + 1, nbands - (uint32_t)left);
+            while (j < jmax && pre[j + 1] - pre[i] <= B) ++j;
+            if (starts) starts->push_back(i);
+            ++n;
+            i = j;
+        }
+        return n;
+    };
+    double lo = 0.0, hi = pre[nbands];
+    for (uint32_t b = 0; b < nbands; ++b) lo = std::max(lo, cost[b]);
+    if (cuts(lo, nullptr) <= nranks) {
+        hi = lo;
+    } else {
+        for (int it = 0; it < 2200; ++it) {              // (2^-1074 steps cover any range)
+            const double mid = lo + (hi - lo) / 2.0;
+            if (!(mid > lo && mid < hi)) break;
+            if (cuts(mid, nullptr) <= nranks) hi = mid; else lo = mid;
+        }
     }
+    std::vector<uint32_t> starts;
+    cuts(hi, &starts);
+    starts.push_back(nbands);
     for (uint32_t r = 0; r < nranks; ++r) {
-        if (r < K)
-            out[r] = {start[r], 1u, start[r + 1] - start[r]};
+        if (r + 1 < starts.size())
+            out[r] = {starts[r], 1u, starts[r + 1] - starts[r]};
         else
-            out[r] = {0u, 1u, 0u};   // more ranks than bands: the rest hold none
+            out[r] = {0u, 1u, 0u};   // no band left (more ranks than ranges)
     }
     return RT_OK;
 }

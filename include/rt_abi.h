@@ -474,9 +474,11 @@ RT_API rt_status rt_band_costs(rt_ctx* ctx, uint32_t width, uint32_t height,
                                const rt_band_set* bands, double* out_cost);
 /* Cost-balanced partition (host only): the nbands bands, band b costing band_cost[b] >= 0,
  * cut into nranks contiguous ranges (out[r] = {first_r, 1, count_r}, in band order, a range
- * may be empty) that minimise the largest range cost (exact, by dynamic programming; ties
- * to the earliest cut).  Any partition gives bit-identical pixels: every seed is a function
- * of the global pixel (wgsl:309-311, 353). */
+ * may be empty; empty ones are {0, 1, 0}) that minimise the largest range cost — exactly:
+ * bisection over that cost with a greedy cut, O(nbands) memory; among optimal cuts one that
+ * gives every rank a band while there are bands (ranges as long as fit, in order, each
+ * leaving a band for every later rank).  Any partition gives bit-identical
+ * pixels: every seed is a function of the global pixel (wgsl:309-311, 353). */
 RT_API rt_status rt_partition_bands(const double* band_cost, uint32_t nbands, uint32_t nranks,
                                     rt_band_set* out);
 /* Root side of a band-set gather: `gathered` holds nranks compact buffers back to back in

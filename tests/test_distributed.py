@@ -231,7 +231,8 @@ def test_partitioned_renderer_finish_gloo(world, w, h, dst, costs):
 
 def test_partition_bands_is_optimal():
     """rt_partition_bands against brute force over every contiguous cut: the largest range
-    cost is the minimum, the ranges are contiguous, in order and cover every band once."""
+    cost is the minimum, the ranges are contiguous, in order, cover every band once, and
+    every rank gets a band while there are bands; a 65 536-band, 1 000-rank cut is quick."""
     import itertools
     from gpu_ray_tracing import partition_bands
     rng = np.random.default_rng(4)
@@ -246,11 +247,17 @@ def test_partition_bands_is_optimal():
             assert st == 1 and (c == 0 or f == pos)
             pos += c
         assert pos == nb
+        assert sum(1 for _, _, c in part if c) == min(world, nb)
         got = max(costs[f:f + c].sum() for f, _, c in part)
         best = min(max(costs[a:b].sum() for a, b in zip((0,) + cut, cut + (nb,)))
                    for cut in itertools.combinations_with_replacement(range(nb + 1), world - 1)
                    if list(cut) == sorted(cut))
         assert got == best, (costs, world, part)
+    import time
+    big = rng.random(65536)
+    t0 = time.perf_counter()
+    part = partition_bands(big, 1000)
+    assert time.perf_counter() - t0 < 5.0 and sum(c for _, _, c in part) == 65536
 
 
 def test_band_set_errors(rt):
@@ -260,6 +267,7 @@ def test_band_set_errors(rt):
     with pytest.raises(rt.RtError):
         partition_bands([1.0, float("nan")], 2)
     assert partition_bands([], 3) == [(0, 1, 0)] * 3
+    assert partition_bands([5.0, 1, 1, 1, 1, 1], 3) == [(0, 1, 1), (1, 1, 4), (5, 1, 1)]
 
 
 def _hip_renderer_worker(rank, world, port, w, h, dst, q):
