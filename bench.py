@@ -475,18 +475,29 @@ def runtime_floor_us(reps=50):
     return round(statistics.median(t) * 1e6, 2)
 
 
-def roofline(kernel, launch_s, bytes_launch, pmc, pmc_path, parts=1, extra=None):
+def roofline(kernel, launch_s, bytes_launch, pmc, pmc_path, parts=1, extra=None,
+             ref_bytes=None):
     """The roofline object of the timed kernel: HBM bytes moved against 8 TB/s, and — when a
     PMC summary of that kernel instance is committed — the VALU issue it measured against
-    the VALU peak (then the bound: these kernels issue far more VALU than they move bytes)."""
+    the VALU peak (then the bound: these kernels issue far more VALU than they move bytes).
+    ref_bytes: the reference's per-dispatch traffic for the same frames (32 B per pixel and
+    frame, SURVEY §8d B_comp), reported beside the bytes actually moved, labelled."""
     gbs = bytes_launch / launch_s / 1e9
     hbm = {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
            "frac": round(gbs / PEAK_HBM_GBS, 4),
            "algorithmic_bytes_per_launch": int(bytes_launch),
            "practical_floor_frac": round(gbs / RMW_FLOOR_GBS, 4)}
+    if ref_bytes and ref_bytes != bytes_launch:
+        hbm["reference_semantics"] = {
+            "bytes_per_launch": int(ref_bytes),
+            "frac": round(ref_bytes / launch_s / 1e9 / PEAK_HBM_GBS, 4),
+            "what": "the reference's 32 B per pixel and frame (a load and a store per "
+                    "dispatch, SURVEY §8d B_comp progressive) over the same time: traffic "
+                    "the fused kernel does not move, an effective-bandwidth figure only"}
     traffic = None
     if pmc and "hbm_bytes_per_launch" in pmc:
         traffic = pmc["hbm_bytes_per_launch"] * parts
+        hbm["traffic_GBs"] = round(traffic / launch_s / 1e9, 1)
     roof = {"bound": "hbm", **hbm, "traffic": traffic, "kernel": kernel,
             "kernel_avg_us": round(launch_s * 1e6, 2)}
     if pmc and pmc.get("valu_insts_per_launch"):
@@ -916,10 +927,11 @@ def main(argv=None):
         bytes_launch = local_px * 16 * 3
     pmc, pmc_path = load_pmc(cfg, kernel, fpl, queues) if world == 1 else (None, None)
     pq = pmc.get("queues", 1) if pmc else 1
-    roof = roofline(kernel, launch_s, bytes_launch, pmc, pmc_path, pq,
-                    {"frames_per_launch": fpl, "launches_per_step": launches_per_step,
-                     "queues": queues, "submit": info.get("submit"),
-                     "kernel_time": kernel_how})
+    ref_bytes = local_px * BYTES_PER_PIXEL_LAUNCH * fpl   # the reference: one dispatch per frame
+    roof = roofline(kernel, launch_s, bytes_launch, pmc, pmc_path, pq, ref_bytes=ref_bytes,
+                    extra={"frames_per_launch": fpl, "launches_per_step": launches_per_step,
+                           "queues": queues, "submit": info.get("submit"),
+                           "kernel_time": kernel_how})
 
     segs = fixture_segments(cfg, frames_total)
     if dispatch and depth == 1:

@@ -87,3 +87,18 @@ def test_fixtures_carry_band_digests(bench):
         assert bands is not None and bands.shape == (h // 8, 32), cfg
         assert segs is not None and segs > 0, cfg
     assert bench._fixture("K5")["px"].size >= 16384
+
+
+def test_roofline_object(bench):
+    """The roofline of a timed launch: HBM bytes against 8 TB/s, and with a PMC summary of
+    the kernel the VALU issue fraction as the bound (SQ_INSTS_VALU x 2 cycles over 1024
+    SIMDs x 2.4 GHz x the launch time), the PMC bytes as `traffic`; the reference's per-frame
+    bytes beside the moved ones when they differ (a fused chain)."""
+    r = bench.roofline("k", 100e-6, 400e6, None, None)
+    assert r["bound"] == "hbm" and r["frac"] == 0.5 and r["traffic"] is None
+    pmc = {"valu_insts_per_launch": 1e8, "hbm_bytes_per_launch": 2e8}
+    r = bench.roofline("k", 100e-6, 400e6, pmc, "p.json", ref_bytes=800e6)
+    assert r["bound"] == "valu" and r["pmc"] == "p.json" and r["traffic"] == 2e8
+    assert abs(r["frac"] - 1e8 * 2 / (1024 * 2.4e9 * 100e-6)) < 1e-4
+    assert r["hbm"]["frac"] == 0.5 and r["hbm"]["traffic_GBs"] == 2000.0
+    assert r["hbm"]["reference_semantics"]["frac"] == 1.0
