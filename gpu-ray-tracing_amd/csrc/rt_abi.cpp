@@ -1845,7 +1845,10 @@ rt_status rt_band_costs(rt_ctx* ctx, uint32_t w, uint32_t h, const rt_band_set* 
     if (!bands || !out_cost) return fail(RT_ERR_INVALID_ARGUMENT, "NULL bands or out_cost");
     const uint32_t group = ctx->cost_key[5];
     const uint32_t want[5] = {w, h, bands->first, bands->step, bands->count};
-    if (!ctx->cost_key_ok || !ctx->tile_cost || !std::equal(want, want + 5, ctx->cost_key))
+    // (and for the lists the context holds now: another camera geometry, scene or share
+    // since then starts a new generation, whose costs are not measured yet)
+    if (!ctx->cost_key_ok || !ctx->tile_cost || !std::equal(want, want + 5, ctx->cost_key) ||
+        ctx->cost_gen != ctx->cand_gen)
         return fail(RT_ERR_INVALID_ARGUMENT, "no tile costs recorded for this share");
     const uint32_t tiles_x = (((w + 7u) >> 3) + group - 1u) / group;
     const uint64_t units = (uint64_t)tiles_x * bands->count;

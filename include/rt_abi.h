@@ -467,8 +467,9 @@ RT_API rt_status rt_update_frames_bands(rt_ctx* ctx, float* image_a, float* imag
 /* The per-band costs the context's last cost-recording launch measured (the fused
  * launches' per-tile durations in device clock ticks, summed over each local band's tiles;
  * rt_set_tile_order), for that launch's share: out_cost[j] for local band j of `bands`,
- * which must be the band set (and width, height) that launch ran — RT_ERR_INVALID_ARGUMENT
- * when it is not or no launch has recorded costs.  Synchronous (reads the costs back on the
+ * which must be the band set (and width, height) that launch ran, with the same camera
+ * geometry and scene since — RT_ERR_INVALID_ARGUMENT otherwise, or when no launch has
+ * recorded costs.  Synchronous (reads the costs back on the
  * context's device with a blocking copy). */
 RT_API rt_status rt_band_costs(rt_ctx* ctx, uint32_t width, uint32_t height,
                                const rt_band_set* bands, double* out_cost);
