@@ -258,6 +258,20 @@ def load_pmc(config, kernel, frames_per_launch, queues=1):
     return None, None
 
 
+def load_weighted(config, kernel, pmc_path):
+    """The weighted VALU cycles per launch of the timed kernel (tools/valu_weighted.py: the
+    PMC's instruction classes priced at the kernel's own forms' measured issue costs), if
+    committed for that kernel and that PMC summary, and its path."""
+    for rnd in ("r06",):
+        p = ROOT / "profiles" / f"valu_weighted_{rnd}_{config}.json"
+        if not p.exists():
+            continue
+        d = json.loads(p.read_text())
+        if d.get("kernel") == kernel and d.get("pmc") == pmc_path:
+            return d, p.relative_to(ROOT).as_posix()
+    return None, None
+
+
 # ---- image checks against the committed fixtures ---------------------------------------
 def canon_sha(a) -> str:
     """SHA-256 of a float32 image's bytes with every NaN as 0x7FC00000 (the parity tests
@@ -476,7 +490,7 @@ def runtime_floor_us(reps=50):
 
 
 def roofline(kernel, launch_s, bytes_launch, pmc, pmc_path, parts=1, extra=None,
-             ref_bytes=None):
+             ref_bytes=None, weighted=None):
     """The roofline object of the timed kernel: HBM bytes moved against 8 TB/s, and — when a
     PMC summary of that kernel instance is committed — the VALU issue it measured against
     the VALU peak (then the bound: these kernels issue far more VALU than they move bytes).
@@ -511,6 +525,16 @@ def roofline(kernel, launch_s, bytes_launch, pmc, pmc_path, parts=1, extra=None,
                 "rule": "frac = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x 2.4 GHz x "
                         "kernel_avg_us); achieved = SQ_INSTS_VALU x 64 lanes / kernel_avg_us",
                 "hbm": hbm}
+        if weighted:
+            wd, wpath = weighted
+            wc = wd["weighted_cycles"] * parts
+            roof["weighted"] = {
+                "frac": round(wc / (SIMDS * CLOCK_GHZ * 1e9 * launch_s), 4),
+                "cycles_per_launch": wc, "mean_cycles_per_valu": wd["mean_cycles_per_valu"],
+                "file": wpath,
+                "what": "each VALU instruction class priced at the measured issue cost of the "
+                        "kernel's own forms (tools/valu_weighted.py): the SIMD cycles the VALU "
+                        "work holds, against 1024 SIMDs x 2.4 GHz"}
     if extra:
         roof.update(extra)
     return roof
@@ -928,7 +952,9 @@ def main(argv=None):
     pmc, pmc_path = load_pmc(cfg, kernel, fpl, queues) if world == 1 else (None, None)
     pq = pmc.get("queues", 1) if pmc else 1
     ref_bytes = local_px * BYTES_PER_PIXEL_LAUNCH * fpl   # the reference: one dispatch per frame
+    wgt = load_weighted(cfg, kernel, pmc_path) if pmc else (None, None)
     roof = roofline(kernel, launch_s, bytes_launch, pmc, pmc_path, pq, ref_bytes=ref_bytes,
+                    weighted=wgt if wgt[0] else None,
                     extra={"frames_per_launch": fpl, "launches_per_step": launches_per_step,
                            "queues": queues, "submit": info.get("submit"),
                            "kernel_time": kernel_how})
