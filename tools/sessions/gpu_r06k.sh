@@ -14,5 +14,5 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.log
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err \
   || { echo "bench failed"; tail $O/bench_driver.err; exit 1; }
-python tools/summarize_bench.py $O/bench_driver.json | head -4
+python tools/summarize_bench.py $O/bench_driver.json > $O/summary.txt; head -4 $O/summary.txt
 python -c "import json; r=json.load(open('$O/bench_driver.json'))['roofline']; print('weighted', r.get('weighted', {}).get('frac'), 'ref', r['hbm'].get('reference_semantics', {}).get('frac'), 'traffic GB/s', r['hbm'].get('traffic_GBs'))"
