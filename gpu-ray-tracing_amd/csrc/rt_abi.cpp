@@ -953,15 +953,19 @@ uint32_t next_count(uint32_t n, uint32_t spp) {
 // launch: 0) and returns the count every pixel holds after the launch.
 uint32_t fill_hint(rtk::TraceParams& p, uint32_t n_in) {
     const uint32_t spp = p.spp, depth = p.depth;
-    uint32_t hf = std::min<uint32_t>(p.frames, rtk::kHintFrames);
+    const uint32_t af = std::min<uint32_t>(p.frames, rtk::kHintFrames);
+    uint32_t hf = af;
     if (depth > 0) hf = std::min<uint32_t>(hf, rtk::kHintEntries / depth);
     p.hint_frames = hf;
+    p.hint_acc_frames = af;
     uint32_t n = n_in;
     for (uint32_t f = 0; f < p.frames; ++f) {
-        if (f < hf) {
+        if (f < af) {
             p.hint_n[f] = n;
             // RN32(1 / f32(n + 1)) (exact integer for n + 1 <= 2^24, where the kernels use it)
             p.hint_rcp[f] = 1.0f / (float)(n + 1u);
+        }
+        if (f < hf) {
             const uint32_t B = p.seed_b[f];
             for (uint32_t i = 0; i < depth; ++i) {
                 // wgsl:268 with seed + 1 = n + B + 2 (wgsl:353, 358)
@@ -983,6 +987,7 @@ void plan_hint(rt_ctx* ctx, rtk::TraceParams& p, const void* in, const void* out
     const bool known = p.reset_first || lookup_count(ctx, in, p, n_in);
     if (!known) {
         p.hint_frames = 0;
+        p.hint_acc_frames = 0;
         forget_count(ctx, out);
         return;
     }
@@ -1042,6 +1047,7 @@ rt_status prepare(rt_ctx* ctx, const void* in, const void* out, uint32_t w, uint
     p.height = h;
     p.count = count;
     p.normal_rn = ctx->normal_rn ? 1u : 0u;
+    p.roots_fast = ctx->scene_bound <= 0x1p40 ? 1u : 0u;
     p.band_first = bs.first;
     p.band_step = bs.step;
     p.local_bands = bs.count;
@@ -1626,6 +1632,7 @@ rt_status update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t w,
             for (uint32_t f = 0; f + 1u < nf; ++f) n_prev = next_count(n_prev, p.spp);
         } else {
             p.hint_frames = 0;
+            p.hint_acc_frames = 0;
         }
         // Frame groups (several waves per tile, alternate frames) whenever every frame of
         // the launch is hinted: faster at every rank count measured.

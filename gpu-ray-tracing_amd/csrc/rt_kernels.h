@@ -122,6 +122,12 @@ struct TraceParams {
     // the scene (rt_rcp_check_kernel at upload: exhaustive over the numerators' significands)
     uint32_t normal_rn;
     uint32_t hint_frames;  // 0 = no hint
+    // hint_n / hint_rcp hold frames [0, hint_acc_frames) (hint_frames <= hint_acc_frames:
+    // hint_rs has room for fewer frames at depth > 1); 0 = no hint
+    uint32_t hint_acc_frames;
+    // The scene's |C| + |R| stay within 2^40 (rt_abi.cpp scene_bound): with roots_fast_wave's
+    // per-wave check of the rays, the root test's sqrt and divisions may run on the fast cores
+    uint32_t roots_fast;
     uint32_t hint_n[kHintFrames];
     // RN32(1 / f32(hint_n[f] + 1)): the accumulator's division by f32(n + 1) as a Markstein
     // division (rtd::div_rn; exact for integer n + 1 < 2^22, rt_kernels.hip kAccRnMax)

@@ -479,6 +479,36 @@ __device__ __forceinline__ void consider_any(float disc, float h, float a, uint3
         }
     }
 }
+// consider_any with consider_fast's arithmetic (sqrt_core of D + 2^-126, div_core with the
+// shared reciprocal ya of a): the IEEE roots wherever they decide anything, on consider_fast's
+// domain (a in [2^-11, 2^20], |h| and sqrt(D) <= 2^53), which roots_fast_wave checks per wave.
+__device__ __forceinline__ void consider_any_fast(float disc, float h, float a, float ya,
+                                                  uint32_t i, float& tmax, int& idx) {
+    if (!(disc < 0.0f)) {                                               // wgsl:189
+        const float q = sqrt_core(disc + 0x1p-126f);
+        float root = div_core(h - q, a, ya);
+        if (root <= 0x1.0624dep-10f) {                                  // wgsl:196
+            root = div_core(h + q, a, ya);
+            if (root <= 0x1.0624dep-10f) return;                        // wgsl:198
+        }
+        if (root < tmax || (root == tmax && (int)i < idx)) {
+            tmax = root;
+            idx = (int)i;
+        }
+    }
+}
+// Whether every live ray of the wave is in consider_fast's domain against every sphere of a
+// scene with |C| + |R| <= 2^40 (scene_ok: TraceParams::roots_fast): a = |d|^2 in
+// [2^-11, 2^20] and |o|'s components below 2^39.  Then |oc| <= |C| + |o| < 2^41,
+// |h| <= |d| |oc| < 2^51 and, with c = |oc|^2 - R^2 >= -R^2, sqrt(D) <= sqrt(h^2 + a R^2)
+// < 2^52.  NaN or infinite a / o fail the test.  (Bounce rays and the bounce instance's camera
+// rays: the camera-ray-only instances have the host's camera_rays_bounded instead.)
+__device__ __forceinline__ bool roots_fast_wave(uint32_t scene_ok, v3 o, float a, bool live) {
+    const uint32_t om = max(max(abs_bits(o.x), abs_bits(o.y)), abs_bits(o.z));
+    const bool ok = __float_as_uint(a) - 0x3A000000u <= 0x49800000u - 0x3A000000u &&  // a
+                    om < 0x53000000u;                                               // 2^39
+    return scene_ok != 0u && rt_ballot(live && !ok) == 0ull;
+}
 // The grid's launch parameters (TraceParams grid_*), as one value: built from the kernel
 // argument, or (rt_bounce_kernel) re-read from the kernarg segment at every use so that they
 // do not stay live in SGPRs across the frame loop.
@@ -490,10 +520,12 @@ struct GridP {
     const float4* sgeom;     // TraceParams::geom (the big spheres' records)
     uint32_t nx, nz, nbig;
     float x0, z0, s, inv_s, ylo, yhi, cx, cy, cz, reach, m, e;
+    uint32_t roots_fast;     // TraceParams::roots_fast
 };
 template <typename P>
 __device__ __forceinline__ GridP grid_params(const P& p) {
     GridP g;
+    g.roots_fast = p.roots_fast;
     g.cells = p.grid_cells;
     g.geom = p.grid_geom;
     g.items = p.grid_items;
@@ -516,24 +548,44 @@ __device__ __forceinline__ GridP grid_params(const P& p) {
     g.e = p.grid_e;
     return g;
 }
-__device__ __forceinline__ Hit scan_grid(const GridP& p, v3 o, v3 d, bool live) {
+// kFast: the roots by consider_any_fast (the wave passed roots_fast_wave; same bits).
+// The walk's own t values (slab and box entry / exit, cell-boundary crossings and their
+// steps) are products with refined reciprocals of d's components (rcp_refined: one Newton
+// step from v_rcp_f32) rather than IEEE quotients: they only steer the traversal, whose cells
+// are padded by e (build_grid).  Each such product is within 1 ulp (<= 2 eps, eps = 2^-24) of
+// its exact value instead of half an ulp, so a crossing after k steps is off by at most
+// (4 + 6k) eps x the coordinate magnitudes (the start and the k additions of the step,
+// each step's own error included), inside e's (k + 16) x 8 eps.  A zero component keeps its
+// branch; a subnormal one gives an infinite or huge reciprocal, i.e. an axis the ray does not
+// cross (it moves less than 2^-60 along it inside the box), or a NaN t that fminf / fmaxf /
+// the compares skip the same way.
+template <bool kFast>
+__device__ __forceinline__ Hit scan_grid_t(const GridP& p, v3 o, v3 d, bool live) {
     const float a = dot(d, d);
+    const float ya = kFast ? rcp_refined(a) : 0.0f;
     float tmax = 0x1.05ed2ep+118f;             // 3.4e35 (wgsl:266)
     int idx = -1;
+    auto test = [&](float disc, float h, uint32_t i) {
+        if (kFast)
+            consider_any_fast(disc, h, a, ya, i, tmax, idx);
+        else
+            consider_any(disc, h, a, i, tmax, idx);
+    };
     // spheres outside the grid (the ground, large ones): every live lane tests them
     for (uint32_t b = 0; b < p.nbig; ++b) {
         const uint32_t i = p.big[b];
         const float4 g = p.sgeom[i];
         float h;
         const float disc = discriminant(g, o, d, a, h);
-        if (live) consider_any(disc, h, a, i, tmax, idx);
+        if (live) test(disc, h, i);
     }
     if (!live) return Hit{idx, tmax};
     // t range of the ray inside the slab and the grid box (t >= 0)
+    const float rx = rcp_refined(d.x), ry = rcp_refined(d.y), rz = rcp_refined(d.z);
     float t0 = 0.0f, t1 = 0x1.05ed2ep+118f;
-    auto clip = [&](float oc, float dc, float lo, float hi) {
+    auto clip = [&](float oc, float dc, float rc, float lo, float hi) {
         if (dc != 0.0f) {
-            const float ta = (lo - oc) / dc, tb = (hi - oc) / dc;
+            const float ta = (lo - oc) * rc, tb = (hi - oc) * rc;
             t0 = fmaxf(t0, fminf(ta, tb));
             t1 = fminf(t1, fmaxf(ta, tb));
         } else if (oc < lo || oc > hi) {
@@ -542,9 +594,9 @@ __device__ __forceinline__ Hit scan_grid(const GridP& p, v3 o, v3 d, bool live) 
     };
     const float xhi = p.x0 + p.s * (float)p.nx;
     const float zhi = p.z0 + p.s * (float)p.nz;
-    clip(o.y, d.y, p.ylo, p.yhi);
-    clip(o.x, d.x, p.x0, xhi);
-    clip(o.z, d.z, p.z0, zhi);
+    clip(o.y, d.y, ry, p.ylo, p.yhi);
+    clip(o.x, d.x, rx, p.x0, xhi);
+    clip(o.z, d.z, rz, p.z0, zhi);
     if (!(t0 <= t1)) return Hit{idx, tmax};
     // 2-D DDA over the cells from P(t0) to P(t1)
     const int nx = (int)p.nx, nz = (int)p.nz;
@@ -554,19 +606,17 @@ __device__ __forceinline__ Hit scan_grid(const GridP& p, v3 o, v3 d, bool live) 
     iz = min(max(iz, 0), nz - 1);
     const int sx = d.x > 0.0f ? 1 : -1, sz = d.z > 0.0f ? 1 : -1;
     const float inf = 0x1.05ed2ep+118f;
-    float tx = d.x != 0.0f
-                   ? (p.x0 + p.s * (float)(ix + (sx > 0)) - o.x) / d.x : inf;
-    float tz = d.z != 0.0f
-                   ? (p.z0 + p.s * (float)(iz + (sz > 0)) - o.z) / d.z : inf;
-    const float dtx = d.x != 0.0f ? p.s / fabsf(d.x) : inf;
-    const float dtz = d.z != 0.0f ? p.s / fabsf(d.z) : inf;
+    float tx = d.x != 0.0f ? (p.x0 + p.s * (float)(ix + (sx > 0)) - o.x) * rx : inf;
+    float tz = d.z != 0.0f ? (p.z0 + p.s * (float)(iz + (sz > 0)) - o.z) * rz : inf;
+    const float dtx = d.x != 0.0f ? p.s * fabsf(rx) : inf;
+    const float dtz = d.z != 0.0f ? p.s * fabsf(rz) : inf;
     const float slack = 2.0f * p.e * rsqrtf(a) * 1.01f;
     for (int step = 0; step < nx + nz + 2; ++step) {
         const uint2 range = p.cells[iz * nx + ix];
         for (uint32_t k = range.x; k < range.y; ++k) {
             float h;
             const float disc = discriminant(p.geom[k], o, d, a, h);
-            consider_any(disc, h, a, p.items[k], tmax, idx);
+            test(disc, h, p.items[k]);
         }
         // A cell entered beyond t1, or beyond the closest hit so far, holds no better hit;
         // slack: the walk's position error (grid_e, as t) and 1e-4 of t.
@@ -583,6 +633,10 @@ __device__ __forceinline__ Hit scan_grid(const GridP& p, v3 o, v3 d, bool live) 
         }
     }
     return Hit{idx, tmax};
+}
+__device__ __forceinline__ Hit scan_grid(const GridP& p, v3 o, v3 d, bool live) {
+    if (roots_fast_wave(p.roots_fast, o, dot(d, d), live)) return scan_grid_t<true>(p, o, d, live);
+    return scan_grid_t<false>(p, o, d, live);
 }
 
 // The wave may walk the grid: every live ray finite and within reach of the grid margin.
@@ -2120,14 +2174,28 @@ struct Scatter {
     v3 hp, nd, att;
     bool ok;   // false: the metal scatter absorbed the path
 };
+// The divisions and square roots run on the exact fast cores where a wave-wide check of
+// their operands allows (the camera-ray instances' checks, same bits): the normal's
+// (p - C) / R by normal_div when every hit lane has |R| in [2^-20, 2^20] and its three
+// numerators in [2^-100, 2^60] (div_core's domain; normal_rn: the scene's radii passed the
+// one-step check), the metal / dielectric normalisations by normalize_w<true>.
 __device__ __forceinline__ Scatter scatter_path(float4 pr, float4 mat, float t, v3 o, v3 d,
-                                                uint32_t sb) {
+                                                uint32_t sb, bool normal_rn) {
     // (results returned by value: out-parameters through references stayed in scratch)
     const float r_sb = rf(sb);
     const v3 ruv = random_unit_vector(r_sb, sb);
     const v3 hp = fmas(t, d, o);
     v3 nd, att;
-    const v3 outward = divs(sub(hp, mk(pr.x, pr.y, pr.z)), pr.w);          // wgsl:209
+    const v3 rel = sub(hp, mk(pr.x, pr.y, pr.z));
+    const uint32_t rel_lo = min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z));
+    const uint32_t rel_hi = max(max(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z));
+    const bool nfast = rel_lo >= kBits2m100 && rel_hi <= 0x5D800000u &&            // 2^60
+                       abs_bits(pr.w) - kBits2m20 <= 0x49800000u - kBits2m20;      // 2^20
+    v3 outward;                                                                    // wgsl:209
+    if (rt_ballot(!nfast) == 0ull)
+        outward = normal_div(rel, pr.w, rcp_refined(pr.w), normal_rn);
+    else
+        outward = divs(rel, pr.w);
     const bool front = dot(d, outward) < 0.0f;
     // (component selects: a select of whole v3 values made the compiler keep them in
     // scratch memory)
@@ -2137,19 +2205,19 @@ __device__ __forceinline__ Scatter scatter_path(float4 pr, float4 mat, float t, 
         nd = sel3(dot(dir, dir) < 0x1.0c6f7ap-20f, n, dir);
         att = mk(mat.x, mat.y, mat.z);
     } else if (mat.w <= 1.0f) {                               // metal wgsl:95-100
-        const v3 refl = fmas(mat.w, ruv, normalize(reflect(d, n)));
+        const v3 refl = fmas(mat.w, ruv, normalize_w<true>(reflect(d, n)));
         if (!(dot(refl, n) > 0.0f)) return Scatter{hp, d, d, false};   // wgsl:277-279
-        nd = normalize(refl);
+        nd = normalize_w<true>(refl);
         att = mk(mat.x, mat.y, mat.z);
     } else {                                                  // dielectric wgsl:102-135
         att = mk(1.0f, 1.0f, 1.0f);
         const float ratio = front ? 1.0f / mat.x : mat.x;
-        const v3 u = normalize(d);
+        const v3 u = normalize_w<true>(d);
         const float cos_t = fminf(dot(neg(u), n), 1.0f);
         const float sin_t = sqrtf(fmaf(-cos_t, cos_t, 1.0f));
         const bool cannot = ratio * sin_t > 1.0f;
         const bool refl = cannot || reflectance(cos_t, ratio) > r_sb;
-        nd = normalize(sel3(refl, reflect(u, n), refract(u, n, ratio)));
+        nd = normalize_w<true>(sel3(refl, reflect(u, n), refract(u, n, ratio)));
     }
     return Scatter{hp, nd, att, true};
 }
@@ -2358,10 +2426,20 @@ rt_bounce_kernel(const TraceParams p) {
             if (rt_ballot(live) != 0ull) {
                 const bool listed = i == 0u && ncand != kCandNone;
                 const GridP gp = grid_params(*karg_bounce_params());
-                hit = listed ? scan_exhaustive<RT_SCAN_CHUNK, false, true>(blk + kCandRecOff,
-                                                                          ncand, o, d)
-                      : p.lds_records ? scan_culled<true>(gp, p.geom, p.count, o, d, live, i > 0)
-                                      : scan_culled<false>(gp, p.geom, p.count, o, d, live, i > 0);
+                if (listed) {
+                    // the tile's camera rays: consider_fast's roots where the wave is in
+                    // their domain (roots_fast_wave), the IEEE ones otherwise
+                    if (roots_fast_wave(p.roots_fast, o, dot(d, d), live))
+                        hit = scan_exhaustive<RT_SCAN_CHUNK, true, true>(blk + kCandRecOff,
+                                                                         ncand, o, d);
+                    else
+                        hit = scan_exhaustive<RT_SCAN_CHUNK, false, true>(blk + kCandRecOff,
+                                                                          ncand, o, d);
+                } else {
+                    hit = p.lds_records
+                              ? scan_culled<true>(gp, p.geom, p.count, o, d, live, i > 0)
+                              : scan_culled<false>(gp, p.geom, p.count, o, d, live, i > 0);
+                }
                 if (listed) hs = blk + kCandSphOff;
             }
             bool done = false, keep = false;
@@ -2369,11 +2447,11 @@ rt_bounce_kernel(const TraceParams p) {
             if (live) {
                 if (hit.idx < 0) {                                // wgsl:288-290: sky
                     done = true;
-                    col = sky(cf, d);
+                    col = sky_w(cf, d);
                 } else {
                     const float4 pr = hs[2 * hit.idx], mat = hs[2 * hit.idx + 1];
                     const uint32_t sb = hash(pseed + i * 1000u);  // wgsl:268
-                    const Scatter sc = scatter_path(pr, mat, hit.t, o, d, sb);
+                    const Scatter sc = scatter_path(pr, mat, hit.t, o, d, sb, p.normal_rn != 0u);
                     const v3 hp = sc.hp, nd = sc.nd, att = sc.att;
                     if (!sc.ok) {
                         done = true;                              // absorbed: black
@@ -2383,7 +2461,7 @@ rt_bounce_kernel(const TraceParams p) {
                         d = nd;
                         if (i + 1u == depth) {                    // depth exhausted: sky
                             done = true;
-                            col = sky(cf, d);
+                            col = sky_w(cf, d);
                         } else {
                             keep = true;
                         }
@@ -2453,10 +2531,17 @@ rt_bounce_kernel(const TraceParams p) {
                     const float4 r = s_pair_col[lane];
                     col = mk(r.x, r.y, r.z);
                 }
-                if (valid && n < spp) {                           // wgsl:352, 356-357
+                // wgsl:352, 356-357; num / f32(n + 1) as the Markstein step from the host's
+                // RN32(1 / f32(n + 1)) (acc_rn) when every accumulating pixel of the wave holds
+                // the hinted count (a reset launch's pixels all do), else the IEEE division
+                const bool acc = valid && n < spp;
+                const v3 num = sub(col, c);
+                if (fj < p.hint_acc_frames && p.hint_n[fj] < kAccRnMax &&
+                    rt_ballot(acc && (n != p.hint_n[fj] || !acc_ok(num))) == 0ull) {
+                    if (acc) c = acc_rn(c, num, (float)(n + 1u), p.hint_rcp[fj]);
+                } else if (acc) {
                     const float k = (float)(n + 1u);
-                    c = mk(c.x + (col.x - c.x) / k, c.y + (col.y - c.y) / k,
-                           c.z + (col.z - c.z) / k);
+                    c = mk(c.x + num.x / k, c.y + num.y / k, c.z + num.z / k);
                 }
                 // the images of the launch's last two frames survive (wgsl:362-363): frame
                 // fj's image belongs to out for even fj, out2 (the input buffer) for odd fj

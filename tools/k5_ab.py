@@ -1,79 +1,84 @@
-"""Interleaved A/B of bounce path schedules on K5 rank shares (diagnostic): for each world
-size, rank 0's share of the 3840x2160 depth-8 64-spp render, one 64-frame launch per
-measurement, the modes alternating launch by launch (so clock and power drift hits every
-mode alike); reports each mode's median and min us per step.
-usage: python tools/k5_ab.py [reps] [worlds, e.g. 4,8] [modes, e.g. per_wave,split4,split2f25]
-(split<S>f<P>: S chunks for the costliest P % of the tiles; split<S>a<P>: the unit order
-with alpha = P / 100)"""
+"""Interleaved A/B of library builds on bench.py --config K5's step (diagnostic):
+    python tools/k5_ab.py ROUNDS LIB [LIB ...]        (LIB: a librt_hip.so path, or "tree")
+Each round runs every build in its own process (RT_HIP_LIB), in order.  A process renders
+the K5 fixture's 64-spp step (3840x2160, 500 spheres, depth 8: one 64-frame bounce launch from
+a reset) twice to warm up, then R = 5 more, each timed wall-clock around the call and a
+synchronize, and checks the last image's whole-image digest against tests/golden/k5.npz;
+then the same for rank 0's 8-rank share (round-robin bands, the default path schedule: its
+second step runs the measured split order), checked band by band.  Prints one JSON line per
+(round, build) and the medians."""
 import json
 import os
+import statistics as st
+import subprocess
 import sys
 import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-sys.path[:0] = [str(ROOT / "gpu-ray-tracing_amd"), str(ROOT)]
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
-import gpu_ray_tracing as rt  # noqa: E402
-from gpu_ray_tracing.distributed import StripeRenderer  # noqa: E402
-
-reps = int(sys.argv[1]) if len(sys.argv) > 1 else 7
-worlds = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "4,8").split(",")]
-modes = (sys.argv[3] if len(sys.argv) > 3 else "per_wave,split2,split4").split(",")
-g = dict(np.load(ROOT / "tests" / "golden" / "k5.npz"))
-w, h = int(g["width"]), int(g["height"])
-cam, sc, seeds = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"]), g["seeds"]
-pipe = rt.ComputeShaderPipeline(0)
-pipe.set_spheres(sc)
 
 
-def set_mode(m):
-    # split<S>[f<P> | a<P>]: S chunks for the costliest P % of the tiles of the tile order
-    # (f), or the unit order with alpha = P / 100 (a; default: the library's alpha)
-    os.environ.pop("RT_SPLIT_FRAC", None)
-    os.environ.pop("RT_SPLIT_ALPHA", None)
-    if m.startswith("split"):
-        rest = m[5:]
-        key = "f" if "f" in rest else "a" if "a" in rest else None
-        s, _, f = rest.partition(key) if key else (rest, "", "")
-        os.environ["RT_BOUNCE_SPLIT"] = s or "4"
-        if key:
-            os.environ["RT_SPLIT_FRAC" if key == "f" else "RT_SPLIT_ALPHA"] = str(int(f) / 100)
-        pipe.set_path_compaction("split")
+def one():
+    sys.path[:0] = [str(ROOT / "gpu-ray-tracing_amd"), str(ROOT), str(ROOT / "tests")]
+    import numpy as np
+    import torch
+    import gpu_ray_tracing as rt
+    from conftest import bands_match, canon_sha
+    g = dict(np.load(ROOT / "tests" / "golden" / "k5.npz"))
+    w, h = int(g["width"]), int(g["height"])
+    cam, sc, seeds = rt.SceneCamera(g["camera"]), rt.SphereCollection(g["spheres"]), g["seeds"]
+    out = {}
+    for world in (1, 8):
+        pipe = rt.ComputeShaderPipeline(0)
+        rows = rt.stripe_local_rows(h, 0, world)
+        a, b = pipe.new_image(w, rows), pipe.new_image(w, rows)
+        walls = []
+        newest = 0
+        for k in range(7):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            newest = pipe.update_frames(a, b, w, h, cam, sc, seeds, 0, world)
+            torch.cuda.synchronize()
+            if k >= 2:
+                walls.append((time.perf_counter() - t0) * 1e6)
+        img = (b if newest == 1 else a).cpu().numpy()
+        if world == 1:
+            ok = canon_sha(img) == str(g["sha256"])
+        else:
+            ok = bands_match(img, range(0, h // 8, world), g["band_sha"]) == []
+        out[str(world)] = {"wall_us": round(st.median(walls), 1),
+                           "kernel": pipe.last_launch_info()["kernel_name"], "ok": ok}
+        pipe.close()
+    print(json.dumps(out))
+
+
+def main():
+    rounds, libs = int(sys.argv[1]), sys.argv[2:]
+    res = {l: [] for l in libs}
+    for rd in range(rounds):
+        for l in libs:
+            env = dict(os.environ)
+            if l != "tree":
+                env["RT_HIP_LIB"] = str(Path(l).resolve())
+            p = subprocess.run([sys.executable, __file__, "--one"], env=env, capture_output=True,
+                               text=True, timeout=300)
+            line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+            if p.returncode or not line:
+                print(l, "FAILED", p.stderr[-2000:], flush=True)
+                sys.exit(1)
+            d = json.loads(line[-1])
+            res[l].append(d)
+            print(json.dumps({"round": rd, "lib": Path(l).name, **d}), flush=True)
+    summary = {}
+    for l, ds in res.items():
+        summary[Path(l).name] = {w: round(st.median(d[w]["wall_us"] for d in ds), 1)
+                                 for w in ("1", "8")}
+        summary[Path(l).name]["all_ok"] = all(d[w]["ok"] for d in ds for w in ("1", "8"))
+    print(json.dumps({"summary": summary}), flush=True)
+
+
+if __name__ == "__main__":
+    if "--one" in sys.argv:
+        one()
     else:
-        os.environ.pop("RT_BOUNCE_SPLIT", None)
-        pipe.set_path_compaction(m)
-
-
-# warm: two whole-image steps
-warm = StripeRenderer(pipe, w, h, 0, 1)
-for _ in range(2):
-    warm.frames(cam, sc, seeds)
-torch.cuda.synchronize()
-del warm
-for world in worlds:
-    r = StripeRenderer(pipe, w, h, 0, world)
-    for m in modes:                     # costs recorded, order built, buffers allocated
-        set_mode(m)
-        r.frames(cam, sc, seeds)
-        r.frames(cam, sc, seeds)
-    torch.cuda.synchronize()
-    res = {m: [] for m in modes}
-    for rep in range(reps):
-        for m in modes:
-            set_mode(m)
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            r.frames(cam, sc, seeds)
-            e1.record()
-            torch.cuda.synchronize()
-            res[m].append(e0.elapsed_time(e1) * 1e3)
-    for m in modes:
-        v = sorted(res[m])
-        print(json.dumps({"world": world, "mode": m, "median_us": round(v[len(v) // 2], 1),
-                          "min_us": round(v[0], 1), "us_per_spp_median": round(v[len(v) // 2] / 64, 2),
-                          "kernel": None, "runs": [round(x, 1) for x in res[m]]}), flush=True)
-pipe.close()
+        main()
