@@ -53,6 +53,7 @@ struct rt_ctx {
     // (rt_rcp_check_kernel, exhaustive over the numerators; TraceParams::normal_rn)
     bool normal_rn = false;
     uint32_t* d_flag = nullptr;     // the check's result word, then up to kRcpRadii radii
+    float4* d_hint_rs = nullptr;    // TraceParams::hint_rs_dev (plan_hint_rs)
     // XZ grid of the small spheres for bounce rays (build_grid; TraceParams
     // grid_*): device arrays and the parameters copied into every launch.
     void* d_grid = nullptr;  // cell ranges (uint2), item records (float4), item indices, big list
@@ -767,6 +768,24 @@ constexpr uint64_t kSplit4MaxTiles = RT_SPLIT4_MAX_TILES, kSplit2MaxTiles = RT_S
 #ifndef RT_SPLIT_ALPHA
 #define RT_SPLIT_ALPHA 0.25
 #endif
+// The bounce instance's table of scatter random numbers (TraceParams::hint_rs_dev) for the
+// hinted frames of a launch: the context's buffer, filled on the stream by launch_bounce.
+rt_status plan_hint_rs(rt_ctx* ctx, rtk::TraceParams& p, int kernel) {
+    p.hint_rs_dev = nullptr;
+    p.hint_rs_dev_frames = 0;
+    if (kernel != rtk::kTraceBounce || p.hint_acc_frames == 0 || p.depth == 0 ||
+        p.depth > rtk::kHintRsDepth)
+        return RT_OK;
+    if (!ctx->d_hint_rs) {
+        const hipError_t e = hipMalloc(&ctx->d_hint_rs, sizeof(float4) * rtk::kHintFrames *
+                                                            rtk::kHintRsDepth);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(hint table)");
+    }
+    p.hint_rs_dev = ctx->d_hint_rs;
+    p.hint_rs_dev_frames = p.hint_acc_frames;
+    return RT_OK;
+}
+
 rt_status plan_split(rt_ctx* ctx, rtk::TraceParams& p, int kernel, hipStream_t stream) {
     p.split = 1;
     p.split_tiles = 0;
@@ -1280,6 +1299,7 @@ rt_status trace(rt_ctx* ctx, const float* in, float* out, uint32_t w, uint32_t h
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         if (rt_status s = plan_wg_order(ctx, p, kernel, stream)) return s;
         if (rt_status s = plan_split(ctx, p, kernel, stream)) return s;
+        if (rt_status s = plan_hint_rs(ctx, p, kernel)) return s;
         hipError_t e = rtk::launch_trace(p, kernel, stream);
         if (e != hipSuccess) return hip_fail(e, "rt_trace_kernel launch");
         finish_tile_order(ctx, p);
@@ -1367,6 +1387,7 @@ rt_status rt_destroy(rt_ctx* ctx) {
         (void)hipFree(ctx->d_geom);
         (void)hipFree(ctx->d_sph);
         (void)hipFree(ctx->d_flag);
+        (void)hipFree(ctx->d_hint_rs);
         (void)hipFree(ctx->d_band_src);
         for (hipEvent_t ev : ctx->time_ev)
             if (ev) (void)hipEventDestroy(ev);
@@ -1678,6 +1699,7 @@ rt_status update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t w,
         if (rt_status s = plan_tile_order(ctx, p, kernel, stream)) return s;
         if (rt_status s = plan_wg_order(ctx, p, kernel, stream)) return s;
         if (rt_status s = plan_split(ctx, p, kernel, stream)) return s;
+        if (rt_status s = plan_hint_rs(ctx, p, kernel)) return s;
         CALL_STAMP(4);
         if (aql) {
             // frame f of part k is a packet on the chain's queue k, after part k's frame f - 1

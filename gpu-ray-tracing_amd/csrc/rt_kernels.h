@@ -35,6 +35,9 @@ static_assert(kCandSphOff + 2u * kCandMax <= kCandStride, "sphere records fit");
 #endif
 constexpr uint32_t kHintFrames = RT_HINT_FRAMES;
 constexpr uint32_t kHintEntries = RT_HINT_FRAMES;
+// the bounce instance's device table of scatter random numbers (TraceParams::hint_rs_dev):
+// up to kHintFrames frames of up to kHintRsDepth bounces
+constexpr uint32_t kHintRsDepth = 16;
 
 // Everything the `update` kernel needs, passed by value (kernarg -> SGPRs).
 struct TraceParams {
@@ -128,6 +131,12 @@ struct TraceParams {
     // The scene's |C| + |R| stay within 2^40 (rt_abi.cpp scene_bound): with roots_fast_wave's
     // per-wave check of the rays, the root test's sqrt and divisions may run on the fast cores
     uint32_t roots_fast;
+    // The scatter step's random numbers of the bounce instance (hint_rs for every hinted
+    // frame and bounce: hint_rs holds too few entries at depth > 1): row f * depth + i of a
+    // device table that rt_hint_rs_kernel fills from hint_n and seed_b before the launch, for
+    // frames [0, hint_rs_dev_frames); 0 = none (depth > kHintRsDepth, or no hint)
+    float4* hint_rs_dev;
+    uint32_t hint_rs_dev_frames;
     uint32_t hint_n[kHintFrames];
     // RN32(1 / f32(hint_n[f] + 1)): the accumulator's division by f32(n + 1) as a Markstein
     // division (rtd::div_rn; exact for integer n + 1 < 2^22, rt_kernels.hip kAccRnMax)

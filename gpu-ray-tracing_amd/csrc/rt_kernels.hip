@@ -2178,12 +2178,12 @@ struct Scatter {
 // their operands allows (the camera-ray instances' checks, same bits): the normal's
 // (p - C) / R by normal_div when every hit lane has |R| in [2^-20, 2^20] and its three
 // numerators in [2^-100, 2^60] (div_core's domain; normal_rn: the scene's radii passed the
-// one-step check), the metal / dielectric normalisations by normalize_w<true>.
+// one-step check), the metal / dielectric normalisations by normalize_w<true>.  (The
+// dielectric's 1 / ir, reflectance division and square roots on the cores too measured
+// neutral, K5 21.53 against 21.56 ms, and stay IEEE: profiles/r06/r06p/.)
 __device__ __forceinline__ Scatter scatter_path(float4 pr, float4 mat, float t, v3 o, v3 d,
-                                                uint32_t sb, bool normal_rn) {
+                                                float r_sb, v3 ruv, bool normal_rn) {
     // (results returned by value: out-parameters through references stayed in scratch)
-    const float r_sb = rf(sb);
-    const v3 ruv = random_unit_vector(r_sb, sb);
     const v3 hp = fmas(t, d, o);
     v3 nd, att;
     const v3 rel = sub(hp, mk(pr.x, pr.y, pr.z));
@@ -2406,12 +2406,17 @@ rt_bounce_kernel(const TraceParams p) {
         const uint32_t B = p.seed_b[frame_in ? f : f0];           // wgsl:311, 353
         const bool sampling = valid && frame_in && nf < spp;      // wgsl:352
         const uint32_t seed = 1u + nf + B;                        // wgsl:353
+        // every sampling pixel of the wave at the hinted count of frame f: the scatter's
+        // random numbers (pixel-independent given the count) come from hint_rs_dev
+        // (compaction moves paths between waves: it keeps computing them)
+        const bool uni_rs = !kCompact && f < p.hint_rs_dev_frames &&
+                            rt_ballot(sampling && nf != p.hint_n[f]) == 0ull;
         v3 res = mk(0.0f, 0.0f, 0.0f);                            // this pixel's colour
         if (kCompact) s_bounce.res[me] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         // bounce 0: this wave's own camera rays (wgsl:305-325), its tile's scan
         v3 o, d, cf = mk(1.0f, 1.0f, 1.0f);
         const Cam cam = cam_params(*karg_bounce_params());
-        get_ray<false>(cam, tc.x, tc.y, hxy, seed * 25u + B, o, d);
+        get_ray<kSingleDisk>(cam, tc.x, tc.y, hxy, seed * 25u + B, o, d);
         uint32_t pseed = seed + 1u;                               // ray_color's seed
         bool live = sampling;
         uint32_t owner = me;
@@ -2450,8 +2455,22 @@ rt_bounce_kernel(const TraceParams p) {
                     col = sky_w(cf, d);
                 } else {
                     const float4 pr = hs[2 * hit.idx], mat = hs[2 * hit.idx + 1];
-                    const uint32_t sb = hash(pseed + i * 1000u);  // wgsl:268
-                    const Scatter sc = scatter_path(pr, mat, hit.t, o, d, sb, p.normal_rn != 0u);
+                    // the scatter's random numbers (wgsl:268, 234-243): from the device
+                    // table when every path of the wave is at the hinted count
+                    float r_sb;
+                    v3 ruv;
+                    if (uni_rs) {
+                        const float4 hr =
+                            ((const kconst float4*)p.hint_rs_dev)[f * depth + i];
+                        r_sb = hr.x;
+                        ruv = mk(hr.y, hr.z, hr.w);
+                    } else {
+                        const uint32_t sb = hash(pseed + i * 1000u);
+                        r_sb = rf(sb);
+                        ruv = random_unit_vector(r_sb, sb);
+                    }
+                    const Scatter sc = scatter_path(pr, mat, hit.t, o, d, r_sb, ruv,
+                                                    p.normal_rn != 0u);
                     const v3 hp = sc.hp, nd = sc.nd, att = sc.att;
                     if (!sc.ok) {
                         done = true;                              // absorbed: black
@@ -3296,9 +3315,30 @@ static hipError_t launch_tpair(const TraceParams& p, hipStream_t stream) {
                          grid, dim3(64 * G), 0, stream, &args, sizeof(args));
 }
 
+// TraceParams::hint_rs_dev: row f * depth + i = (rf(sb), random_unit_vector(sb)) with
+// sb = hash(hint_n[f] + seed_b[f] + 2 + 1000 i) (wgsl:268, 353) — the values a pixel at the
+// hinted count computes itself, by the same device functions.
+__global__ __launch_bounds__(256) void rt_hint_rs_kernel(const TraceParams p) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= p.hint_rs_dev_frames * p.depth) return;
+    const uint32_t f = t / p.depth, i = t % p.depth;
+    const uint32_t sb = hash(p.hint_n[f] + p.seed_b[f] + 2u + i * 1000u);
+    const float r_sb = rf(sb);
+    const v3 u = random_unit_vector(r_sb, sb);
+    p.hint_rs_dev[t] = make_float4(r_sb, u.x, u.y, u.z);
+}
+
 // Workgroups of kBounceWaves tiles along a stripe band: grid (column groups, bands).
 static hipError_t launch_bounce(const TraceParams& p, hipStream_t stream) {
     const uint32_t tiles_x = (p.width + 7u) >> 3;
+    if (p.hint_rs_dev && p.hint_rs_dev_frames) {
+        if (p.hint_rs_dev_frames > kHintFrames || p.depth > kHintRsDepth)
+            return hipErrorInvalidValue;
+        const uint32_t n = p.hint_rs_dev_frames * p.depth;
+        rt_hint_rs_kernel<<<dim3((n + 255u) / 256u), dim3(256), 0, stream>>>(p);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     const uint32_t w = p.compact == 1u ? kBounceWaves : 1u;   // tiles per workgroup
     dim3 grid((tiles_x + w - 1u) / w, p.local_bands);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
