@@ -984,6 +984,60 @@ def test_bounce_launches_in_tile_order(rt, oracle, paths, w, h, depth, frames, s
     _check_bounce_launches(rt, oracle, paths, w, h, depth, frames, scene, nranks, 2, images)
 
 
+@pytest.mark.parametrize("variant", ["far_sphere", "huge_ground", "mixed_counts"])
+def test_bounce_fast_core_fallbacks_match_oracle(rt, oracle, variant):
+    """The bounce instance's exact fast cores on the inputs their wave-wide
+    checks send back to the IEEE operations, against the oracle's chained updates:
+    far_sphere — one sphere 2^41 away, so the scene fails TraceParams::roots_fast (IEEE
+    roots, no grid: cone and exhaustive scans); huge_ground — a ground sphere of radius 2^21,
+    outside the normal's [2^-20, 2^20] (its hits take the IEEE (p - C) / R while the small
+    spheres' take the cores); mixed_counts — an image the library believes at count 1 with a
+    sprinkling of pixels rewritten to other counts behind its back: waves holding one of them
+    compute their scatter random numbers per lane and accumulate by the IEEE division, the
+    others read the device table and take the Markstein step."""
+    w, h, depth = 64, 48, 3
+    base = np.array(rt.create_default_spheres(3).spheres, np.float32).reshape(-1, 8)
+    if variant == "far_sphere":
+        far = np.array([[2.0 ** 41, 0.0, 0.0, 1.0, 0.5, 0.5, 0.5, -2.0]], np.float32)
+        base = np.concatenate([base, far])
+    elif variant == "huge_ground":
+        base[0, 1], base[0, 3] = -(2.0 ** 21), 2.0 ** 21
+    sc = rt.SphereCollection(base)
+    seeds = rt.frame_seeds(21, 4)
+    cam = camera(rt, w, h, depth=depth, spp=500, seed=0.375)
+    p = rt.ComputeShaderPipeline(0)
+    try:
+        a, b = p.new_image(w, h), p.new_image(w, h)
+        if variant != "mixed_counts":
+            newest = p.update_frames(a, b, w, h, cam, sc, seeds, 0, 1)
+            assert p.last_launch_info()["kernel_name"].startswith("rt_bounce_kernel")
+            yy, xx = np.mgrid[0:h, 0:w]
+            want, _ = oracle.render_pixels(np.zeros((h * w, 4), np.float32), xx.ravel(),
+                                           yy.ravel(), cam.blob, sc.spheres, seeds)
+            assert_same(host(b if newest == 1 else a), want.reshape(h, w, 4))
+            return
+        # one reset frame: the library records count 1 for b
+        assert p.update_frames(a, b, w, h, cam, sc, seeds[:1], 0, 1) == 1
+        state = host(b).copy()
+        rng = np.random.default_rng(5)
+        pick = rng.random((h, w)) < 0.01          # ~30 pixels in a few waves
+        state[pick, 3] = rng.integers(2, 6, int(pick.sum())).astype(np.float32)
+        state[pick, :3] = rng.random((int(pick.sum()), 3), np.float32)
+        b.copy_(to_dev(state))
+        still = cam.with_fields(camera_has_moved=0.0)
+        newest = p.update_frames(b, a, w, h, still, sc, seeds[1:], 0, 1)
+        ref, prev = state, None
+        for s_ in seeds[1:]:
+            prev = ref
+            ref, _ = oracle.update(ref, still.with_fields(random_seed=float(s_)).blob,
+                                   sc.spheres)
+        got_new, got_prev = (host(a), host(b)) if newest == 1 else (host(b), host(a))
+        assert_same(got_new, ref)
+        assert_same(got_prev, prev)
+    finally:
+        p.close()
+
+
 def test_accumulator_written_outside_the_library(rt, oracle, pipe):
     """Accumulators written behind the library's back (mixed per-pixel counts, NaN,
     fractional and negative counts) after init_image and between fused frames."""
