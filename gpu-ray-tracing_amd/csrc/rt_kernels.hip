@@ -1999,6 +1999,7 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
     const float4* __restrict__ a_cand, const uint32_t* __restrict__ a_hx,
     const float4* __restrict__ a_in, uint32_t a_width, uint32_t a_height, uint32_t a_bands,
     const TraceParams p) {
+    WAVE_TRACE(0);
     constexpr uint32_t S = 2, Gu = (uint32_t)G;
     static_assert(!kSingleLds<S>, "the pair sample reads its records from the candidate blocks");
     const uint32_t lane = threadIdx.x & 63u;
@@ -2138,6 +2139,7 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
     }
     if (p.tile_cost && w == 0u && lane == 0u)
         p.tile_cost[unit] = (uint32_t)__builtin_amdgcn_s_memtime() - p.tile_cost[unit];
+    WAVE_TRACE(1);
 }
 
 // ---- Bounce paths with workgroup-wide compaction (kTraceBounce) -----------------------
