@@ -60,6 +60,27 @@ __device__ __forceinline__ void wave_trace(int end) {
 #define WAVE_TRACE(e) ((void)0)
 #endif
 
+// ---- diagnostic bounce counters (RT_BOUNCE_COUNTS=1 builds only; never in the product) ---
+// BCOUNT(k): the wave's first active lane adds 1 to g_bcount[k] and the active lanes' count
+// to g_bcount[k + 1] — wave-level trips and lane-level work of a code region
+// (tools/bounce_counts.py reads them via rt_diag_bounce_counts).
+#ifndef RT_BOUNCE_COUNTS
+#define RT_BOUNCE_COUNTS 0
+#endif
+#if RT_BOUNCE_COUNTS
+__device__ unsigned long long g_bcount[32];
+__device__ __forceinline__ void bcount(int k) {
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(ex)) {
+        atomicAdd(&g_bcount[k], 1ull);
+        atomicAdd(&g_bcount[k + 1], (unsigned long long)__builtin_popcountll(ex));
+    }
+}
+#define BCOUNT(k) bcount(k)
+#else
+#define BCOUNT(k) ((void)0)
+#endif
+
 // ---- diagnostic phase stamps of the one-frame kernel (RT_SSTAMPS=1 builds only) ------
 // Per wave of rt_single_kernel: s_memtime when each phase's result is available (the asm
 // consumes the value, so the stamp waits for it): 0 entry, 1 workgroup order resolved,
@@ -559,8 +580,10 @@ __device__ __forceinline__ GridP grid_params(const P& p) {
 // branch; a subnormal one gives an infinite or huge reciprocal, i.e. an axis the ray does not
 // cross (it moves less than 2^-60 along it inside the box), or a NaN t that fminf / fmaxf /
 // the compares skip the same way.
+// walk: this lane walks the grid (false: a far ray that misses every small sphere, which only
+// tests the big list; grid_usable).
 template <bool kFast>
-__device__ __forceinline__ Hit scan_grid_t(const GridP& p, v3 o, v3 d, bool live) {
+__device__ __forceinline__ Hit scan_grid_t(const GridP& p, v3 o, v3 d, bool live, bool walk) {
     const float a = dot(d, d);
     const float ya = kFast ? rcp_refined(a) : 0.0f;
     float tmax = 0x1.05ed2ep+118f;             // 3.4e35 (wgsl:266)
@@ -579,7 +602,9 @@ __device__ __forceinline__ Hit scan_grid_t(const GridP& p, v3 o, v3 d, bool live
         const float disc = discriminant(g, o, d, a, h);
         if (live) test(disc, h, i);
     }
-    if (!live) return Hit{idx, tmax};
+    BCOUNT(26);
+    if (!live || !walk) return Hit{idx, tmax};
+    BCOUNT(kFast ? 0 : 14);
     // t range of the ray inside the slab and the grid box (t >= 0)
     const float rx = rcp_refined(d.x), ry = rcp_refined(d.y), rz = rcp_refined(d.z);
     float t0 = 0.0f, t1 = 0x1.05ed2ep+118f;
@@ -612,8 +637,10 @@ __device__ __forceinline__ Hit scan_grid_t(const GridP& p, v3 o, v3 d, bool live
     const float dtz = d.z != 0.0f ? p.s * fabsf(rz) : inf;
     const float slack = 2.0f * p.e * rsqrtf(a) * 1.01f;
     for (int step = 0; step < nx + nz + 2; ++step) {
+        BCOUNT(2);
         const uint2 range = p.cells[iz * nx + ix];
         for (uint32_t k = range.x; k < range.y; ++k) {
+            BCOUNT(4);
             float h;
             const float disc = discriminant(p.geom[k], o, d, a, h);
             test(disc, h, p.items[k]);
@@ -634,20 +661,38 @@ __device__ __forceinline__ Hit scan_grid_t(const GridP& p, v3 o, v3 d, bool live
     }
     return Hit{idx, tmax};
 }
-__device__ __forceinline__ Hit scan_grid(const GridP& p, v3 o, v3 d, bool live) {
-    if (roots_fast_wave(p.roots_fast, o, dot(d, d), live)) return scan_grid_t<true>(p, o, d, live);
-    return scan_grid_t<false>(p, o, d, live);
+__device__ __forceinline__ Hit scan_grid(const GridP& p, v3 o, v3 d, bool live, bool walk) {
+    if (roots_fast_wave(p.roots_fast, o, dot(d, d), live))
+        return scan_grid_t<true>(p, o, d, live, walk);
+    return scan_grid_t<false>(p, o, d, live, walk);
 }
 
 // The wave may walk the grid: every live ray finite and within reach of the grid margin.
-__device__ __forceinline__ bool grid_usable(const GridP& p, v3 o, v3 d, bool live) {
+// A ray farther out (walk false) may still share the wave's walk when it certainly misses
+// every small sphere: it tests the big list only.  The small spheres lie in the ball B(c,
+// reach); sphere i's discriminant is certainly negative where the line passes farther than
+// sqrt(R_i^2 + m_i^2) from C_i, m_i = 2.5e-3 (|o - C_i| + R_i) <= m_far = 2.5e-3 (|o - c| +
+// reach) (the cone test's margin), so a line at least reach + m_far from c misses them all
+// (|C_i - c| + R_i <= reach), and so does a ray whose origin lies past the whole ball (c's
+// projection t < -(reach + m_far): both roots of every small sphere negative).  Evaluated with
+// a 1.01 / 1.001 widening and 1e-5 |o - c| for the f32 rounding of t and of |o - c|^2 - t^2.
+// (K5: 0.038 of every wave-frame fell back to the 500-sphere exhaustive scan for the
+// far ground's bounce rays, profiles/r06/r06v/.)
+__device__ __forceinline__ bool grid_usable(const GridP& p, v3 o, v3 d, bool live, bool& walk) {
     if (p.nx == 0u) return false;
     const v3 oc = mk(o.x - p.cx, o.y - p.cy, o.z - p.cz);
-    const float dist = __builtin_amdgcn_sqrtf(dot(oc, oc));
+    const float vv = dot(oc, oc);
+    const float dist = __builtin_amdgcn_sqrtf(vv);
     const float dd = dot(d, d);
-    const bool ok = finite3(o) && finite3(d) && dd >= 0x1p-20f && dd <= 0x1p20f &&
-                    2.5e-3f * 1.01f * (dist + p.reach) <= p.m;
-    return rt_ballot(live && !ok) == 0ull;
+    const bool fin = finite3(o) && finite3(d) && dd >= 0x1p-20f && dd <= 0x1p20f;
+    walk = 2.5e-3f * 1.01f * (dist + p.reach) <= p.m;
+    bool far_miss = false;
+    if (fin && !walk) {
+        const float t = -dot(oc, d) * __builtin_amdgcn_rsqf(dd);   // c along the unit ray
+        const float thr = (p.reach + 2.5e-3f * 1.01f * (dist + p.reach)) * 1.001f + 1e-5f * dist;
+        far_miss = fmaf(-t, t, vv) > fmaf(1e-5f, vv, thr * thr * 1.0001f) || t < -thr;
+    }
+    return rt_ballot(live && !(fin && (walk || far_miss))) == 0ull;
 }
 
 template <bool kLds>
@@ -657,13 +702,17 @@ __device__ __forceinline__ Hit scan_culled(const GridP& gp, const float4* __rest
     // Bounce rays walk the grid whenever the wave may (measured faster than the cone
     // culling even for coherent specular waves); camera rays of tiles without a candidate
     // list keep the cone, whose rays share a narrow beam.
-    if (bounce && count >= kCullMinSpheres && grid_usable(gp, o, d, live))
-        return scan_grid(gp, o, d, live);
+    bool walk;
+    if (bounce && count >= kCullMinSpheres && grid_usable(gp, o, d, live, walk))
+        return scan_grid(gp, o, d, live, walk);
     (void)bounce;
     (void)gp;
     Cone k;
-    if (count < kCullMinSpheres || !wave_cone(o, d, live, k))
+    if (count < kCullMinSpheres || !wave_cone(o, d, live, k)) {
+        BCOUNT(bounce ? 18 : 20);
         return scan_exhaustive<RT_SCAN_CHUNK>(geom, count, o, d);
+    }
+    BCOUNT(bounce ? 22 : 24);
     const uint32_t lane = threadIdx.x & 63u;
     const float a = dot(d, d);
     float tmax = 0x1.05ed2ep+118f;
@@ -2413,6 +2462,7 @@ rt_bounce_kernel(const TraceParams p) {
         // (compaction moves paths between waves: it keeps computing them)
         const bool uni_rs = !kCompact && f < p.hint_rs_dev_frames &&
                             rt_ballot(sampling && nf != p.hint_n[f]) == 0ull;
+        BCOUNT(uni_rs ? 12 : 16);
         v3 res = mk(0.0f, 0.0f, 0.0f);                            // this pixel's colour
         if (kCompact) s_bounce.res[me] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         // bounce 0: this wave's own camera rays (wgsl:305-325), its tile's scan
@@ -2432,6 +2482,7 @@ rt_bounce_kernel(const TraceParams p) {
             const float4* hs = p.sph;
             if (rt_ballot(live) != 0ull) {
                 const bool listed = i == 0u && ncand != kCandNone;
+                BCOUNT(i == 0u ? 6 : 8);
                 const GridP gp = grid_params(*karg_bounce_params());
                 if (listed) {
                     // the tile's camera rays: consider_fast's roots where the wave is in
@@ -2471,6 +2522,7 @@ rt_bounce_kernel(const TraceParams p) {
                         r_sb = rf(sb);
                         ruv = random_unit_vector(r_sb, sb);
                     }
+                    BCOUNT(10);
                     const Scatter sc = scatter_path(pr, mat, hit.t, o, d, r_sb, ruv,
                                                     p.normal_rn != 0u);
                     const v3 hp = sc.hp, nd = sc.nd, att = sc.att;
@@ -3649,6 +3701,19 @@ extern "C" __attribute__((visibility("default"))) int rt_diag_single_stamps(
 }
 #endif
 
+#if RT_BOUNCE_COUNTS
+// Diagnostic builds: copies the bounce counters (n <= 32) to out and clears them.
+extern "C" __attribute__((visibility("default"))) int rt_diag_bounce_counts(unsigned long long* out,
+                                                                            unsigned n) {
+    if (n > 32) n = 32;
+    static unsigned long long c[32];
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    if (hipMemcpyFromSymbol(c, HIP_SYMBOL(rtk::g_bcount), sizeof(c)) != hipSuccess) return 1;
+    for (unsigned i = 0; i < n; ++i) out[i] = c[i];
+    static const unsigned long long zero[32] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(rtk::g_bcount), zero, sizeof(zero)) == hipSuccess ? 0 : 1;
+}
+#endif
 #if RT_WAVE_TRACE
 // Diagnostic builds: copies (start, end, hw_id, xcc_id) of the first n waves of the last
 // traced launch to out[4 n] and clears them.
