@@ -297,8 +297,14 @@ constexpr uint32_t kGridMinSpheres = 64;
 #ifndef RT_GRID_PAD_ROUND4
 #define RT_GRID_PAD_ROUND4 0
 #endif
+// (K5 per 64-spp step with far rays sharing the walk, tools/k5_ab.py, profiles/r06/r06x/,
+// r06y/: 2 / 2.5 / 3 / 3.5 / 4 reaches 18.75 / 17.82 / 17.83-17.90 / 17.97 / 18.14 ms — a wider
+// reach pads every registration, a narrower one leaves more far lanes that fail the miss test)
 #ifndef RT_GRID_REACHES
-#define RT_GRID_REACHES 4.0
+#define RT_GRID_REACHES 3.0
+#endif
+#ifndef RT_GRID_E_STEPS
+#define RT_GRID_E_STEPS 1
 #endif
 constexpr uint32_t kGridMaxDim = 256;
 
@@ -338,7 +344,9 @@ rt_status build_grid(rt_ctx* ctx, const rt_sphere* sp, uint32_t count, hipStream
     s = std::max({s, (hi[0] - lo[0]) / (kGridMaxDim - 8), (hi[2] - lo[2]) / (kGridMaxDim - 8),
                   2.0 * rmax / 8.0, 1e-6});
     const double L = norm3d(c) + m / 2.5e-3 + 2.0 * reach + 4.0 * s;
-    const double e = (2.0 * kGridMaxDim + 16.0) * 8.0 * 0x1p-24 * L + 1e-3 * s;
+    // e for walks of up to 2 kGridMaxDim steps; re-derived below from the grid's own step
+    // bound nx + nz + 2 (RT_GRID_E_STEPS)
+    double e = (2.0 * kGridMaxDim + 16.0) * 8.0 * 0x1p-24 * L + 1e-3 * s;
     // A ray that may use the grid accepts sphere (C, R) only at a point within
     // sqrt(R^2 + m^2) of C, plus the root's own rounding (< 1e-5 L): the computed
     // discriminant is negative beyond (the bound E <= m^2 of the culled scan).
@@ -352,23 +360,37 @@ rt_status build_grid(rt_ctx* ctx, const rt_sphere* sp, uint32_t count, hipStream
         return std::sqrt(rr * rr + m * m) + e + 1e-5 * L;
 #endif
     };
-    double x0 = INFINITY, x1 = -INFINITY, z0 = INFINITY, z1 = -INFINITY;
-    double ylo = INFINITY, yhi = -INFINITY;
-    for (uint32_t i : small) {
-        const double w = reg_w(radii[i]);
-        x0 = std::min(x0, sp[i].position[0] - w);
-        x1 = std::max(x1, sp[i].position[0] + w);
-        z0 = std::min(z0, sp[i].position[2] - w);
-        z1 = std::max(z1, sp[i].position[2] + w);
-        ylo = std::min(ylo, sp[i].position[1] - w);
-        yhi = std::max(yhi, sp[i].position[1] + w);
-    }
-    x0 = (double)(float)x0 - e;
-    z0 = (double)(float)z0 - e;
+    double x0, x1, z0, z1, ylo, yhi;
+    uint32_t nx = 0, nz = 0;
     s = (double)(float)s;
-    const uint32_t nx = (uint32_t)std::ceil((x1 + e - x0) / s);
-    const uint32_t nz = (uint32_t)std::ceil((z1 + e - z0) / s);
-    if (nx < 1 || nz < 1 || nx > kGridMaxDim || nz > kGridMaxDim) return RT_OK;
+    auto box = [&]() {
+        x0 = INFINITY, x1 = -INFINITY, z0 = INFINITY, z1 = -INFINITY;
+        ylo = INFINITY, yhi = -INFINITY;
+        for (uint32_t i : small) {
+            const double w = reg_w(radii[i]);
+            x0 = std::min(x0, sp[i].position[0] - w);
+            x1 = std::max(x1, sp[i].position[0] + w);
+            z0 = std::min(z0, sp[i].position[2] - w);
+            z1 = std::max(z1, sp[i].position[2] + w);
+            ylo = std::min(ylo, sp[i].position[1] - w);
+            yhi = std::max(yhi, sp[i].position[1] + w);
+        }
+        x0 = (double)(float)x0 - e;
+        z0 = (double)(float)z0 - e;
+        const double fx = std::ceil((x1 + e - x0) / s), fz = std::ceil((z1 + e - z0) / s);
+        nx = fx >= 1.0 && fx <= kGridMaxDim ? (uint32_t)fx : 0u;
+        nz = fz >= 1.0 && fz <= kGridMaxDim ? (uint32_t)fz : 0u;
+    };
+    box();
+    if (nx < 1 || nz < 1) return RT_OK;
+#if RT_GRID_E_STEPS
+    // A walk takes at most nx + nz + 2 steps of this grid; e for that many is smaller, and
+    // the box it gives lies inside this one (nx, nz do not grow), so it still bounds the
+    // walks of the final grid (K5: 0.019 -> 0.003, 12 % fewer registrations).
+    e = ((double)nx + (double)nz + 2.0 + 16.0) * 8.0 * 0x1p-24 * L + 1e-3 * s;
+    box();
+    if (nx < 1 || nz < 1) return RT_OK;
+#endif
     // CSR: count, prefix, fill (small spheres in index order within every cell)
     const uint32_t cells = nx * nz;
     std::vector<uint32_t> start(cells + 1, 0u);

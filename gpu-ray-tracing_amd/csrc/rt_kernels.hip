@@ -485,8 +485,11 @@ extern __shared__ float4 lds_recs[];
 // gridded spheres' slab, and each sphere is registered in every cell within
 // sqrt(R^2 + grid_m^2) + grid_e of its centre (rt_abi.cpp): no sphere that could be accepted
 // is skipped.
+// (items: the grid's item index array — the sphere index items[i] is loaded only for a root
+// that is accepted or ties; null: i is the sphere index)
 __device__ __forceinline__ void consider_any(float disc, float h, float a, uint32_t i,
-                                             float& tmax, int& idx) {
+                                             float& tmax, int& idx,
+                                             const uint32_t* items = nullptr) {
     if (!(disc < 0.0f)) {                                               // wgsl:189
         const float q = sqrtf(disc);
         float root = (h - q) / a;
@@ -494,9 +497,12 @@ __device__ __forceinline__ void consider_any(float disc, float h, float a, uint3
             root = (h + q) / a;
             if (root <= 0x1.0624dep-10f) return;                        // wgsl:198
         }
-        if (root < tmax || (root == tmax && (int)i < idx)) {
-            tmax = root;
-            idx = (int)i;
+        if (root <= tmax) {
+            const int si = (int)(items ? items[i] : i);
+            if (root < tmax || si < idx) {
+                tmax = root;
+                idx = si;
+            }
         }
     }
 }
@@ -504,7 +510,8 @@ __device__ __forceinline__ void consider_any(float disc, float h, float a, uint3
 // shared reciprocal ya of a): the IEEE roots wherever they decide anything, on consider_fast's
 // domain (a in [2^-11, 2^20], |h| and sqrt(D) <= 2^53), which roots_fast_wave checks per wave.
 __device__ __forceinline__ void consider_any_fast(float disc, float h, float a, float ya,
-                                                  uint32_t i, float& tmax, int& idx) {
+                                                  uint32_t i, float& tmax, int& idx,
+                                                  const uint32_t* items = nullptr) {
     if (!(disc < 0.0f)) {                                               // wgsl:189
         const float q = sqrt_core(disc + 0x1p-126f);
         float root = div_core(h - q, a, ya);
@@ -512,9 +519,12 @@ __device__ __forceinline__ void consider_any_fast(float disc, float h, float a, 
             root = div_core(h + q, a, ya);
             if (root <= 0x1.0624dep-10f) return;                        // wgsl:198
         }
-        if (root < tmax || (root == tmax && (int)i < idx)) {
-            tmax = root;
-            idx = (int)i;
+        if (root <= tmax) {
+            const int si = (int)(items ? items[i] : i);
+            if (root < tmax || si < idx) {
+                tmax = root;
+                idx = si;
+            }
         }
     }
 }
@@ -588,11 +598,11 @@ __device__ __forceinline__ Hit scan_grid_t(const GridP& p, v3 o, v3 d, bool live
     const float ya = kFast ? rcp_refined(a) : 0.0f;
     float tmax = 0x1.05ed2ep+118f;             // 3.4e35 (wgsl:266)
     int idx = -1;
-    auto test = [&](float disc, float h, uint32_t i) {
+    auto test = [&](float disc, float h, uint32_t i, const uint32_t* items) {
         if (kFast)
-            consider_any_fast(disc, h, a, ya, i, tmax, idx);
+            consider_any_fast(disc, h, a, ya, i, tmax, idx, items);
         else
-            consider_any(disc, h, a, i, tmax, idx);
+            consider_any(disc, h, a, i, tmax, idx, items);
     };
     // spheres outside the grid (the ground, large ones): every live lane tests them
     for (uint32_t b = 0; b < p.nbig; ++b) {
@@ -600,7 +610,7 @@ __device__ __forceinline__ Hit scan_grid_t(const GridP& p, v3 o, v3 d, bool live
         const float4 g = p.sgeom[i];
         float h;
         const float disc = discriminant(g, o, d, a, h);
-        if (live) test(disc, h, i);
+        if (live) test(disc, h, i, nullptr);
     }
     BCOUNT(26);
     if (!live || !walk) return Hit{idx, tmax};
@@ -643,7 +653,7 @@ __device__ __forceinline__ Hit scan_grid_t(const GridP& p, v3 o, v3 d, bool live
             BCOUNT(4);
             float h;
             const float disc = discriminant(p.geom[k], o, d, a, h);
-            test(disc, h, p.items[k]);
+            test(disc, h, k, p.items);
         }
         // A cell entered beyond t1, or beyond the closest hit so far, holds no better hit;
         // slack: the walk's position error (grid_e, as t) and 1e-4 of t.
