@@ -879,6 +879,17 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
     d = sub(pc, o);
 }
 
+// A zero vector materialised where this is called: the frame loops' colour of a frame that
+// traces nothing.  As a plain constant the compiler hoists its six v_mov ahead of the branch,
+// onto every traced frame (12 per tile-pair frame in rt_tpair_kernel<2>).
+__device__ __forceinline__ v3 zero_v3_here() {
+    float x, y, z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(x));
+    asm volatile("v_mov_b32 %0, 0" : "=v"(y));
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return mk(x, y, z);
+}
+
 // component-wise select of two v3 (a select of whole v3 values can leave them in
 // scratch memory)
 __device__ __forceinline__ v3 sel3(bool c, v3 a, v3 b) {
@@ -1185,12 +1196,13 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
     constexpr uint32_t kFrameGroup = frame_group<kScan>();
     for (uint32_t f = 0; f < p.frames; f += kFrameGroup) {
         const uint32_t fw = f + w;
-        v3 col = mk(0.0f, 0.0f, 0.0f);
-        if (fw < p.frames) {
-            const uint32_t ng = p.hint_n[fw];   // every pixel's count before frame fw
-            if (ng < spp && rt_ballot(tc.valid) != 0ull)           // wgsl:352
-                col = sample<kScan>(p, cam, tile, ncand, tc, hxy, ng, p.seed_b[fw], fw,
-                                    tc.valid, fw < p.hint_frames);
+        const uint32_t ng = fw < p.frames ? p.hint_n[fw] : spp;  // count before frame fw
+        v3 col;
+        if (ng < spp && rt_ballot(tc.valid) != 0ull) {             // wgsl:352
+            col = sample<kScan>(p, cam, tile, ncand, tc, hxy, ng, p.seed_b[fw], fw, tc.valid,
+                                fw < p.hint_frames);
+        } else {
+            col = zero_v3_here();
         }
         // two LDS slots alternating by group: wave 0 reads group g's slot before it reaches
         // the barrier of group g + 1, so one barrier per group suffices
@@ -2122,12 +2134,14 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
         const float4 zero4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         for (uint32_t f = 0; f < p.frames; f += Gu) {
             const uint32_t fw = f + w;
+            // (single_sample writes every lane's colour; zeros only where nothing is traced)
             v3 col[S];
+            const uint32_t ng = fw < p.frames ? p.hint_n[fw] : spp;  // count before frame fw
+            if (ng >= spp) {
 #pragma unroll
-            for (uint32_t s = 0; s < S; ++s) col[s] = mk(0.0f, 0.0f, 0.0f);
-            if (fw < p.frames) {
-                const uint32_t ng = p.hint_n[fw];   // every pixel's count before frame fw
-                if (ng < spp) {                                   // wgsl:352
+                for (uint32_t s = 0; s < S; ++s) col[s] = zero_v3_here();
+            } else {                                              // wgsl:352
+                {
                     FrameView v;
                     v.geom = p.geom;
                     v.sph = p.sph;
