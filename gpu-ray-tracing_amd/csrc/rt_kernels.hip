@@ -2158,7 +2158,20 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
                         seed[s] = 1u + ng + v.seed_b;             // wgsl:353
                         live[s] = tc[s].valid;
                     }
-                    single_sample<S, true>(v, cam, tc, hxy, seed, blk, ncand, live, valid_m, bv,
+                    // the tiles' list pointers re-derived from the tile indices every frame
+                    // (SALU) instead of staying live across the loop: 45 -> 28 SGPRs spilled
+                    // to VGPR lanes, 30 -> 14 v_readlane in the loop; K3 13.60 -> 13.37 us per
+                    // frame (tools/chain_ab.py, profiles/r06/r06ae/)
+                    const float4* blkf[S];
+                    uint32_t ncf[S];
+#pragma unroll
+                    for (uint32_t s = 0; s < S; ++s) {
+                        uint32_t t = tile[s], nc = ncand[s];
+                        asm volatile("" : "+s"(t), "+s"(nc));
+                        blkf[s] = a_cand + (size_t)t * kCandStride;
+                        ncf[s] = nc;
+                    }
+                    single_sample<S, true>(v, cam, tc, hxy, seed, blkf, ncf, live, valid_m, bv,
                                            nullptr, col);
                 }
             }

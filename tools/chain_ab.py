@@ -1,6 +1,7 @@
 """Interleaved A/B of library builds on the K3 frame-chain structure (the main line's):
     python tools/chain_ab.py ROUNDS LIB [LIB ...]        (LIB: a librt_hip.so path, or "tree")
-Each round runs every build in its own process (RT_HIP_LIB), in order; a process warms 50 ms,
+Each round runs every build in its own process (RT_HIP_LIB), the order rotating from round
+to round; a process warms 50 ms,
 then times the driver's region R = 7 times — a reset + 5 frames, then 20 frames in one
 rt_update_frames call, wall-clock around the call and a synchronize — for the whole image
 and rank 0's 8-rank share, reads the kernel time of three more calls from the timing events
@@ -72,10 +73,17 @@ def main():
     rounds, libs = int(sys.argv[1]), sys.argv[2:]
     res = {l: [] for l in libs}
     for rd in range(rounds):
-        for l in libs:
+        # the order rotates every round (a process's place in the round measurably moves its
+        # time by up to ~2 %: profiles/r06/r06ac/chain_ab_same_build.jsonl)
+        k = rd % len(libs)
+        for l in libs[k:] + libs[:k]:
             env = dict(os.environ)
-            if l != "tree":
-                env["RT_HIP_LIB"] = str(Path(l).resolve())
+            # every build through RT_HIP_LIB, the tree's too: an experiment build runs without
+            # the CPython binding of rt_update_frames (ctypes instead), ~0.1 us more per frame
+            # of a 20-frame call — a bias of ~3 % on the 8-rank share against the tree with
+            # the binding (profiles/r06/r06ac/, r06ad/)
+            env["RT_HIP_LIB"] = str(Path(l).resolve() if l != "tree" else
+                                    ROOT / "gpu-ray-tracing_amd" / "build" / "librt_hip.so")
             p = subprocess.run([sys.executable, __file__, "--one"], env=env, capture_output=True,
                                text=True, timeout=300)
             line = [x for x in p.stdout.splitlines() if x.startswith("{")]

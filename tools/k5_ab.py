@@ -1,6 +1,7 @@
 """Interleaved A/B of library builds on bench.py --config K5's step (diagnostic):
     python tools/k5_ab.py ROUNDS LIB [LIB ...]        (LIB: a librt_hip.so path, or "tree")
-Each round runs every build in its own process (RT_HIP_LIB), in order.  A process renders
+Each round runs every build in its own process (RT_HIP_LIB), the order rotating from round
+to round.  A process renders
 the K5 fixture's 64-spp step (3840x2160, 500 spheres, depth 8: one 64-frame bounce launch from
 a reset) twice to warm up, then R = 5 more, each timed wall-clock around the call and a
 synchronize, and checks the last image's whole-image digest against tests/golden/k5.npz;
@@ -56,7 +57,10 @@ def main():
     rounds, libs = int(sys.argv[1]), sys.argv[2:]
     res = {l: [] for l in libs}
     for rd in range(rounds):
-        for l in libs:
+        # the order rotates every round (a process's place in the round measurably moves its
+        # time by up to ~2 %: profiles/r06/r06ac/chain_ab_same_build.jsonl)
+        k = rd % len(libs)
+        for l in libs[k:] + libs[:k]:
             env = dict(os.environ)
             if l != "tree":
                 env["RT_HIP_LIB"] = str(Path(l).resolve())
