@@ -851,7 +851,8 @@ __device__ __forceinline__ void disk_unit(float sa, float ca, float& ux, float& 
 // when every pixel of the wave holds the same sample count).
 template <int kTable>
 __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, uint32_t hxy,
-                                        uint32_t su, v3& o, v3& d) {
+                                        uint32_t su, v3& o, v3& d,
+                                        const v3* c0v = nullptr) {
     const uint32_t seed = hash(hxy ^ su);
     // rf(v) = f32(hash(v)) * 2^-32 is exact (a power-of-two scale of a value >= 1 or 0), so
     // the next rounding is the only one: rf - 0.5 is one fma, 2pi * rf one multiply by
@@ -861,11 +862,12 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
     const float sx = ((float)x + 0.5f) + offx;
     const float sy = ((float)y + 0.5f) + offy;
     const v3 pc = fmas(sy, cam.pdv, fmas(sx, cam.pdu, cam.vul));
-    // the lens centre in VGPRs first (the copies the lens-less path needs anyway), so that
+    // the lens centre in VGPRs (c0v, the copies the lens-less path needs anyway), so that
     // fma(u, ddu, centre) has one scalar operand (gfx950 VALU: one SGPR per instruction)
-    // instead of a second copy per component
-    v3 c0 = cam.center;
-    asm volatile("" : "+v"(c0.x), "+v"(c0.y), "+v"(c0.z));
+    // instead of a second copy per component; a caller tracing several pixels per lane
+    // passes one copy for all of them
+    v3 c0 = c0v ? *c0v : cam.center;
+    if (!c0v) asm volatile("" : "+v"(c0.x), "+v"(c0.y), "+v"(c0.z));
     if (cam.defocus_angle > 0.0f) {                     // defocus_disk_sample wgsl:327-331
         const float ang = (float)hash(seed + 1u) * 0x1.921fb4p-30f;  // 2*3.1415926 * rf
         float sa, ca, ux, uy;
@@ -1602,10 +1604,13 @@ __device__ __forceinline__ void single_sample(const P& p, const Cam& cam,
                                               v3 (&col)[S]) {
     constexpr int K = 1;    // records per tile and step of the joint list walk
     v3 o[S], d[S];
+    // one VGPR copy of the lens centre for the S pixels (get_ray's c0v)
+    v3 c0 = cam.center;
+    if (S > 1) asm volatile("" : "+v"(c0.x), "+v"(c0.y), "+v"(c0.z));
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {                            // wgsl:311, 305-325
         get_ray<kSingleDisk>(cam, tc[s].x, tc[s].y, hxy[s], seed[s] * 25u + p.seed_b, o[s],
-                             d[s]);
+                             d[s], S > 1 ? &c0 : nullptr);
     }
     SST_V(3, d[S - 1].x);
     const uint32_t lane = threadIdx.x & 63u;
@@ -2161,7 +2166,8 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
                     // the tiles' list pointers re-derived from the tile indices every frame
                     // (SALU) instead of staying live across the loop: 45 -> 28 SGPRs spilled
                     // to VGPR lanes, 30 -> 14 v_readlane in the loop; K3 13.60 -> 13.37 us per
-                    // frame (tools/chain_ab.py, profiles/r06/r06ae/)
+                    // frame (tools/chain_ab.py, profiles/r06/r06ae/); re-reading the unit and
+                    // the counts through the scalar cache every frame instead: 14.17 (r06af/)
                     const float4* blkf[S];
                     uint32_t ncf[S];
 #pragma unroll
