@@ -102,3 +102,17 @@ def test_roofline_object(bench):
     assert abs(r["frac"] - 1e8 * 2 / (1024 * 2.4e9 * 100e-6)) < 1e-4
     assert r["hbm"]["frac"] == 0.5 and r["hbm"]["traffic_GBs"] == 2000.0
     assert r["hbm"]["reference_semantics"]["frac"] == 1.0
+
+
+def test_committed_pmc_and_weighted_model_match(bench):
+    """The committed PMC summaries are found for the kernel instances the bench lines time
+    (K3: rt_tpair_kernel<2>, one 20-frame launch; K5: rt_bounce_kernel<0>, 64 frames), and the
+    weighted VALU model is found for the K3 summary and priced its instruction count — so the
+    driver's line carries roofline.valu from them and roofline.weighted."""
+    pmc3, p3 = bench.load_pmc("K3", "rt_tpair_kernel<2>", 20)
+    assert pmc3 is not None and p3 == "profiles/pmc_r06_K3.json"
+    w, wp = bench.load_weighted("K3", "rt_tpair_kernel<2>", p3)
+    assert w is not None and wp == "profiles/valu_weighted_r06_K3.json"
+    assert w["valu_insts_per_launch"] == pmc3["median_per_launch"]["SQ_INSTS_VALU"]
+    pmc5, p5 = bench.load_pmc("K5", "rt_bounce_kernel<0>", 64)
+    assert pmc5 is not None and p5 == "profiles/pmc_r06_K5.json"
