@@ -306,6 +306,9 @@ constexpr uint32_t kGridMinSpheres = 64;
 #ifndef RT_GRID_E_STEPS
 #define RT_GRID_E_STEPS 1
 #endif
+#ifndef RT_GRID_DISK
+#define RT_GRID_DISK 1
+#endif
 constexpr uint32_t kGridMaxDim = 256;
 
 rt_status build_grid(rt_ctx* ctx, const rt_sphere* sp, uint32_t count, hipStream_t stream) {
@@ -405,11 +408,29 @@ rt_status build_grid(rt_ctx* ctx, const rt_sphere* sp, uint32_t count, hipStream
         az = cell(sp[i].position[2] - w, z0, nz);
         bz = cell(sp[i].position[2] + w, z0, nz);
     };
+    // Of the square of cells, only those that meet the disk of radius w around the centre
+    // (in XZ) can hold a point where the sphere is accepted, so only they list it (a walk
+    // that passes such a point passes through the cell that contains it).  Widened by 1e-6
+    // of a cell for the float rounding of the cell origin the kernel uses (RT_GRID_DISK).
+    auto touches = [&](uint32_t i, uint32_t x, uint32_t z) {
+#if RT_GRID_DISK
+        const double w = reg_w(radii[i]) + 1e-6 * s;
+        const double cx = sp[i].position[0], cz = sp[i].position[2];
+        const double lx = x0 + s * x, hx = lx + s, lz = z0 + s * z, hz = lz + s;
+        const double dx = std::max({lx - cx, cx - hx, 0.0});
+        const double dz = std::max({lz - cz, cz - hz, 0.0});
+        return dx * dx + dz * dz <= w * w;
+#else
+        (void)i, (void)x, (void)z;
+        return true;
+#endif
+    };
     for (uint32_t i : small) {
         uint32_t ax, bx, az, bz;
         span(i, ax, bx, az, bz);
         for (uint32_t z = az; z <= bz; ++z)
-            for (uint32_t x = ax; x <= bx; ++x) start[z * nx + x + 1]++;
+            for (uint32_t x = ax; x <= bx; ++x)
+                if (touches(i, x, z)) start[z * nx + x + 1]++;
     }
     for (uint32_t k = 0; k < cells; ++k) start[k + 1] += start[k];
     const uint32_t items = start[cells];
@@ -430,6 +451,7 @@ rt_status build_grid(rt_ctx* ctx, const rt_sphere* sp, uint32_t count, hipStream
                                        sp[i].radius * sp[i].radius);   // as upload_spheres
         for (uint32_t z = az; z <= bz; ++z)
             for (uint32_t x = ax; x <= bx; ++x) {
+                if (!touches(i, x, z)) continue;
                 const uint32_t k = fill[z * nx + x]++;
                 gg[k] = rec;
                 gi[k] = i;
