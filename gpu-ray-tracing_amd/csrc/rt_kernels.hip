@@ -254,6 +254,10 @@ __device__ __forceinline__ int max_bits(const float (&dd)[K]) {
 #ifndef RT_LIST_CHUNK
 #define RT_LIST_CHUNK 2
 #endif
+// the bounce instance's camera rays over their tile's list (K5: 2.1 entries per tile)
+#ifndef RT_BOUNCE_LIST_CHUNK
+#define RT_BOUNCE_LIST_CHUNK 2
+#endif
 template <int kScan>
 constexpr int scan_chunk() { return is_list_kernel(kScan) ? RT_LIST_CHUNK : RT_SCAN_CHUNK; }
 // Per-frame stores of fused launches (TraceParams::store_each) in rt_trace_kernel exist in
@@ -2531,10 +2535,10 @@ rt_bounce_kernel(const TraceParams p) {
                     // the tile's camera rays: consider_fast's roots where the wave is in
                     // their domain (roots_fast_wave), the IEEE ones otherwise
                     if (roots_fast_wave(p.roots_fast, o, dot(d, d), live))
-                        hit = scan_exhaustive<RT_SCAN_CHUNK, true, true>(blk + kCandRecOff,
+                        hit = scan_exhaustive<RT_BOUNCE_LIST_CHUNK, true, true>(blk + kCandRecOff,
                                                                          ncand, o, d);
                     else
-                        hit = scan_exhaustive<RT_SCAN_CHUNK, false, true>(blk + kCandRecOff,
+                        hit = scan_exhaustive<RT_BOUNCE_LIST_CHUNK, false, true>(blk + kCandRecOff,
                                                                           ncand, o, d);
                 } else {
                     hit = p.lds_records
