@@ -1705,17 +1705,18 @@ rt_status update_frames(rt_ctx* ctx, float* image_a, float* image_b, uint32_t w,
         const bool pairable = kernel == rtk::kTraceList && p.store_each && known &&
                               p.hint_frames == nf;
         if (pairable && ctx->frame_pairs != RT_FRAME_PAIRS_OFF) {
-            // AUTO: four waves per tile when the share is small (a few tiles per SIMD), two
-            // per pair of tiles for whole-image-sized launches, else two per tile (DESIGN.md
-            // §5 "Frame groups over tile pairs")
+            // AUTO: four waves per tile when the share is small (a few tiles per SIMD), four
+            // per pair of tiles up to twice that, two per pair above (rt_kernels.h
+            // kQuadMaxTiles / kQuad2MaxTiles; DESIGN.md §5 "Frame groups over tile pairs")
             const int mode = ctx->frame_pairs;
             const uint64_t tiles = (uint64_t)((w + 7u) >> 3) * p.local_bands;
-            const bool quad = mode == RT_FRAME_PAIRS_QUAD || mode == RT_FRAME_PAIRS_QUAD2 ||
-                              (mode == RT_FRAME_PAIRS_AUTO && tiles <= rtk::kQuadMaxTiles);
+            const bool automode = mode == RT_FRAME_PAIRS_AUTO;
             // (the tile-pair instances read the candidate blocks: lists required)
             const bool tpair = p.cand && (mode == RT_FRAME_PAIRS_ON2 || mode == RT_FRAME_PAIRS_QUAD2 ||
-                                          (mode == RT_FRAME_PAIRS_AUTO && !quad &&
-                                           tiles >= rtk::kTpairMinTiles));
+                                          (automode && tiles > rtk::kQuadMaxTiles));
+            const bool quad = mode == RT_FRAME_PAIRS_QUAD || mode == RT_FRAME_PAIRS_QUAD2 ||
+                              (automode && (tiles <= rtk::kQuadMaxTiles ||
+                                            (tpair && tiles <= rtk::kQuad2MaxTiles)));
             kernel = quad ? (tpair ? rtk::kTraceListQuad2 : rtk::kTraceListQuad)
                           : (tpair ? rtk::kTraceListPair2 : rtk::kTraceListPair);
         }

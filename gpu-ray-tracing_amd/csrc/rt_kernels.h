@@ -200,13 +200,16 @@ constexpr bool trace_ordered(int k) {
     return k == kTraceListQuad2 || k == kTraceListPair2 ||
            (is_list_kernel(k) && (is_group_kernel(k) || RT_WG_WAVES == 1));
 }
-// Tiles per launch at or below which frame groups of four are used.
+// AUTO's frame groups by tiles per launch (rank 0's K3 share, 20-frame chains, wall µs per
+// frame, profiles/r06/r06al/, r06an/): up to kQuadMaxTiles four waves per tile
+// (rt_trace_kernel<4>; 8 ranks, 4 080 tiles: 3.08, four per tile pair 3.05, two per tile
+// 3.12); up to kQuad2MaxTiles four waves per pair of tiles (rt_tpair_kernel<4>; 3 ranks,
+// 10 800 tiles: 5.65 against 5.83 / 5.80 two per tile / pair; 4 ranks, 8 160 tiles: 4.61
+// against 4.72 / 5.04); above it two per pair (rt_tpair_kernel<2>; 2 ranks, 16 200 tiles:
+// 7.61 against 7.86 / 8.18; the whole image).  The tile-pair instances need candidate lists;
+// without them the same sizes run one tile per group.
 constexpr uint64_t kQuadMaxTiles = 6144;
-// Tiles per launch from which AUTO's groups of two own a pair of tiles (rt_tpair_kernel<2>:
-// 2 waves per pair, 7 waves per SIMD).  K3 20-frame chains, µs per frame one tile / tile
-// pair: whole image 16.74 / 16.03, 2-rank share 8.62 / 8.61, 4-rank share (8 100 tiles:
-// 8 100 waves for 7 168 wave slots) 4.71 / 5.14 (profiles/r05/r05ag/pairs_chain.jsonl).
-constexpr uint64_t kTpairMinTiles = 24000;
+constexpr uint64_t kQuad2MaxTiles = 12288;
 // The seed-hash tables share one buffer: hash(x*73) for x < hy_offset(width), then
 // hash(y*51) per row (TraceParams::hy == hx + hy_offset(width)).
 constexpr uint32_t hy_offset(uint32_t width) { return (width + 63u) & ~63u; }

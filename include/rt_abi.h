@@ -322,8 +322,8 @@ RT_API rt_status rt_set_frame_images(rt_ctx* ctx, int mode);
  * per tile).  The groups' waves own one tile (ON: 2 waves, QUAD: 4) or a pair of adjacent
  * tiles, each lane tracing one pixel of each (ON2: 2 waves, QUAD2: 4; ABI 6).  AUTO
  * (default): 4 waves per tile for launches of at most 6144 tiles (small per-rank shares),
- * 2 waves per pair of tiles from 24000 tiles (whole images), else 2 waves per tile; OFF:
- * one wave per tile. */
+ * 4 waves per pair of tiles up to 12288 tiles, 2 waves per pair above (whole images) — the
+ * pair forms when candidate lists exist, else 2 waves per tile; OFF: one wave per tile. */
 #define RT_FRAME_PAIRS_AUTO 0
 #define RT_FRAME_PAIRS_OFF 1
 #define RT_FRAME_PAIRS_ON 2

@@ -7,7 +7,9 @@ step (median and quartiles), and, for the last repetition, `timeline_host` stamp
 so that tools/timeline.py can place the call on a rocprofv3 kernel trace of this process:
     rocprofv3 --kernel-trace -f csv -d DIR -- python3 tools/share_region.py 8 0 > line.json
     python tools/timeline.py DIR line.json
-usage: python tools/share_region.py [N] [rank] [R] [frames] [pairs: auto|on|quad|off]"""
+usage: python tools/share_region.py [N] [rank] [R] [frames] [pairs: auto|on|quad|on2|quad2|off]
+(SHARE_CFG=K2: bench.py's K2 scene instead, three spheres)"""
+import os
 import json
 import statistics as st
 import sys
@@ -27,7 +29,9 @@ R = int(sys.argv[3]) if len(sys.argv) > 3 else 15
 F = int(sys.argv[4]) if len(sys.argv) > 4 else 20
 PAIRS = sys.argv[5] if len(sys.argv) > 5 else "auto"
 w, h = 1920, 1080
-sc = rt.SphereCollection.generate(rt.SCENE_N, 500, 1)
+CFG = os.environ.get("SHARE_CFG", "K3")
+sc = (rt.SphereCollection.generate(rt.SCENE_THREE, 3, 1) if CFG == "K2" else
+      rt.SphereCollection.generate(rt.SCENE_N, 500, 1))
 seeds = rt.frame_seeds(0x5EED, 5 + F)
 cam0 = rt.SceneCamera.from_settings(rt.CameraSettings(max_depth=1, samples_per_pixel=65536),
                                     w, h, float(seeds[0]))
@@ -73,7 +77,7 @@ def q(v):
     return [round(s[len(s) // 4], 2), round(st.median(s), 2), round(s[(3 * len(s)) // 4], 2)]
 
 
-print(json.dumps({"share": f"rank {RANK} of {N}", "steps": F, "reps": R, "pairs": PAIRS,
+print(json.dumps({"config": CFG, "share": f"rank {RANK} of {N}", "steps": F, "reps": R, "pairs": PAIRS,
                   "kernel": info["kernel_name"], "launches": info["launches"],
                   "wall_us_per_step_q1_med_q3": q(wall), "events_us_per_step_q1_med_q3": q(ev),
                   "ms_per_step": round(st.median(wall) / 1e3, 5),
