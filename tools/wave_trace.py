@@ -20,6 +20,7 @@ from gpu_ray_tracing.distributed import StripeRenderer  # noqa: E402
 
 import os
 DEBUG = os.environ.get("WT_DEBUG") == "1"
+NF = int(os.environ.get("WT_FRAMES", "64"))      # frames of the traced launch (bench.py's K3: 20)
 CONF = {"K2": (1920, 1080, rt.SCENE_THREE, 3, 1), "K3": (1920, 1080, rt.SCENE_N, 500, 1),
         "K5": (3840, 2160, rt.SCENE_N, 500, 8)}
 
@@ -74,13 +75,15 @@ def main(cfg="K3"):
     L = rt._lib.lib()
     L.rt_diag_wave_trace.argtypes = [ctypes.c_void_p, ctypes.c_uint]
     buf = (ctypes.c_ulonglong * (4 * (1 << 18)))()
-    for world in ((2, 4, 8) if cfg == "K5" else (1, 2, 4, 8)):   # (K5 at 1 rank: > 2^16 WGs)
+    worlds = [int(x) for x in os.environ["WT_WORLDS"].split(",")] if "WT_WORLDS" in os.environ else \
+        ((2, 4, 8) if cfg == "K5" else (1, 2, 4, 8))
+    for world in worlds:   # (K5 at 1 rank: > 2^16 WGs)
         r = StripeRenderer(pipe, w, h, 0, world)
         r.frames(cam, sc, seeds[:5])                       # reset + tile-cost recording
         r.frames(cam.with_fields(camera_has_moved=0.0), sc, seeds[69:133])  # long recording
         torch.cuda.synchronize()
         assert L.rt_diag_wave_trace(buf, 1 << 18) == 0     # (clears the trace)
-        r.frames(cam.with_fields(camera_has_moved=0.0), sc, seeds[5:69])   # one 64-frame launch
+        r.frames(cam.with_fields(camera_has_moved=0.0), sc, seeds[5:5 + NF])  # one NF-frame launch
         torch.cuda.synchronize()
         assert L.rt_diag_wave_trace(buf, 1 << 18) == 0
         raw = bytes(buf)
