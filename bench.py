@@ -803,10 +803,25 @@ def main(argv=None):
     pipe.set_update_submit(args.submit)
     # the job's one gather: RCCL behind the C ABI (rt_comm_create + rt_gather_stripes)
     use_abi = world > 1 and backend == "nccl" and os.environ.get("RT_GATHER", "abi") == "abi"
-    comm = StripeComm.from_process_group(pipe) if use_abi else None
+    comm, comm_error = None, None
+    if use_abi:
+        # the gather runs after the timed region: should librt_hip.so's communicator fail to
+        # come up on every rank (e.g. no loadable librccl), the job gathers through
+        # torch.distributed's RCCL group instead and says so in `gather.how`
+        try:
+            comm = StripeComm.from_process_group(pipe)
+        except Exception as e:              # noqa: BLE001
+            comm_error = f"{type(e).__name__}: {e}"[:200]
+        ok = torch.tensor([0 if comm_error else 1], dtype=torch.int32, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0 and comm is not None:
+            comm.close()
+            comm, comm_error = None, comm_error or "another rank's rt_comm_create failed"
+        use_abi = comm is not None
     gather_how = ("rt_gather_stripes: ncclGather + de-interleave in librt_hip.so" if use_abi
                   else "none (one rank)" if world == 1
-                  else f"torch.distributed.gather over {backend} + rt_deinterleave_stripes")
+                  else f"torch.distributed.gather over {backend} + rt_deinterleave_stripes"
+                  + (f" (rt_comm_create failed: {comm_error})" if comm_error else ""))
     r = StripeRenderer(pipe, w, h, rank, world, comm=comm)
     stream = torch.cuda.current_stream()
     local_px = w * min(r.rows, h)
