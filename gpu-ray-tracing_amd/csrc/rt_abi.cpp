@@ -1027,6 +1027,7 @@ uint32_t fill_hint(rtk::TraceParams& p, uint32_t n_in) {
             p.hint_n[f] = n;
             // RN32(1 / f32(n + 1)) (exact integer for n + 1 <= 2^24, where the kernels use it)
             p.hint_rcp[f] = 1.0f / (float)(n + 1u);
+            p.hint_cnt[f] = (float)(n < spp ? n + 1u : n);
         }
         if (f < hf) {
             const uint32_t B = p.seed_b[f];

@@ -141,6 +141,10 @@ struct TraceParams {
     // RN32(1 / f32(hint_n[f] + 1)): the accumulator's division by f32(n + 1) as a Markstein
     // division (rtd::div_rn; exact for integer n + 1 < 2^22, rt_kernels.hip kAccRnMax)
     float hint_rcp[kHintFrames];
+    // f32 of the count after frame f: f32(hint_n[f] + 1) where the frame accumulates
+    // (hint_n[f] < spp: also the divisor k of wgsl:356), else f32(hint_n[f]) — the image's
+    // alpha (wgsl:362) and k as scalar operands, no per-frame conversion in the kernels
+    float hint_cnt[kHintFrames];
     float4 hint_rs[kHintEntries];
     uint32_t seed_b[kMaxFramesPerLaunch];
 };

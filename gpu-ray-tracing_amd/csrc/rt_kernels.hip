@@ -294,15 +294,17 @@ constexpr uint32_t kBits2m102 = 0x0C800000u;   // 2^-102
 // ulp / (2 k) > 2^-23 ulp, more than the corrected quotient's error |q - num / k| |k y - 1|
 // <= 1.5 ulp 2^-24 (round-5 ADVICE).  Counts of 2^22 or more take the IEEE division.
 constexpr uint32_t kAccRnMax = 1u << 22;
-__device__ __forceinline__ bool acc_ok(v3 num) {
-    // |x| >= 2^-102 or x == +-0 (NaN, inf pass): one unsigned compare per channel
-    return min(min(abs_bits(num.x) - 1u, abs_bits(num.y) - 1u), abs_bits(num.z) - 1u) >=
-           kBits2m102 - 1u;
-}
-// (acc_ok(num) == acc_min_bits(num) >= kBits2m102 - 1)
+// |x| >= 2^-102 or x == +-0 (NaN, inf pass) as one unsigned compare per channel on
+// 2 (abs_bits(x) - 1) mod 2^32 = (bits << 1) - 2: the sign shifted out, one v_lshl_add per
+// channel instead of an and and an add (x = +-0 wraps to 0xFFFFFFFE, above the bound, as
+// abs_bits(x) - 1 wraps to 0xFFFFFFFF; otherwise the doubling is exact, abs_bits < 2^31)
+constexpr uint32_t kAccOkDbl = 2u * (kBits2m102 - 1u);
+__device__ __forceinline__ uint32_t dbl_m2(float x) { return (__float_as_uint(x) << 1) - 2u; }
+// (acc_ok(num) == acc_min_bits(num) >= kAccOkDbl)
 __device__ __forceinline__ uint32_t acc_min_bits(v3 num) {
-    return min(min(abs_bits(num.x) - 1u, abs_bits(num.y) - 1u), abs_bits(num.z) - 1u);
+    return min(min(dbl_m2(num.x), dbl_m2(num.y)), dbl_m2(num.z));
 }
+__device__ __forceinline__ bool acc_ok(v3 num) { return acc_min_bits(num) >= kAccOkDbl; }
 // c + num / k with y = RN32(1 / k)
 __device__ __forceinline__ v3 acc_rn(v3 c, v3 num, float k, float y) {
     return mk(c.x + div_rn(num.x, k, y), c.y + div_rn(num.y, k, y), c.z + div_rn(num.z, k, y));
@@ -880,7 +882,10 @@ __device__ __forceinline__ void get_ray(const Cam& cam, uint32_t x, uint32_t y, 
         disk_unit<kTable>(sa, ca, ux, uy);
         o = fmas(uy, cam.ddv, fmas(ux, cam.ddu, c0));
     } else {
+        // (made here: as a plain copy the compiler hoists it ahead of the branch, three
+        // v_mov per pixel on every lens frame)
         o = c0;
+        asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z));
     }
     d = sub(pc, o);
 }
@@ -1061,6 +1066,8 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
 // Control flow is wave-uniform down to the shading (the culled scan reduces across
 // lanes); per-lane conditions of the reference (n < spp, the image bounds) become the
 // `live` flag instead of branches.
+// a colour's three channels as one vector store (LDS slots of the frame groups)
+typedef float f3v __attribute__((ext_vector_type(3)));
 struct TileCoord {
     uint32_t x, y;
     size_t idx;
@@ -1213,9 +1220,11 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
         // two LDS slots alternating by group: wave 0 reads group g's slot before it reaches
         // the barrier of group g + 1, so one barrier per group suffices
         float4* slot = lds_recs + ((f / kFrameGroup) & 1u) * (kFrameGroup - 1u) * 64u;
-        if (w != 0u) slot[(w - 1u) * 64u + lane] = make_float4(col.x, col.y, col.z, 0.0f);
+        if (w != 0u)
+            *reinterpret_cast<f3v*>(&slot[(w - 1u) * 64u + lane]) = f3v{col.x, col.y, col.z};
         __syncthreads();
         if (w == 0u) {
+            const uint64_t valid_m = rt_ballot(tc.valid);
 #pragma unroll
             for (uint32_t j = 0; j < kFrameGroup; ++j) {
                 const uint32_t fj = f + j;
@@ -1225,22 +1234,24 @@ __device__ __forceinline__ void trace_pair(const TraceParams& p, const Cam& cam,
                     col = mk(cj.x, cj.y, cj.z);
                 }
                 const uint32_t nb = p.hint_n[fj];                 // count before frame fj
-                uint32_t na = nb;
+                // f32(nb + 1) (the divisor k, wgsl:356) or f32(nb): the host's table
+                const float cnt = p.hint_cnt[fj];
                 if (nb < spp) {                                   // wgsl:352-358
                     const v3 num = sub(col, c);
-                    // num / f32(nb + 1) (wgsl:356) as a Markstein division (acc_rn)
-                    if (nb < kAccRnMax &&
-                        rt_ballot(tc.valid && !acc_ok(num)) == 0ull) {
-                        c = acc_rn(c, num, (float)(nb + 1u), p.hint_rcp[fj]);
+                    // num / f32(nb + 1) (wgsl:356) as a Markstein division (acc_rn); both
+                    // conditions scalar (see rt_tpair_kernel)
+                    const bool rn = (nb < kAccRnMax) &
+                                    ((mask_ult(acc_min_bits(num), kAccOkDbl) & valid_m) == 0ull);
+                    if (rn) {
+                        c = acc_rn(c, num, cnt, p.hint_rcp[fj]);
                     } else {
-                        const float k = (float)(nb + 1u);         // wgsl:356
+                        const float k = cnt;                      // wgsl:356
                         c = mk(c.x + num.x / k, c.y + num.y / k, c.z + num.z / k);
                     }
-                    na = nb + 1u;
                 }
                 // wgsl:362-363: the images that survive (or every frame's, store_each 2)
                 if ((p.store_each == 2u || fj + 2u >= p.frames) && tc.valid)
-                    ((fj & 1u) ? p.out2 : p.out)[tc.idx] = make_float4(c.x, c.y, c.z, (float)na);
+                    ((fj & 1u) ? p.out2 : p.out)[tc.idx] = make_float4(c.x, c.y, c.z, cnt);
             }
         }
     }
@@ -1649,6 +1660,8 @@ __device__ __forceinline__ void single_sample(const P& p, const Cam& cam,
             m = max(m, ncand[s]);
         }
         if (joint) {
+            // (walking the common length jointly and the longer list's rest alone measured
+            // neutral: profiles/r06/r06av/)
             for (uint32_t i = 0; i < m; i += K) {
                 float hh[S][K], dd[S][K];
                 // "some discriminant of the step is not negative" as the sign of the AND of
@@ -1915,7 +1928,7 @@ __device__ __forceinline__ void single_body(
             if (ng < spp) {                                       // wgsl:352-357
                 const v3 num = sub(col[s], c[s]);
                 if (ng < kAccRnMax &&
-                    (mask_ult(acc_min_bits(num), kBits2m102 - 1u) & valid_m[s]) == 0ull) {
+                    (mask_ult(acc_min_bits(num), kAccOkDbl) & valid_m[s]) == 0ull) {
                     c[s] = acc_rn(c[s], num, (float)(ng + 1u), p.rcp_hint);
                 } else {
                     const float k = (float)(ng + 1u);             // wgsl:356
@@ -2185,13 +2198,14 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
                                            nullptr, col);
                 }
             }
-            // two LDS slots alternating by group (one barrier per group, as trace_pair)
+            // two LDS slots alternating by group (one barrier per group, as trace_pair); the
+            // colours as 12-B records (ds_write_b96: no register pair to fill with a zero)
             float4* slot = s_cols + ((f / Gu) & 1u) * (Gu - 1u) * S * 64u;
             if (w != 0u)
 #pragma unroll
                 for (uint32_t s = 0; s < S; ++s)
-                    slot[((w - 1u) * S + s) * 64u + lane] =
-                        make_float4(col[s].x, col[s].y, col[s].z, 0.0f);
+                    *reinterpret_cast<f3v*>(&slot[((w - 1u) * S + s) * 64u + lane]) =
+                        f3v{col[s].x, col[s].y, col[s].z};
             __syncthreads();
             if (w == 0u) {
 #pragma unroll
@@ -2200,6 +2214,8 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
                     if (fj >= p.frames) break;
                     const uint32_t nb = p.hint_n[fj];             // count before frame fj
                     const bool acc_frame = nb < spp;              // wgsl:352-358
+                    // f32(nb + 1) (the divisor k, wgsl:356) or f32(nb): the host's table
+                    const float cnt = p.hint_cnt[fj];
                     float4* out = (fj & 1u) ? p.out2 : p.out;
                     const bool store = p.store_each == 2u || fj + 2u >= p.frames;
 #pragma unroll
@@ -2214,20 +2230,24 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
                         if (acc_frame) {
                             const v3 num = sub(cj, cs);
                             // num / f32(nb + 1) (wgsl:356) as a Markstein division (acc_rn)
-                            if (nb < kAccRnMax &&
-                                rt_ballot(tc[s].valid && !acc_ok(num)) == 0ull) {
-                                cs = acc_rn(cs, num, (float)(nb + 1u), p.hint_rcp[fj]);
+                            // (both conditions scalar, combined without a branch: a short-
+                            // circuit && here kept nb's test in a VGPR)
+                            const bool rn = (nb < kAccRnMax) &
+                                            ((mask_ult(acc_min_bits(num), kAccOkDbl) &
+                                              valid_m[s]) == 0ull);
+                            if (rn) {
+                                cs = acc_rn(cs, num, cnt, p.hint_rcp[fj]);
                             } else {
-                                const float k = (float)(nb + 1u);   // wgsl:356
+                                const float k = cnt;                 // wgsl:356
                                 cs = mk(cs.x + num.x / k, cs.y + num.y / k, cs.z + num.z / k);
                             }
                         }
-                        s_acc[s * 64u + lane] = make_float4(cs.x, cs.y, cs.z, 0.0f);
+                        // (the alpha rides in the LDS copy: one register quad serves the LDS
+                        // write and the image store)
+                        const float4 v = make_float4(cs.x, cs.y, cs.z, cnt);
+                        s_acc[s * 64u + lane] = v;
                         // wgsl:362-363: the images that survive (or every frame's)
-                        if (store && tc[s].valid)
-                            out[tc[s].idx] =
-                                make_float4(cs.x, cs.y, cs.z,
-                                            (float)(acc_frame ? nb + 1u : nb));
+                        if (store && tc[s].valid) out[tc[s].idx] = v;
                     }
                 }
             }
