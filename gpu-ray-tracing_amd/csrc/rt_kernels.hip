@@ -950,6 +950,14 @@ __device__ __forceinline__ v3 normal_div(v3 rel, float r, float y, bool rn) {
     return mk(div_core(rel.x, r, y), div_core(rel.y, r, y), div_core(rel.z, r, y));
 }
 
+// One 16-B buffer load at a byte offset (raw buffer, no format conversion)
+__device__ __forceinline__ float4 buf_f4(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                       __uint_as_float(v.w));
+}
+
 template <int kScan>
 __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uint32_t ncand,
                                         uint32_t depth, v3 o, v3 d, uint32_t seed, bool live,
@@ -981,6 +989,8 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
         // depend on the scan; the scatter's random numbers do not depend on the material
         // (lambertian and metal draw random_unit_vector(sb), dielectric draws rf(sb), its
         // first component), so they are computed while the loads are in flight.
+        // (buffer loads here, as in single_sample, measured 1.5 % slower in the 8-rank share
+        // kernel: profiles/r06/r06ax/)
         const float4 pr = hs[2 * hit.idx];          // position, radius
         const float4 mat = hs[2 * hit.idx + 1];     // material color
         float r_sb;
@@ -1727,9 +1737,14 @@ __device__ __forceinline__ void single_sample(const P& p, const Cam& cam,
                     pr[s] = lblk[s * kCandStride + kCandSphOff + 2u * j];
                     mat[s] = lblk[s * kCandStride + kCandSphOff + 2u * j + 1u];
                 } else {
+                    // the wave-uniform record array as a buffer, the lane's 32-bit byte offset
+                    // (j < 2^20 spheres, rt_abi.cpp kMaxSpheres): no 64-bit address arithmetic
+                    // per lane
                     const float4* hs = ncand[s] != kCandNone ? blk[s] + kCandSphOff : p.sph;
-                    pr[s] = hs[2u * j];
-                    mat[s] = hs[2u * j + 1u];
+                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                        (void*)hs, 0, (int)0x7FFFFFFF, 0x00020000);
+                    pr[s] = buf_f4(rs, j * 32u);
+                    mat[s] = buf_f4(rs, j * 32u + 16u);
                 }
             }
 #pragma unroll
@@ -2170,6 +2185,8 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
                     v.count = p.count;
                     v.depth = p.depth;
                     v.seed_b = p.seed_b[fw];
+                    // (read from the kernarg segment every frame: as a loop invariant the
+                    // flag was spilled and turned back into a lane mask per pixel, four VALU)
                     v.normal_rn = p.normal_rn;
                     v.rs = p.hint_rs[fw * p.depth];
                     uint32_t seed[S];
