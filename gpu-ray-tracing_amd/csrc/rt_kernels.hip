@@ -157,6 +157,11 @@ __device__ __forceinline__ uint64_t mask_not_lt(float a, float b) {
 #define kconst
 #endif
 
+// min(|x|, |y|, |z|) (v_min3_f32 with abs modifiers; NaN channels ignored, as IEEE minNum)
+__device__ __forceinline__ float min_abs3(v3 v) {
+    return fminf(fminf(fabsf(v.x), fabsf(v.y)), fabsf(v.z));
+}
+
 struct Hit {
     int idx;     // winning sphere, -1 = miss
     float t;     // its root
@@ -921,8 +926,9 @@ __device__ __forceinline__ v3 normalize_w(v3 v) {
     if (kFast) {
         const float dd = dot(v, v);
         const uint32_t span = __float_as_uint(dd) - kBits2m20;
-        const uint32_t vmin = min(min(abs_bits(v.x), abs_bits(v.y)), abs_bits(v.z));
-        if ((mask_uge(span, kBits2p40 - kBits2m20) | mask_ult(vmin, kBits2m100)) == 0ull) {
+        // (a component below 2^-100: min_abs3 and an ordered compare, as in shade_hit)
+        if ((mask_uge(span, kBits2p40 - kBits2m20) |
+             __builtin_amdgcn_fcmpf(min_abs3(v), 0x1p-100f, 4)) == 0ull) {
             float y;
             const float len = sqrt_core_rcp(dd, y);
             return mk(div_core(v.x, len, y), div_core(v.y, len, y), div_core(v.z, len, y));
@@ -1012,8 +1018,7 @@ __device__ __forceinline__ v3 ray_color(const TraceParams& p, uint32_t tile, uin
         const v3 rel = sub(hp, C);
         v3 outward;
         if (fast_core<kScan>(2) &&
-            rt_ballot(min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z)) <
-                     kBits2m100) == 0ull) {
+            rt_ballot(min_abs3(rel) < 0x1p-100f) == 0ull) {    // (see shade_hit)
             const float y = rcp_refined(pr.w);
             outward = normal_div(rel, pr.w, y, p.normal_rn != 0u);
         } else {
@@ -1544,8 +1549,10 @@ __device__ __forceinline__ void shade_hit(float4 pr, float4 mat, float t, v3 o, 
     const v3 hp = fmas(t, d, o);
     const v3 rel = sub(hp, mk(pr.x, pr.y, pr.z));
     v3 outward;                                                   // wgsl:209
-    const uint32_t rel_min = min(min(abs_bits(rel.x), abs_bits(rel.y)), abs_bits(rel.z));
-    if ((mask_ult(rel_min, kBits2m100) & hm) == 0ull) {
+    // (some |rel| below 2^-100 as one v_min3_f32 on |.| and one ordered compare: the same
+    // lanes as the minimum of the abs bit patterns — a NaN channel is never the small one
+    // either way, and rel, an arithmetic result, is never a signalling NaN)
+    if ((__builtin_amdgcn_fcmpf(min_abs3(rel), 0x1p-100f, 4) & hm) == 0ull) {   // (FCMP_OLT)
         const float y = rcp_refined(pr.w);
         outward = normal_div(rel, pr.w, y, normal_rn);
     } else {
