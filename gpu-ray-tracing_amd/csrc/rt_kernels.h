@@ -209,11 +209,13 @@ constexpr bool trace_ordered(int k) {
 // (rt_trace_kernel<4>; 8 ranks, 4 080 tiles: 3.08, four per tile pair 3.05, two per tile
 // 3.12); up to kQuad2MaxTiles four waves per pair of tiles (rt_tpair_kernel<4>; 3 ranks,
 // 10 800 tiles: 5.65 against 5.83 / 5.80 two per tile / pair; 4 ranks, 8 160 tiles: 4.61
-// against 4.72 / 5.04); above it two per pair (rt_tpair_kernel<2>; 2 ranks, 16 200 tiles:
-// 7.61 against 7.86 / 8.18; the whole image).  The tile-pair instances need candidate lists;
-// without them the same sizes run one tile per group.
+// against 4.72 / 5.04); above it two per pair (rt_tpair_kernel<2>; the whole image).  With
+// the tile pairs' accumulation split over their two tiles' waves (late round 6,
+// profiles/r06/r06bj/) four per pair also won at 2 ranks (16 320 tiles: 7.75-7.80 against
+// 8.04-8.13 two per pair), so the bound now covers 2 ranks (was 12 288).  The tile-pair
+// instances need candidate lists; without them the same sizes run one tile per group.
 constexpr uint64_t kQuadMaxTiles = 6144;
-constexpr uint64_t kQuad2MaxTiles = 12288;
+constexpr uint64_t kQuad2MaxTiles = 20000;
 // The seed-hash tables share one buffer: hash(x*73) for x < hy_offset(width), then
 // hash(y*51) per row (TraceParams::hy == hx + hy_offset(width)).
 constexpr uint32_t hy_offset(uint32_t width) { return (width + 63u) & ~63u; }

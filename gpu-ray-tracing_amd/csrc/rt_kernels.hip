@@ -2166,9 +2166,9 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
         }
     } else {
         const uint32_t spp = p.spp;                               // wgsl:343
-        // wave 0's accumulators stay in LDS between groups (no registers live across the
+        // the tiles' accumulators stay in LDS between groups (no registers live across the
         // samples; the foreign-count fallback above sets the register peak)
-        __shared__ float4 s_cols[2u * (Gu - 1u) * S * 64u];
+        __shared__ float4 s_cols[2u * Gu * S * 64u];
         __shared__ float4 s_acc[S * 64u];
         if (w == 0u)
 #pragma unroll
@@ -2222,16 +2222,21 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
                                            nullptr, col);
                 }
             }
-            // two LDS slots alternating by group (one barrier per group, as trace_pair); the
-            // colours as 12-B records (ds_write_b96: no register pair to fill with a zero)
-            float4* slot = s_cols + ((f / Gu) & 1u) * (Gu - 1u) * S * 64u;
-            if (w != 0u)
+            // two LDS slots alternating by group (one barrier per group, as trace_pair): wave w
+            // leaves its colour of tile t (frame f + w) in slot [w][t] unless it accumulates
+            // that tile itself; wave t (< S) accumulates tile t's G frames in frame order —
+            // the tiles' accumulation on two waves instead of all of it on wave 0.  The colours
+            // as 12-B records (ds_write_b96: no register quad to fill with a zero).
+            float4* slot = s_cols + ((f / Gu) & 1u) * Gu * S * 64u;
 #pragma unroll
-                for (uint32_t s = 0; s < S; ++s)
-                    *reinterpret_cast<f3v*>(&slot[((w - 1u) * S + s) * 64u + lane]) =
-                        f3v{col[s].x, col[s].y, col[s].z};
+            for (uint32_t t = 0; t < S; ++t)
+                if (w != t)
+                    *reinterpret_cast<f3v*>(&slot[(w * S + t) * 64u + lane]) =
+                        f3v{col[t].x, col[t].y, col[t].z};
             __syncthreads();
-            if (w == 0u) {
+#pragma unroll
+            for (uint32_t t = 0; t < S; ++t) {
+                if (w != t) continue;                             // (wave-uniform)
 #pragma unroll
                 for (uint32_t j = 0; j < Gu; ++j) {
                     const uint32_t fj = f + j;
@@ -2242,37 +2247,34 @@ __global__ __launch_bounds__(64 * G, RT_TPAIR_MIN_WAVES) void rt_tpair_kernel(
                     const float cnt = p.hint_cnt[fj];
                     float4* out = (fj & 1u) ? p.out2 : p.out;
                     const bool store = p.store_each == 2u || fj + 2u >= p.frames;
-#pragma unroll
-                    for (uint32_t s = 0; s < S; ++s) {
-                        const float4 ca = s_acc[s * 64u + lane];
-                        v3 cs = mk(ca.x, ca.y, ca.z);
-                        v3 cj = col[s];
-                        if (j != 0) {
-                            const float4 t = slot[((j - 1u) * S + s) * 64u + lane];
-                            cj = mk(t.x, t.y, t.z);
-                        }
-                        if (acc_frame) {
-                            const v3 num = sub(cj, cs);
-                            // num / f32(nb + 1) (wgsl:356) as a Markstein division (acc_rn)
-                            // (both conditions scalar, combined without a branch: a short-
-                            // circuit && here kept nb's test in a VGPR)
-                            const bool rn = (nb < kAccRnMax) &
-                                            ((mask_ult(acc_min_bits(num), kAccOkDbl) &
-                                              valid_m[s]) == 0ull);
-                            if (rn) {
-                                cs = acc_rn(cs, num, cnt, p.hint_rcp[fj]);
-                            } else {
-                                const float k = cnt;                 // wgsl:356
-                                cs = mk(cs.x + num.x / k, cs.y + num.y / k, cs.z + num.z / k);
-                            }
-                        }
-                        // (the alpha rides in the LDS copy: one register quad serves the LDS
-                        // write and the image store)
-                        const float4 v = make_float4(cs.x, cs.y, cs.z, cnt);
-                        s_acc[s * 64u + lane] = v;
-                        // wgsl:362-363: the images that survive (or every frame's)
-                        if (store && tc[s].valid) out[tc[s].idx] = v;
+                    const float4 ca = s_acc[t * 64u + lane];
+                    v3 cs = mk(ca.x, ca.y, ca.z);
+                    v3 cj = col[t];
+                    if (j != t) {
+                        const float4 c4 = slot[(j * S + t) * 64u + lane];
+                        cj = mk(c4.x, c4.y, c4.z);
                     }
+                    if (acc_frame) {
+                        const v3 num = sub(cj, cs);
+                        // num / f32(nb + 1) (wgsl:356) as a Markstein division (acc_rn)
+                        // (both conditions scalar, combined without a branch: a short-
+                        // circuit && here kept nb's test in a VGPR)
+                        const bool rn = (nb < kAccRnMax) &
+                                        ((mask_ult(acc_min_bits(num), kAccOkDbl) &
+                                          valid_m[t]) == 0ull);
+                        if (rn) {
+                            cs = acc_rn(cs, num, cnt, p.hint_rcp[fj]);
+                        } else {
+                            const float k = cnt;                     // wgsl:356
+                            cs = mk(cs.x + num.x / k, cs.y + num.y / k, cs.z + num.z / k);
+                        }
+                    }
+                    // (the alpha rides in the LDS copy: one register quad serves the LDS
+                    // write and the image store)
+                    const float4 v = make_float4(cs.x, cs.y, cs.z, cnt);
+                    s_acc[t * 64u + lane] = v;
+                    // wgsl:362-363: the images that survive (or every frame's)
+                    if (store && tc[t].valid) out[tc[t].idx] = v;
                 }
             }
         }
